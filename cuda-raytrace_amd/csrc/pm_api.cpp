@@ -1,0 +1,1004 @@
+/*
+ * pm_api.cpp — the C-ABI of libpmhip.so (declared in include/pm_api.h):
+ * context, scene flattening, BVH build + upload, stage orchestration and
+ * the whole-render entry point. Host code only; kernels live in
+ * pm_kernels.hip. No CPU fallback: every compute entry point launches HIP
+ * kernels and fails with PM_ERR_HIP when the device is unusable.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "pm_build.h"
+#include "pm_kernels.h"
+
+#pragma clang fp contract(off)
+
+using namespace pm;
+
+namespace {
+
+std::string g_last_error;
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= bytes && p) return hipSuccess;
+        if (p) { hipFree(p); p = nullptr; bytes = 0; }
+        if (n == 0) n = 16;
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    bool external = false; /* caller-owned memory: never freed or grown here */
+    void release() { if (p && !external) hipFree(p); p = nullptr; bytes = 0; external = false; }
+    template <class T> T *as() const { return (T *)p; }
+};
+
+struct HMesh { int material, light, has_n, has_uv; };
+struct HTri { int v[3]; int mesh; };
+struct Timer { hipEvent_t a = nullptr, b = nullptr; };
+struct TimerPool { std::vector<Timer> ev; size_t used = 0; };
+
+struct Ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    /* host scene */
+    std::vector<float4> materials;
+    std::vector<float> P, N, UV;
+    std::vector<HMesh> meshes;
+    std::vector<HTri> tris;
+    std::vector<float4> disks;   /* 5 per disk */
+    std::vector<float4> spheres; /* 4 per sphere */
+    std::vector<float> sphere_o2w;
+    std::vector<LightDev> lights;
+    int rand2d_total = 0;
+    int pinhole = 0, W = 0, H = 0;
+    float eye[3] = {0}, fwd[3] = {0}, right[3] = {0}, up[3] = {0};
+    std::vector<float> rays, rand2d;
+    int64_t nrays = 0;
+    int n2d = 0;
+    bool committed = false;
+    /* device scene */
+    DevBuf d_nodes, d_refs, d_tri_geo, d_tri_info, d_tri_id, d_verts, d_norms, d_uvs, d_meshes, d_disks,
+        d_spheres, d_materials, d_lights, d_rays, d_rand2d;
+    SceneDev S{};
+    float bbox_lo[3] = {0, 0, 0}, bbox_hi[3] = {0, 0, 0};
+    int bvh_depth = 0;
+    /* records */
+    DevBuf d_pos, d_nrm, d_state, d_n, d_dl;
+    int64_t nrec = 0;
+    /* slots */
+    DevBuf d_slots;
+    int64_t slots_used = 0;
+    /* photon buckets */
+    DevBuf d_keys, d_vals, d_keys2, d_vals2, d_cell_count, d_cell_start, d_nvalid, d_pha, d_phb, d_phc,
+        d_sort_tmp, d_scan_tmp;
+    GridDesc grid{};
+    int map_kind = -1;
+    int64_t map_slots = 0;
+    /* kd-tree */
+    DevBuf d_kd;
+    int64_t kd_count = 0;
+    /* misc */
+    DevBuf d_out, d_counters;
+    bool counting = false;
+    std::map<std::string, TimerPool> timers;
+};
+
+#define FAIL(c, code, ...)                                                     \
+    do {                                                                       \
+        char _b[512];                                                          \
+        snprintf(_b, sizeof(_b), __VA_ARGS__);                                 \
+        if (c) (c)->err = _b;                                                  \
+        g_last_error = _b;                                                     \
+        return code;                                                           \
+    } while (0)
+
+#define HIPCHK(c, expr)                                                                   \
+    do {                                                                                  \
+        hipError_t _e = (expr);                                                           \
+        if (_e != hipSuccess) FAIL(c, PM_ERR_HIP, "%s: %s", #expr, hipGetErrorString(_e)); \
+    } while (0)
+
+#define GETCTX(ptr)                                                  \
+    Ctx *c = (Ctx *)(ptr);                                           \
+    if (!c) FAIL((Ctx *)nullptr, PM_ERR_INVALID, "null context");    \
+    (void)hipSetDevice(c->device)
+
+hipStream_t pick(Ctx *c, void *s) { return s ? (hipStream_t)s : c->stream; }
+
+/* Every stage launch records a fresh event pair from a per-stage pool, on the
+ * stream the kernels run on; nothing synchronizes until a reader asks. */
+int timer_begin(Ctx *c, const char *name, hipStream_t s) {
+    TimerPool &tp = c->timers[name];
+    if (tp.used == tp.ev.size()) {
+        Timer t;
+        hipEventCreate(&t.a);
+        hipEventCreate(&t.b);
+        tp.ev.push_back(t);
+    }
+    hipEventRecord(tp.ev[tp.used].a, s);
+    return 0;
+}
+void timer_end(Ctx *c, const char *name, hipStream_t s) {
+    TimerPool &tp = c->timers[name];
+    hipEventRecord(tp.ev[tp.used].b, s);
+    tp.used++;
+}
+double pair_ms(const Timer &t) {
+    hipEventSynchronize(t.b);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, t.a, t.b) != hipSuccess) return -1.0;
+    return ms;
+}
+/* duration of the most recent launch of a stage */
+double timer_ms(Ctx *c, const char *name) {
+    auto it = c->timers.find(name);
+    if (it == c->timers.end() || it->second.used == 0) return -1.0;
+    return pair_ms(it->second.ev[it->second.used - 1]);
+}
+
+inline float4 f4(float x, float y, float z, float w) { return make_float4(x, y, z, w); }
+inline float ibits(int v) { float f; std::memcpy(&f, &v, 4); return f; }
+inline int fbits_h(float f) { int v; std::memcpy(&v, &f, 4); return v; }
+
+int64_t num_records(const Ctx *c) {
+    if (c->pinhole) return (int64_t)((c->W + 7) / 8) * ((c->H + 7) / 8) * 64;
+    return c->nrays;
+}
+
+/* pbrt-v2 PermutedHalton(5, RNG(seed)) table (montecarlo.h GeneratePermutation
+ * + Shuffle over MT19937 == std::mt19937; photonmappingrenderer.cpp:216). */
+void halton_perm(uint32_t seed, uint32_t out[28]) {
+    std::mt19937 rng(seed);
+    const uint32_t primes[5] = {2, 3, 5, 7, 11};
+    uint32_t *p = out;
+    for (int d = 0; d < 5; ++d) {
+        uint32_t b = primes[d];
+        for (uint32_t i = 0; i < b; ++i) p[i] = i;
+        for (uint32_t i = 0; i < b; ++i) {
+            uint32_t other = i + ((uint32_t)rng() % (b - i));
+            std::swap(p[i], p[other]);
+        }
+        p += b;
+    }
+}
+
+template <class T>
+int upload(Ctx *c, DevBuf &b, const std::vector<T> &v) {
+    HIPCHK(c, b.ensure(std::max<size_t>(v.size() * sizeof(T), 16)));
+    if (!v.empty()) HIPCHK(c, hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return PM_OK;
+}
+
+int ensure_records(Ctx *c) {
+    int64_t n = num_records(c);
+    if (n <= 0) FAIL(c, PM_ERR_INVALID, "no eye samples (call pm_set_pinhole or pm_set_eye_rays)");
+    HIPCHK(c, c->d_pos.ensure(n * sizeof(float4)));
+    HIPCHK(c, c->d_nrm.ensure(n * sizeof(float4)));
+    HIPCHK(c, c->d_state.ensure(n * sizeof(float4)));
+    HIPCHK(c, c->d_n.ensure(n * sizeof(float)));
+    HIPCHK(c, c->d_dl.ensure(n * sizeof(float4)));
+    c->nrec = n;
+    return PM_OK;
+}
+
+RecordsDev recs(Ctx *c) {
+    RecordsDev R;
+    R.pos = c->d_pos.as<float4>(); R.nrm = c->d_nrm.as<float4>(); R.state = c->d_state.as<float4>();
+    R.n = c->d_n.as<float>(); R.dl = c->d_dl.as<float4>(); R.count = c->nrec;
+    return R;
+}
+
+GatherParams gather_params(Ctx *c, const pm_render_params *p) {
+    GatherParams G{};
+    G.R = recs(c);
+    G.materials = c->d_materials.as<float4>();
+    G.ppm_alpha = p->ppm_alpha;
+    G.grid = c->grid;
+    G.cell_start = c->d_cell_start.as<uint32_t>();
+    G.ph_a = c->d_pha.as<float4>(); G.ph_b = c->d_phb.as<float4>(); G.ph_c = c->d_phc.as<float>();
+    G.kd_nodes = c->d_kd.as<pm_photon>(); G.kd_count = c->kd_count;
+    G.counters = c->d_counters.as<unsigned long long>();
+    return G;
+}
+
+int check_params(Ctx *c, const pm_render_params *p) {
+    if (!p) FAIL(c, PM_ERR_INVALID, "null params");
+    if (!c->committed) FAIL(c, PM_ERR_INVALID, "scene not committed (call pm_commit)");
+    if (p->max_photon_count < 1 || p->max_photon_count > 64) FAIL(c, PM_ERR_INVALID, "max_photon_count out of range");
+    if (p->light_source_index < 0 || p->light_source_index >= (int)c->lights.size())
+        FAIL(c, PM_ERR_INVALID, "light_source_index %d out of range (%zu lights)", p->light_source_index,
+             c->lights.size());
+    if (!(p->initial_radius2 > 0.f)) FAIL(c, PM_ERR_INVALID, "initial_radius2 must be > 0");
+    return PM_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+const char *pm_version(void) { return "pmhip 0.1 (gfx950)"; }
+
+void pm_default_params(pm_render_params *p) {
+    std::memset(p, 0, sizeof(*p));
+    p->scene_epsilon = 0.1f;
+    p->initial_radius2 = 4.0f;
+    p->ppm_alpha = 0.7f;
+    p->max_photon_count = 4;
+    p->paths_per_pass = 512 * 512;
+    p->passes = 1;
+    p->light_source_index = 0;
+    p->max_specular_depth = 10;
+    p->rng_seed = 777u;
+    p->light_rng_seed = 2047u;
+    p->gather_structure = PM_GATHER_GRID;
+}
+
+int pm_create(void **out, const pm_config *cfg) {
+    if (!out) FAIL((Ctx *)nullptr, PM_ERR_INVALID, "null output pointer");
+    *out = nullptr;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0)
+        FAIL((Ctx *)nullptr, PM_ERR_HIP, "no HIP device available (%s)", hipGetErrorString(e));
+    int dev = cfg ? cfg->device : 0;
+    if (dev < 0 || dev >= ndev) FAIL((Ctx *)nullptr, PM_ERR_INVALID, "device %d out of range (%d devices)", dev, ndev);
+    Ctx *c = new Ctx();
+    c->device = dev;
+    hipSetDevice(dev);
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        FAIL((Ctx *)nullptr, PM_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    e = c->d_counters.ensure(4 * sizeof(unsigned long long));
+    if (e != hipSuccess) {
+        delete c;
+        FAIL((Ctx *)nullptr, PM_ERR_HIP, "hipMalloc: %s", hipGetErrorString(e));
+    }
+    *out = c;
+    return PM_OK;
+}
+
+void pm_destroy(void *ptr) {
+    Ctx *c = (Ctx *)ptr;
+    if (!c) return;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    for (auto &kv : c->timers)
+        for (Timer &t : kv.second.ev) {
+            hipEventDestroy(t.a);
+            hipEventDestroy(t.b);
+        }
+    DevBuf *bufs[] = {&c->d_nodes, &c->d_refs, &c->d_tri_geo, &c->d_tri_info, &c->d_tri_id, &c->d_verts,
+                      &c->d_norms, &c->d_uvs, &c->d_meshes, &c->d_disks, &c->d_spheres, &c->d_materials,
+                      &c->d_lights, &c->d_rays, &c->d_rand2d, &c->d_pos, &c->d_nrm, &c->d_state, &c->d_n,
+                      &c->d_dl, &c->d_slots, &c->d_keys, &c->d_vals, &c->d_keys2, &c->d_vals2,
+                      &c->d_cell_count, &c->d_cell_start, &c->d_nvalid, &c->d_pha, &c->d_phb, &c->d_phc,
+                      &c->d_sort_tmp, &c->d_scan_tmp, &c->d_kd, &c->d_out, &c->d_counters};
+    for (DevBuf *b : bufs) b->release();
+    hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char *pm_last_error(void *ptr) {
+    Ctx *c = (Ctx *)ptr;
+    return c ? c->err.c_str() : g_last_error.c_str();
+}
+
+int64_t pm_kdtree_build_host(const pm_photon *slots, int64_t nslots, pm_photon *nodes_out) {
+    if (!slots || !nodes_out || nslots < 0) return -1;
+    std::vector<pm_photon> nodes;
+    int64_t m = build_kdtree_pbrt(slots, nslots, nodes);
+    if (m > 0) std::memcpy(nodes_out, nodes.data(), (size_t)m * sizeof(pm_photon));
+    return m;
+}
+
+int pm_halton_permutation(uint32_t seed, uint32_t out[28]) {
+    if (!out) return PM_ERR_INVALID;
+    halton_perm(seed, out);
+    return PM_OK;
+}
+
+/* ------------------------------------------------------------------ scene */
+int pm_add_material(void *ptr, int type, const float rgb[3], int *out_id) {
+    GETCTX(ptr);
+    if (type != PM_MATTE && type != PM_MIRROR && type != PM_GLASS) FAIL(c, PM_ERR_INVALID, "bad material type %d", type);
+    float r = rgb ? rgb[0] : 0.f, g = rgb ? rgb[1] : 0.f, b = rgb ? rgb[2] : 0.f;
+    c->materials.push_back(f4(r, g, b, ibits(type)));
+    if (out_id) *out_id = (int)c->materials.size() - 1;
+    c->committed = false;
+    return PM_OK;
+}
+
+int pm_add_trimesh(void *ptr, const float *P, int nverts, const int *idx, int ntris, const float *N, const float *uv,
+                   int material, int light) {
+    GETCTX(ptr);
+    if (!P || !idx || nverts <= 0 || ntris <= 0) FAIL(c, PM_ERR_INVALID, "empty or null mesh");
+    if (material < 0 || material >= (int)c->materials.size()) FAIL(c, PM_ERR_INVALID, "bad material id %d", material);
+    for (int64_t i = 0; i < 3 * (int64_t)ntris; ++i)
+        if (idx[i] < 0 || idx[i] >= nverts) FAIL(c, PM_ERR_INVALID, "vertex index %d out of range", idx[i]);
+    int64_t base = (int64_t)c->P.size() / 3;
+    c->P.insert(c->P.end(), P, P + 3 * (size_t)nverts);
+    if (N) c->N.insert(c->N.end(), N, N + 3 * (size_t)nverts);
+    else c->N.insert(c->N.end(), 3 * (size_t)nverts, 0.f);
+    if (uv) c->UV.insert(c->UV.end(), uv, uv + 2 * (size_t)nverts);
+    else c->UV.insert(c->UV.end(), 2 * (size_t)nverts, 0.f);
+    int mid = (int)c->meshes.size();
+    c->meshes.push_back(HMesh{material, light, N != nullptr, uv != nullptr});
+    for (int t = 0; t < ntris; ++t)
+        c->tris.push_back(HTri{{(int)(base + idx[3 * t]), (int)(base + idx[3 * t + 1]), (int)(base + idx[3 * t + 2])}, mid});
+    c->committed = false;
+    return PM_OK;
+}
+
+int pm_add_sphere(void *ptr, float radius, const float o2w[16], const float w2o[16], int material, int light) {
+    GETCTX(ptr);
+    if (!o2w || !w2o || !(radius > 0.f)) FAIL(c, PM_ERR_INVALID, "bad sphere");
+    if (material < 0 || material >= (int)c->materials.size()) FAIL(c, PM_ERR_INVALID, "bad material id %d", material);
+    c->spheres.push_back(f4(w2o[0], w2o[1], w2o[2], w2o[3]));
+    c->spheres.push_back(f4(w2o[4], w2o[5], w2o[6], w2o[7]));
+    c->spheres.push_back(f4(w2o[8], w2o[9], w2o[10], w2o[11]));
+    c->spheres.push_back(f4(radius, ibits(material), ibits(light), ibits(0)));
+    c->sphere_o2w.insert(c->sphere_o2w.end(), o2w, o2w + 16);
+    c->committed = false;
+    return PM_OK;
+}
+
+/* derived uniforms as cudadisk.cpp:24-43 computes them */
+int pm_add_disk(void *ptr, const float o[3], const float x[3], const float y[3], const float z[3], float inner,
+                float phimax, int material, int light) {
+    GETCTX(ptr);
+    if (!o || !x || !y || !z) FAIL(c, PM_ERR_INVALID, "null disk vector");
+    if (material < 0 || material >= (int)c->materials.size()) FAIL(c, PM_ERR_INVALID, "bad material id %d", material);
+    float inv_rx2 = 1.f / (x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+    float inv_ry2 = 1.f / (y[0] * y[0] + y[1] * y[1] + y[2] * y[2]);
+    float moffset = o[0] * z[0] + o[1] * z[1] + o[2] * z[2];
+    c->disks.push_back(f4(o[0], o[1], o[2], inner));
+    c->disks.push_back(f4(x[0], x[1], x[2], phimax));
+    c->disks.push_back(f4(y[0], y[1], y[2], moffset));
+    c->disks.push_back(f4(z[0], z[1], z[2], inv_rx2));
+    c->disks.push_back(f4(inv_ry2, ibits(material), ibits(light), ibits(0)));
+    c->committed = false;
+    return PM_OK;
+}
+
+int pm_add_light_point(void *ptr, const float pos[3], const float I[3]) {
+    GETCTX(ptr);
+    if (!pos || !I) FAIL(c, PM_ERR_INVALID, "null point light");
+    LightDev L{};
+    L.o_type = f4(pos[0], pos[1], pos[2], ibits(PM_LIGHT_POINT));
+    L.p1_ns = f4(0, 0, 0, ibits(1)); /* nSample = 1, cudalight.cpp:22 */
+    L.p2_r2d = f4(0, 0, 0, ibits(0));
+    L.n_area = f4(0, 0, 0, 0);
+    L.le = f4(I[0], I[1], I[2], 0);
+    c->lights.push_back(L);
+    c->committed = false;
+    return PM_OK;
+}
+
+int pm_add_light_disk(void *ptr, const float o[3], const float p1[3], const float p2[3], const float n[3],
+                      const float Le[3], float area, int nsamples) {
+    GETCTX(ptr);
+    if (!o || !p1 || !p2 || !n || !Le) FAIL(c, PM_ERR_INVALID, "null disk light vector");
+    int ns = std::max(1, nsamples);
+    LightDev L{};
+    L.o_type = f4(o[0], o[1], o[2], ibits(PM_LIGHT_AREA_DISK));
+    L.p1_ns = f4(p1[0], p1[1], p1[2], ibits(ns));
+    L.p2_r2d = f4(p2[0], p2[1], p2[2], ibits(c->rand2d_total)); /* CudaSample::Add2D offset */
+    L.n_area = f4(n[0], n[1], n[2], area);
+    L.le = f4(Le[0], Le[1], Le[2], 0);
+    c->rand2d_total += ns;
+    c->lights.push_back(L);
+    c->committed = false;
+    return PM_OK;
+}
+
+int pm_set_pinhole(void *ptr, const float eye[3], const float fwd[3], const float right[3], const float up[3], int W,
+                   int H) {
+    GETCTX(ptr);
+    if (W <= 0 || H <= 0 || !eye || !fwd || !right || !up) FAIL(c, PM_ERR_INVALID, "bad pinhole camera");
+    c->pinhole = 1; c->W = W; c->H = H;
+    std::memcpy(c->eye, eye, 12); std::memcpy(c->fwd, fwd, 12);
+    std::memcpy(c->right, right, 12); std::memcpy(c->up, up, 12);
+    return PM_OK;
+}
+
+int pm_set_eye_rays(void *ptr, const float *rays, int64_t nrays, const float *rand2d, int n2d) {
+    GETCTX(ptr);
+    if (!rays || nrays <= 0) FAIL(c, PM_ERR_INVALID, "no rays");
+    c->pinhole = 0;
+    c->nrays = nrays;
+    c->rays.assign(rays, rays + 6 * nrays);
+    c->n2d = (rand2d && n2d > 0) ? n2d : 0;
+    if (c->n2d) c->rand2d.assign(rand2d, rand2d + (size_t)2 * n2d * nrays);
+    else c->rand2d.clear();
+    HIPCHK(c, c->d_rays.ensure(c->rays.size() * sizeof(float)));
+    HIPCHK(c, hipMemcpy(c->d_rays.p, c->rays.data(), c->rays.size() * sizeof(float), hipMemcpyHostToDevice));
+    if (c->n2d) {
+        HIPCHK(c, c->d_rand2d.ensure(c->rand2d.size() * sizeof(float)));
+        HIPCHK(c, hipMemcpy(c->d_rand2d.p, c->rand2d.data(), c->rand2d.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
+    return PM_OK;
+}
+
+int pm_commit(void *ptr) {
+    GETCTX(ptr);
+    if (c->lights.empty()) FAIL(c, PM_ERR_INVALID, "scene has no lights");
+    const int64_t nt = (int64_t)c->tris.size(), nd = (int64_t)c->disks.size() / 5,
+                  ns = (int64_t)c->spheres.size() / 4;
+    if (nt + nd + ns == 0) FAIL(c, PM_ERR_INVALID, "scene has no shapes");
+    if (nt >= (1 << 30) || nd >= (1 << 30) || ns >= (1 << 30)) FAIL(c, PM_ERR_INVALID, "too many primitives");
+    /* global ids: triangles, then disks, then spheres (tie-break order) */
+    for (int64_t i = 0; i < nd; ++i) c->disks[5 * i + 4].w = ibits((int)(nt + i));
+    for (int64_t i = 0; i < ns; ++i) c->spheres[4 * i + 3].w = ibits((int)(nt + nd + i));
+
+    std::vector<BuildPrim> prims;
+    prims.reserve(nt + nd + ns);
+    float blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    auto add_box = [&](float lo[3], float hi[3], uint32_t ref) {
+        BuildPrim bp;
+        for (int a = 0; a < 3; ++a) {
+            blo[a] = std::min(blo[a], lo[a]); bhi[a] = std::max(bhi[a], hi[a]);
+            float pad = 1e-4f * std::max(1.0f, std::max(fabsf(lo[a]), fabsf(hi[a])));
+            bp.lo[a] = lo[a] - pad; bp.hi[a] = hi[a] + pad;
+        }
+        bp.ref = ref;
+        prims.push_back(bp);
+    };
+    const float *V = c->P.data();
+    for (int64_t t = 0; t < nt; ++t) {
+        const HTri &tr = c->tris[t];
+        float lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) {
+            float v0 = V[3 * tr.v[0] + a], v1 = V[3 * tr.v[1] + a], v2 = V[3 * tr.v[2] + a];
+            lo[a] = std::min(v0, std::min(v1, v2)); hi[a] = std::max(v0, std::max(v1, v2));
+        }
+        add_box(lo, hi, (PRIM_TRI << 30) | (uint32_t)t);
+    }
+    for (int64_t i = 0; i < nd; ++i) {
+        const float4 *d = &c->disks[5 * i];
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int sx = -1; sx <= 1; sx += 2)
+            for (int sy = -1; sy <= 1; sy += 2) { /* cudadisk.cu:87-96 */
+                float p[3] = {d[0].x + sx * d[1].x + sy * d[2].x, d[0].y + sx * d[1].y + sy * d[2].y,
+                              d[0].z + sx * d[1].z + sy * d[2].z};
+                for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], p[a]); hi[a] = std::max(hi[a], p[a]); }
+            }
+        add_box(lo, hi, (PRIM_DISK << 30) | (uint32_t)i);
+    }
+    for (int64_t i = 0; i < ns; ++i) {
+        const float *m = &c->sphere_o2w[16 * i];
+        float r = c->spheres[4 * i + 3].x;
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int k = 0; k < 8; ++k) {
+            float x = (k & 1) ? r : -r, y = (k & 2) ? r : -r, z = (k & 4) ? r : -r;
+            float w[3] = {m[0] * x + m[1] * y + m[2] * z + m[3], m[4] * x + m[5] * y + m[6] * z + m[7],
+                          m[8] * x + m[9] * y + m[10] * z + m[11]};
+            for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], w[a]); hi[a] = std::max(hi[a], w[a]); }
+        }
+        add_box(lo, hi, (PRIM_SPHERE << 30) | (uint32_t)i);
+    }
+    BvhOut bvh;
+    build_bvh(prims, BVH_STACK - 2, bvh);
+    c->bvh_depth = bvh.depth;
+    if (bvh.depth >= BVH_STACK) FAIL(c, PM_ERR_INVALID, "BVH too deep (%d)", bvh.depth);
+
+    /* triangles in leaf order; per-triangle precomputed (p0, e0, e1, n) */
+    std::vector<float4> tri_geo;
+    std::vector<int4> tri_info;
+    std::vector<uint32_t> tri_id;
+    tri_geo.reserve(3 * nt); tri_info.reserve(nt); tri_id.reserve(nt);
+    for (uint32_t &ref : bvh.refs) {
+        if ((ref >> 30) != PRIM_TRI) continue;
+        uint32_t t = ref & 0x3fffffffu;
+        const HTri &tr = c->tris[t];
+        const float *p0 = V + 3 * tr.v[0], *p1 = V + 3 * tr.v[1], *p2 = V + 3 * tr.v[2];
+        float e0[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
+        float e1[3] = {p0[0] - p2[0], p0[1] - p2[1], p0[2] - p2[2]};
+        float n[3] = {e1[1] * e0[2] - e1[2] * e0[1], e1[2] * e0[0] - e1[0] * e0[2], e1[0] * e0[1] - e1[1] * e0[0]};
+        uint32_t k = (uint32_t)tri_info.size();
+        tri_geo.push_back(f4(p0[0], p0[1], p0[2], e0[0]));
+        tri_geo.push_back(f4(e0[1], e0[2], e1[0], e1[1]));
+        tri_geo.push_back(f4(e1[2], n[0], n[1], n[2]));
+        tri_info.push_back(make_int4(tr.v[0], tr.v[1], tr.v[2], tr.mesh));
+        tri_id.push_back(t);
+        ref = (PRIM_TRI << 30) | k;
+    }
+    std::vector<float4> verts(c->P.size() / 3), norms(c->P.size() / 3);
+    std::vector<float2> uvs(c->P.size() / 3);
+    for (size_t i = 0; i < verts.size(); ++i) {
+        verts[i] = f4(c->P[3 * i], c->P[3 * i + 1], c->P[3 * i + 2], 0.f);
+        norms[i] = f4(c->N[3 * i], c->N[3 * i + 1], c->N[3 * i + 2], 0.f);
+        uvs[i] = make_float2(c->UV[2 * i], c->UV[2 * i + 1]);
+    }
+    std::vector<int4> meshes;
+    for (auto &m : c->meshes) meshes.push_back(make_int4(m.material, m.light, m.has_n, m.has_uv));
+    std::vector<float4> nodes4(bvh.nodes.size() / 4);
+    std::memcpy(nodes4.data(), bvh.nodes.data(), bvh.nodes.size() * sizeof(float));
+
+    int rc;
+    if ((rc = upload(c, c->d_nodes, nodes4))) return rc;
+    if ((rc = upload(c, c->d_refs, bvh.refs))) return rc;
+    if ((rc = upload(c, c->d_tri_geo, tri_geo))) return rc;
+    if ((rc = upload(c, c->d_tri_info, tri_info))) return rc;
+    if ((rc = upload(c, c->d_tri_id, tri_id))) return rc;
+    if ((rc = upload(c, c->d_verts, verts))) return rc;
+    if ((rc = upload(c, c->d_norms, norms))) return rc;
+    if ((rc = upload(c, c->d_uvs, uvs))) return rc;
+    if ((rc = upload(c, c->d_meshes, meshes))) return rc;
+    if ((rc = upload(c, c->d_disks, c->disks))) return rc;
+    if ((rc = upload(c, c->d_spheres, c->spheres))) return rc;
+    if ((rc = upload(c, c->d_materials, c->materials))) return rc;
+    if ((rc = upload(c, c->d_lights, c->lights))) return rc;
+
+    SceneDev &S = c->S;
+    S.nodes = c->d_nodes.as<float4>(); S.refs = c->d_refs.as<uint32_t>();
+    S.tri_geo = c->d_tri_geo.as<float4>(); S.tri_info = c->d_tri_info.as<int4>(); S.tri_id = c->d_tri_id.as<uint32_t>();
+    S.verts = c->d_verts.as<float4>(); S.norms = c->d_norms.as<float4>(); S.uvs = c->d_uvs.as<float2>();
+    S.meshes = c->d_meshes.as<int4>(); S.disks = c->d_disks.as<float4>(); S.spheres = c->d_spheres.as<float4>();
+    S.materials = c->d_materials.as<float4>(); S.lights = c->d_lights.as<LightDev>();
+    S.n_lights = (int)c->lights.size(); S.n_nodes = (int)nodes4.size() / 4;
+    for (int a = 0; a < 3; ++a) { c->bbox_lo[a] = blo[a]; c->bbox_hi[a] = bhi[a]; }
+    c->committed = true;
+    return PM_OK;
+}
+
+/* ------------------------------------------------------------- stages */
+int pm_eye_pass(void *ptr, const pm_render_params *p, void *stream) {
+    GETCTX(ptr);
+    int rc;
+    if ((rc = check_params(c, p))) return rc;
+    if ((rc = ensure_records(c))) return rc;
+    if (!c->pinhole && c->rand2d_total > c->n2d)
+        FAIL(c, PM_ERR_INVALID, "eye rays carry %d 2D samples, lights need %d", c->n2d, c->rand2d_total);
+    hipStream_t s = pick(c, stream);
+    EyeParams E{};
+    E.S = c->S;
+    E.R = recs(c);
+    E.pinhole = c->pinhole; E.W = c->W; E.H = c->H; E.n2d = c->n2d;
+    E.eye = f4(c->eye[0], c->eye[1], c->eye[2], 0); E.fwd = f4(c->fwd[0], c->fwd[1], c->fwd[2], 0);
+    E.right = f4(c->right[0], c->right[1], c->right[2], 0); E.up = f4(c->up[0], c->up[1], c->up[2], 0);
+    E.rays = c->d_rays.as<float>(); E.rand2d = c->d_rand2d.as<float>();
+    E.eps = p->scene_epsilon; E.r2init = p->initial_radius2; E.max_spec = p->max_specular_depth;
+    E.light_seed = p->light_rng_seed;
+    timer_begin(c, "eye", s);
+    HIPCHK(c, launch_eye(E, s));
+    timer_end(c, "eye", s);
+    return PM_OK;
+}
+
+int pm_reserve_slots(void *ptr, int64_t n, void **d_slots) {
+    GETCTX(ptr);
+    if (n < 0) FAIL(c, PM_ERR_INVALID, "negative slot count");
+    if ((size_t)n * sizeof(pm_photon) > c->d_slots.bytes) {
+        if (c->d_slots.external)
+            FAIL(c, PM_ERR_INVALID, "external slot buffer holds %zu slots, %lld needed",
+                 c->d_slots.bytes / sizeof(pm_photon), (long long)n);
+        /* keep the contents: grow by copy */
+        DevBuf nb;
+        HIPCHK(c, nb.ensure((size_t)n * sizeof(pm_photon)));
+        if (c->d_slots.p) {
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            HIPCHK(c, hipMemcpy(nb.p, c->d_slots.p, c->d_slots.bytes, hipMemcpyDeviceToDevice));
+            c->d_slots.release();
+        }
+        c->d_slots = nb;
+        nb.p = nullptr;
+    }
+    if (d_slots) *d_slots = c->d_slots.p;
+    return PM_OK;
+}
+
+int pm_set_slot_buffer(void *ptr, void *d, int64_t n) {
+    GETCTX(ptr);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->d_slots.release();
+    if (d) {
+        if (n <= 0) FAIL(c, PM_ERR_INVALID, "external slot buffer needs n_slots > 0");
+        c->d_slots.p = d;
+        c->d_slots.bytes = (size_t)n * sizeof(pm_photon);
+        c->d_slots.external = true;
+    }
+    c->slots_used = 0;
+    return PM_OK;
+}
+
+int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t path_begin, int64_t path_count,
+                     int64_t slot_path_base, void *stream) {
+    GETCTX(ptr);
+    int rc;
+    if ((rc = check_params(c, p))) return rc;
+    if (path_count < 0 || path_begin < slot_path_base) FAIL(c, PM_ERR_INVALID, "bad path range");
+    if ((uint64_t)(path_begin + path_count) * (uint64_t)p->max_photon_count > 0xffffffffull)
+        FAIL(c, PM_ERR_INVALID, "photon slot index exceeds 32 bits (reference pm_index is a uint)");
+    const int64_t mpc = p->max_photon_count;
+    const int64_t end_slot = (path_begin + path_count - slot_path_base) * mpc;
+    if ((rc = pm_reserve_slots(c, end_slot, nullptr))) return rc;
+    hipStream_t s = pick(c, stream);
+    TraceParams T{};
+    T.S = c->S;
+    T.slots = c->d_slots.as<pm_photon>();
+    halton_perm((uint32_t)pass, T.perm);
+    T.path_begin = path_begin; T.path_count = path_count; T.slot_path_base = slot_path_base;
+    T.pass = pass; T.mpc = (int)mpc; T.max_spec = p->max_specular_depth; T.light_index = p->light_source_index;
+    T.eps = p->scene_epsilon; T.seed = p->rng_seed;
+    timer_begin(c, "trace", s);
+    /* invalid = zero (build divergence: the reference leaves early-return slots stale) */
+    HIPCHK(c, hipMemsetAsync(c->d_slots.as<pm_photon>() + (path_begin - slot_path_base) * mpc, 0,
+                             (size_t)(path_count * mpc) * sizeof(pm_photon), s));
+    HIPCHK(c, launch_trace(T, s));
+    timer_end(c, "trace", s);
+    c->slots_used = std::max(c->slots_used, end_slot);
+    return PM_OK;
+}
+
+int pm_build_photon_map(void *ptr, const pm_render_params *p, int64_t n_slots, void *stream) {
+    GETCTX(ptr);
+    int rc;
+    if ((rc = check_params(c, p))) return rc;
+    if (n_slots <= 0) n_slots = c->slots_used;
+    if ((size_t)n_slots * sizeof(pm_photon) > c->d_slots.bytes) FAIL(c, PM_ERR_INVALID, "n_slots beyond slot buffer");
+    hipStream_t s = pick(c, stream);
+    c->map_slots = n_slots;
+    if (p->gather_structure == PM_GATHER_KDTREE) {
+        /* reference path (CreatePhotonMap): DtoH, CPU pbrt KdTree, HtoD */
+        timer_begin(c, "build", s);
+        std::vector<pm_photon> h((size_t)n_slots), nodes;
+        HIPCHK(c, hipMemcpyAsync(h.data(), c->d_slots.p, n_slots * sizeof(pm_photon), hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        int64_t m = build_kdtree_pbrt(h.data(), n_slots, nodes);
+        c->kd_count = m;
+        if (m > 0) {
+            HIPCHK(c, c->d_kd.ensure(m * sizeof(pm_photon)));
+            HIPCHK(c, hipMemcpyAsync(c->d_kd.p, nodes.data(), m * sizeof(pm_photon), hipMemcpyHostToDevice, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+        }
+        timer_end(c, "build", s);
+        c->map_kind = PM_GATHER_KDTREE;
+        if (m == 0) FAIL(c, PM_ERR_NO_PHOTONS, "0 valid photons");
+        return PM_OK;
+    }
+    /* photon buckets: cell size >= 2 r_max (PPM radii only shrink) */
+    GridDesc &g = c->grid;
+    const float rq = sqrtf(p->initial_radius2) * 1.0001f + 1e-4f;
+    float cs = 2.0f * rq * 1.001f;
+    float ext[3];
+    for (int a = 0; a < 3; ++a) ext[a] = std::max(c->bbox_hi[a] - c->bbox_lo[a], 1e-3f);
+    int64_t dims[3];
+    while (true) {
+        for (int a = 0; a < 3; ++a) dims[a] = std::max<int64_t>(1, (int64_t)std::ceil(ext[a] / cs) + 1);
+        if (dims[0] * dims[1] * dims[2] <= (int64_t)1 << 26) break;
+        cs *= 1.25f;
+    }
+    g.gx = c->bbox_lo[0]; g.gy = c->bbox_lo[1]; g.gz = c->bbox_lo[2];
+    g.inv_cs = 1.0f / cs;
+    g.dx = (int)dims[0]; g.dy = (int)dims[1]; g.dz = (int)dims[2];
+    g.ncells = (uint32_t)(dims[0] * dims[1] * dims[2]);
+    int end_bit = 1;
+    while (end_bit < 32 && ((uint64_t)1 << end_bit) <= g.ncells) ++end_bit;
+    const size_t n = (size_t)n_slots;
+    HIPCHK(c, c->d_keys.ensure(n * 4)); HIPCHK(c, c->d_vals.ensure(n * 4));
+    HIPCHK(c, c->d_keys2.ensure(n * 4)); HIPCHK(c, c->d_vals2.ensure(n * 4));
+    HIPCHK(c, c->d_cell_count.ensure(((size_t)g.ncells + 1) * 4));
+    HIPCHK(c, c->d_cell_start.ensure(((size_t)g.ncells + 1) * 4));
+    HIPCHK(c, c->d_nvalid.ensure(16));
+    HIPCHK(c, c->d_pha.ensure(n * 16)); HIPCHK(c, c->d_phb.ensure(n * 16)); HIPCHK(c, c->d_phc.ensure(n * 4));
+    size_t sort_b = grid_sort_temp_bytes((int64_t)n, g.ncells), scan_b = grid_scan_temp_bytes(g.ncells);
+    HIPCHK(c, c->d_sort_tmp.ensure(sort_b)); HIPCHK(c, c->d_scan_tmp.ensure(scan_b));
+    timer_begin(c, "build", s);
+    HIPCHK(c, hipMemsetAsync(c->d_cell_count.p, 0, ((size_t)g.ncells + 1) * 4, s));
+    HIPCHK(c, hipMemsetAsync(c->d_nvalid.p, 0, 4, s));
+    HIPCHK(c, launch_grid_keys(c->d_slots.as<pm_photon>(), n_slots, g, c->d_keys.as<uint32_t>(), c->d_vals.as<uint32_t>(),
+                               c->d_cell_count.as<uint32_t>(), c->d_nvalid.as<uint32_t>(), s));
+    HIPCHK(c, launch_grid_sort(c->d_sort_tmp.p, c->d_sort_tmp.bytes, c->d_keys.as<uint32_t>(), c->d_keys2.as<uint32_t>(),
+                               c->d_vals.as<uint32_t>(), c->d_vals2.as<uint32_t>(), n_slots, end_bit, s));
+    HIPCHK(c, launch_grid_scan(c->d_scan_tmp.p, c->d_scan_tmp.bytes, c->d_cell_count.as<uint32_t>(),
+                               c->d_cell_start.as<uint32_t>(), g.ncells, s));
+    HIPCHK(c, launch_grid_scatter(c->d_slots.as<pm_photon>(), c->d_vals2.as<uint32_t>(), c->d_nvalid.as<uint32_t>(),
+                                  n_slots, c->d_pha.as<float4>(), c->d_phb.as<float4>(), c->d_phc.as<float>(), s));
+    timer_end(c, "build", s);
+    c->map_kind = PM_GATHER_GRID;
+    return PM_OK;
+}
+
+static int gather_common(Ctx *c, const pm_render_params *p, float4 *partial, int64_t rec_begin, int64_t rec_count,
+                         void *stream) {
+    int rc;
+    if ((rc = check_params(c, p))) return rc;
+    if (c->nrec <= 0) FAIL(c, PM_ERR_INVALID, "no records (run pm_eye_pass first)");
+    if (c->map_kind != p->gather_structure) FAIL(c, PM_ERR_INVALID, "photon map not built for this gather structure");
+    if (rec_begin < 0 || rec_count < 0 || rec_begin + rec_count > c->nrec) FAIL(c, PM_ERR_INVALID, "bad record range");
+    hipStream_t s = pick(c, stream);
+    GatherParams G = gather_params(c, p);
+    G.partial = partial;
+    G.rec_begin = rec_begin;
+    G.rec_end = rec_begin + rec_count;
+    if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters.p, 0, 32, s));
+    timer_begin(c, "gather", s);
+    HIPCHK(c, launch_gather(G, p->gather_structure, partial != nullptr, c->counting, s));
+    timer_end(c, "gather", s);
+    return PM_OK;
+}
+
+int pm_gather(void *ptr, const pm_render_params *p, void *stream) {
+    GETCTX(ptr);
+    return gather_common(c, p, nullptr, 0, c->nrec, stream);
+}
+
+int pm_gather_range(void *ptr, const pm_render_params *p, int64_t rec_begin, int64_t rec_count, void *stream) {
+    GETCTX(ptr);
+    return gather_common(c, p, nullptr, rec_begin, rec_count, stream);
+}
+
+int pm_gather_partial(void *ptr, const pm_render_params *p, void *d_partial, void *stream) {
+    GETCTX(ptr);
+    if (!d_partial) FAIL(c, PM_ERR_INVALID, "null partial buffer");
+    return gather_common(c, p, (float4 *)d_partial, 0, c->nrec, stream);
+}
+
+int pm_ppm_update(void *ptr, const pm_render_params *p, const void *d_partial, int64_t rec_begin, int64_t rec_count,
+                  void *stream) {
+    GETCTX(ptr);
+    int rc;
+    if ((rc = check_params(c, p))) return rc;
+    if (!d_partial || rec_begin < 0 || rec_count < 0 || rec_begin + rec_count > c->nrec)
+        FAIL(c, PM_ERR_INVALID, "bad record range");
+    hipStream_t s = pick(c, stream);
+    GatherParams G = gather_params(c, p);
+    timer_begin(c, "update", s);
+    HIPCHK(c, launch_ppm_update(G, (const float4 *)d_partial, rec_begin, rec_count, s));
+    timer_end(c, "update", s);
+    return PM_OK;
+}
+
+int pm_final(void *ptr, double emitted, int64_t rec_begin, int64_t rec_count, void *d_out, void *stream) {
+    GETCTX(ptr);
+    if (!d_out || rec_begin < 0 || rec_count < 0 || rec_begin + rec_count > c->nrec)
+        FAIL(c, PM_ERR_INVALID, "bad final range");
+    hipStream_t s = pick(c, stream);
+    FinalParams F{};
+    F.R = recs(c);
+    F.emitted = (float)emitted; /* gContext["emittingPhotons"]->setFloat((float)totalPhotons) */
+    F.rec_begin = rec_begin; F.rec_count = rec_count; F.out = (float *)d_out; F.raster = 0; F.W = c->W;
+    timer_begin(c, "final", s);
+    HIPCHK(c, launch_final(F, s));
+    timer_end(c, "final", s);
+    return PM_OK;
+}
+
+/* ------------------------------------------------------------ whole render */
+int pm_render(void *ptr, const pm_render_params *p, float *out_rgb, pm_stats *st) {
+    GETCTX(ptr);
+    int rc;
+    if ((rc = check_params(c, p))) return rc;
+    if (!out_rgb) FAIL(c, PM_ERR_INVALID, "null output");
+    if (p->passes < 1 || p->paths_per_pass < 1) FAIL(c, PM_ERR_INVALID, "passes and paths_per_pass must be >= 1");
+    hipStream_t s = c->stream;
+    double t_eye = 0, t_trace = 0, t_build = 0, t_gather = 0, t_final = 0;
+    if ((rc = pm_eye_pass(c, p, s))) return rc;
+    t_eye = timer_ms(c, "eye");
+    int64_t nvalid = 0;
+    int64_t counters[2] = {0, 0};
+    for (int pass = 0; pass < p->passes; ++pass) {
+        if ((rc = pm_trace_photons(c, p, pass, 0, p->paths_per_pass, 0, s))) return rc;
+        t_trace += timer_ms(c, "trace");
+        if ((rc = pm_build_photon_map(c, p, p->paths_per_pass * p->max_photon_count, s))) return rc;
+        t_build += timer_ms(c, "build");
+        if (p->gather_structure == PM_GATHER_GRID) {
+            uint32_t nv = 0;
+            HIPCHK(c, hipMemcpyAsync(&nv, c->d_nvalid.p, 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            nvalid = nv;
+        } else {
+            nvalid = c->kd_count;
+        }
+        if (nvalid == 0) FAIL(c, PM_ERR_NO_PHOTONS, "0 valid photons (photonmappingrenderer.cpp:165-167)");
+        if ((rc = pm_gather(c, p, s))) return rc;
+        t_gather += timer_ms(c, "gather");
+        if (c->counting) {
+            unsigned long long hc[2];
+            HIPCHK(c, hipMemcpy(hc, c->d_counters.p, 16, hipMemcpyDeviceToHost));
+            counters[0] = (int64_t)hc[0]; counters[1] = (int64_t)hc[1];
+        }
+    }
+    const double emitted = (double)p->paths_per_pass * p->passes;
+    const int64_t nout = c->pinhole ? (int64_t)c->W * c->H : c->nrec;
+    HIPCHK(c, c->d_out.ensure(nout * 3 * sizeof(float)));
+    FinalParams F{};
+    F.R = recs(c);
+    F.emitted = (float)emitted;
+    F.rec_begin = 0; F.rec_count = c->nrec; F.out = c->d_out.as<float>(); F.raster = c->pinhole; F.W = c->W;
+    timer_begin(c, "final", s);
+    HIPCHK(c, launch_final(F, s));
+    timer_end(c, "final", s);
+    HIPCHK(c, hipMemcpyAsync(out_rgb, c->d_out.p, nout * 3 * sizeof(float), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    t_final = timer_ms(c, "final");
+    if (st) {
+        std::memset(st, 0, sizeof(*st));
+        st->paths_emitted = (int64_t)emitted;
+        st->photons_valid = nvalid;
+        std::vector<float4> pos(c->nrec);
+        HIPCHK(c, hipMemcpy(pos.data(), c->d_pos.p, c->nrec * sizeof(float4), hipMemcpyDeviceToHost));
+        int64_t act = 0;
+        for (auto &q : pos) act += (fbits_h(q.w) & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) == 0;
+        st->gather_points = act;
+        st->nodes_visited = counters[0];
+        st->photons_in_radius = counters[1];
+        st->ms_eye = t_eye; st->ms_trace = t_trace; st->ms_build = t_build; st->ms_gather = t_gather;
+        st->ms_final = t_final;
+    }
+    return PM_OK;
+}
+
+/* ------------------------------------------------------- buffers / tests */
+int64_t pm_num_records(void *ptr) {
+    Ctx *c = (Ctx *)ptr;
+    return c ? num_records(c) : -1;
+}
+
+int pm_record_pixel(void *ptr, int64_t r, int64_t *pixel) {
+    GETCTX(ptr);
+    if (!pixel) FAIL(c, PM_ERR_INVALID, "null output");
+    if (!c->pinhole) { *pixel = r; return PM_OK; }
+    int64_t tile = r >> 6;
+    int lane = (int)(r & 63), tilesX = (c->W + 7) / 8;
+    int px = (int)(tile % tilesX) * 8 + (lane & 7), py = (int)(tile / tilesX) * 8 + (lane >> 3);
+    *pixel = (px >= c->W || py >= c->H) ? -1 : (int64_t)py * c->W + px;
+    return PM_OK;
+}
+
+int pm_download_slots(void *ptr, pm_photon *out, int64_t n) {
+    GETCTX(ptr);
+    if (!out || n < 0 || (size_t)n * sizeof(pm_photon) > c->d_slots.bytes) FAIL(c, PM_ERR_INVALID, "bad slot range");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(out, c->d_slots.p, n * sizeof(pm_photon), hipMemcpyDeviceToHost));
+    return PM_OK;
+}
+
+int pm_upload_slots(void *ptr, const pm_photon *in, int64_t n) {
+    GETCTX(ptr);
+    int rc;
+    if (!in || n < 0) FAIL(c, PM_ERR_INVALID, "bad slots");
+    if ((rc = pm_reserve_slots(c, n, nullptr))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(c->d_slots.p, in, n * sizeof(pm_photon), hipMemcpyHostToDevice));
+    c->slots_used = n;
+    return PM_OK;
+}
+
+int pm_download_records(void *ptr, pm_record *out, int64_t n) {
+    GETCTX(ptr);
+    if (!out || n < 0 || n > c->nrec) FAIL(c, PM_ERR_INVALID, "bad record range");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<float4> pos(n), nrm(n), st(n), dl(n);
+    std::vector<float> N(n);
+    HIPCHK(c, hipMemcpy(pos.data(), c->d_pos.p, n * 16, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(nrm.data(), c->d_nrm.p, n * 16, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(st.data(), c->d_state.p, n * 16, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(dl.data(), c->d_dl.p, n * 16, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(N.data(), c->d_n.p, n * 4, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n; ++i) {
+        pm_record &r = out[i];
+        r.pos[0] = pos[i].x; r.pos[1] = pos[i].y; r.pos[2] = pos[i].z; r.flags = (uint32_t)fbits_h(pos[i].w);
+        r.ns[0] = nrm[i].x; r.ns[1] = nrm[i].y; r.ns[2] = nrm[i].z; r.material = fbits_h(nrm[i].w);
+        r.flux[0] = st[i].x; r.flux[1] = st[i].y; r.flux[2] = st[i].z; r.radius2 = st[i].w;
+        r.dl[0] = dl[i].x; r.dl[1] = dl[i].y; r.dl[2] = dl[i].z; r.photon_count = N[i];
+    }
+    return PM_OK;
+}
+
+int pm_upload_records(void *ptr, const pm_record *in, int64_t n) {
+    GETCTX(ptr);
+    int rc;
+    if (!in || n != num_records(c)) FAIL(c, PM_ERR_INVALID, "record count must equal pm_num_records");
+    if ((rc = ensure_records(c))) return rc;
+    std::vector<float4> pos(n), nrm(n), st(n), dl(n);
+    std::vector<float> N(n);
+    for (int64_t i = 0; i < n; ++i) {
+        const pm_record &r = in[i];
+        pos[i] = f4(r.pos[0], r.pos[1], r.pos[2], ibits((int)r.flags));
+        nrm[i] = f4(r.ns[0], r.ns[1], r.ns[2], ibits(r.material));
+        st[i] = f4(r.flux[0], r.flux[1], r.flux[2], r.radius2);
+        dl[i] = f4(r.dl[0], r.dl[1], r.dl[2], 0.f);
+        N[i] = r.photon_count;
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(c->d_pos.p, pos.data(), n * 16, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_nrm.p, nrm.data(), n * 16, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_state.p, st.data(), n * 16, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_dl.p, dl.data(), n * 16, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_n.p, N.data(), n * 4, hipMemcpyHostToDevice));
+    return PM_OK;
+}
+
+int64_t pm_kdtree_nodes(void *ptr) {
+    Ctx *c = (Ctx *)ptr;
+    return c ? c->kd_count : -1;
+}
+
+int pm_download_kdtree(void *ptr, pm_photon *out, int64_t n) {
+    GETCTX(ptr);
+    if (!out || n < 0 || n > c->kd_count) FAIL(c, PM_ERR_INVALID, "bad kd range");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(out, c->d_kd.p, n * sizeof(pm_photon), hipMemcpyDeviceToHost));
+    return PM_OK;
+}
+
+int pm_gather_counters(void *ptr, int64_t out[4]) {
+    GETCTX(ptr);
+    unsigned long long h[4];
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(h, c->d_counters.p, 32, hipMemcpyDeviceToHost));
+    for (int i = 0; i < 4; ++i) out[i] = (int64_t)h[i];
+    return PM_OK;
+}
+
+int pm_set_counting(void *ptr, int enabled) {
+    GETCTX(ptr);
+    c->counting = enabled != 0;
+    return PM_OK;
+}
+
+int pm_synchronize(void *ptr) {
+    GETCTX(ptr);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PM_OK;
+}
+
+int pm_last_kernel_ms(void *ptr, const char *name, double *ms) {
+    GETCTX(ptr);
+    if (!name || !ms) FAIL(c, PM_ERR_INVALID, "null argument");
+    *ms = timer_ms(c, name);
+    if (*ms < 0) FAIL(c, PM_ERR_INVALID, "no timing recorded for '%s'", name);
+    return PM_OK;
+}
+
+int pm_timing_reset(void *ptr) {
+    GETCTX(ptr);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (auto &kv : c->timers) kv.second.used = 0;
+    return PM_OK;
+}
+
+int pm_timing_total(void *ptr, const char *name, int64_t *count, double *total_ms) {
+    GETCTX(ptr);
+    if (!name || !count || !total_ms) FAIL(c, PM_ERR_INVALID, "null argument");
+    *count = 0;
+    *total_ms = 0.0;
+    auto it = c->timers.find(name);
+    if (it == c->timers.end()) return PM_OK;
+    for (size_t i = 0; i < it->second.used; ++i) {
+        double ms = pair_ms(it->second.ev[i]);
+        if (ms < 0) FAIL(c, PM_ERR_HIP, "event timing failed for '%s'", name);
+        *total_ms += ms;
+    }
+    *count = (int64_t)it->second.used;
+    return PM_OK;
+}
+
+int pm_reset_records(void *ptr, const pm_render_params *p, void *stream) {
+    GETCTX(ptr);
+    int rc;
+    if ((rc = check_params(c, p))) return rc;
+    if (c->nrec <= 0) FAIL(c, PM_ERR_INVALID, "no records (run pm_eye_pass first)");
+    hipStream_t s = pick(c, stream);
+    timer_begin(c, "reset", s);
+    HIPCHK(c, launch_reset_records(recs(c), p->initial_radius2, s));
+    timer_end(c, "reset", s);
+    return PM_OK;
+}
+
+} /* extern "C" */

@@ -1,0 +1,219 @@
+/*
+ * pm_build.cpp — host builders (see pm_build.h).
+ */
+#include "pm_build.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace pm {
+
+namespace {
+
+constexpr int LEAF_MAX = 4;
+constexpr int NBINS = 16;
+
+struct Box {
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    void grow(const float *l, const float *h) {
+        for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], l[a]); hi[a] = std::max(hi[a], h[a]); }
+    }
+    void grow(const Box &b) { grow(b.lo, b.hi); }
+    float half_area() const {
+        float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        if (dx < 0 || dy < 0 || dz < 0) return 0.f;
+        return dx * dy + dy * dz + dz * dx;
+    }
+};
+
+inline float centroid(const BuildPrim &p, int a) { return 0.5f * (p.lo[a] + p.hi[a]); }
+
+struct BvhBuilder {
+    std::vector<BuildPrim> &P;
+    std::vector<float> &nodes;
+    int max_depth;
+    int depth_seen = 0;
+
+    int alloc() {
+        int id = (int)(nodes.size() / 16);
+        nodes.resize(nodes.size() + 16, 0.f);
+        return id;
+    }
+
+    void write_node(int id, const Box &lb, int lcode, int lcount, const Box &rb, int rcode, int rcount) {
+        float *n = &nodes[(size_t)id * 16];
+        n[0] = lb.lo[0]; n[1] = lb.lo[1]; n[2] = lb.lo[2]; n[3] = lb.hi[0];
+        n[4] = lb.hi[1]; n[5] = lb.hi[2]; n[6] = rb.lo[0]; n[7] = rb.lo[1];
+        n[8] = rb.lo[2]; n[9] = rb.hi[0]; n[10] = rb.hi[1]; n[11] = rb.hi[2];
+        int ints[4] = {lcode, rcode, lcount, rcount};
+        std::memcpy(&n[12], ints, sizeof(ints));
+    }
+
+    /* binned SAH; returns split position or -1 for "make a leaf" */
+    int find_split(int b, int e) {
+        int n = e - b;
+        Box cb;
+        for (int i = b; i < e; ++i) {
+            float c[3] = {centroid(P[i], 0), centroid(P[i], 1), centroid(P[i], 2)};
+            cb.grow(c, c);
+        }
+        Box full;
+        for (int i = b; i < e; ++i) full.grow(P[i].lo, P[i].hi);
+        float best_cost = INFINITY;
+        int best_axis = -1, best_bin = -1;
+        for (int a = 0; a < 3; ++a) {
+            float ext = cb.hi[a] - cb.lo[a];
+            if (!(ext > 0.f)) continue;
+            Box bins[NBINS];
+            int cnt[NBINS] = {0};
+            float k = NBINS / ext;
+            for (int i = b; i < e; ++i) {
+                int bi = (int)((centroid(P[i], a) - cb.lo[a]) * k);
+                bi = std::min(NBINS - 1, std::max(0, bi));
+                cnt[bi]++;
+                bins[bi].grow(P[i].lo, P[i].hi);
+            }
+            float rarea[NBINS];
+            int rcnt[NBINS];
+            Box acc;
+            int c = 0;
+            for (int i = NBINS - 1; i > 0; --i) {
+                acc.grow(bins[i]); c += cnt[i];
+                rarea[i] = acc.half_area(); rcnt[i] = c;
+            }
+            Box lacc;
+            int lc = 0;
+            for (int i = 0; i < NBINS - 1; ++i) {
+                lacc.grow(bins[i]); lc += cnt[i];
+                if (lc == 0 || rcnt[i + 1] == 0) continue;
+                float cost = lacc.half_area() * lc + rarea[i + 1] * rcnt[i + 1];
+                if (cost < best_cost) { best_cost = cost; best_axis = a; best_bin = i; }
+            }
+        }
+        float A = full.half_area();
+        if (best_axis < 0) {
+            /* all centroids coincide: median split by index */
+            return n > LEAF_MAX ? b + n / 2 : -1;
+        }
+        float split_cost = 0.125f + (A > 0.f ? best_cost / A : (float)n);
+        if (n <= 8 && (float)n <= split_cost) return -1;
+        float ext = cb.hi[best_axis] - cb.lo[best_axis];
+        float k = NBINS / ext;
+        int a = best_axis;
+        auto mid = std::partition(P.begin() + b, P.begin() + e, [&](const BuildPrim &p) {
+            int bi = (int)((centroid(p, a) - cb.lo[a]) * k);
+            bi = std::min(NBINS - 1, std::max(0, bi));
+            return bi <= best_bin;
+        });
+        int m = (int)(mid - P.begin());
+        if (m == b || m == e) {
+            m = b + n / 2;
+            std::nth_element(P.begin() + b, P.begin() + m, P.begin() + e,
+                             [&](const BuildPrim &x, const BuildPrim &y) { return centroid(x, a) < centroid(y, a); });
+        }
+        return m;
+    }
+
+    void child(int b, int e, int depth, int &code, int &count, Box &box) {
+        box = Box();
+        for (int i = b; i < e; ++i) box.grow(P[i].lo, P[i].hi);
+        int split = -1;
+        if (e - b > LEAF_MAX && depth < max_depth) split = find_split(b, e);
+        if (split < 0) { code = ~b; count = e - b; return; }
+        int id = alloc();
+        depth_seen = std::max(depth_seen, depth + 1);
+        Box lb, rb;
+        int lc, lcnt, rc, rcnt;
+        child(b, split, depth + 1, lc, lcnt, lb);
+        child(split, e, depth + 1, rc, rcnt, rb);
+        write_node(id, lb, lc, lcnt, rb, rc, rcnt);
+        code = id; count = 0;
+    }
+};
+
+} // namespace
+
+void build_bvh(std::vector<BuildPrim> &prims, int max_depth, BvhOut &out) {
+    out.nodes.clear();
+    out.refs.clear();
+    BvhBuilder B{prims, out.nodes, max_depth};
+    int n = (int)prims.size();
+    Box empty;
+    if (n == 0) {
+        int id = B.alloc();
+        B.write_node(id, empty, ~0, -1, empty, ~0, -1);
+    } else {
+        int root = B.alloc();
+        int split = n > LEAF_MAX ? B.find_split(0, n) : -1;
+        if (split < 0) {
+            Box all;
+            for (auto &p : prims) all.grow(p.lo, p.hi);
+            B.write_node(root, all, ~0, n, empty, ~0, -1);
+        } else {
+            Box lb, rb;
+            int lc, lcnt, rc, rcnt;
+            B.child(0, split, 1, lc, lcnt, lb);
+            B.child(split, n, 1, rc, rcnt, rb);
+            B.write_node(root, lb, lc, lcnt, rb, rc, rcnt);
+        }
+    }
+    out.depth = B.depth_seen + 1;
+    out.refs.resize(prims.size());
+    for (size_t i = 0; i < prims.size(); ++i) out.refs[i] = prims[i].ref;
+}
+
+int64_t build_kdtree_pbrt(const pm_photon *slots, int64_t nslots, std::vector<pm_photon> &nodes) {
+    std::vector<pm_photon> ph;
+    ph.reserve((size_t)nslots);
+    for (int64_t i = 0; i < nslots; ++i)
+        if (slots[i].bits & 1u) ph.push_back(slots[i]);
+    const int64_t m = (int64_t)ph.size();
+    nodes.resize((size_t)m);
+    if (m == 0) return 0;
+    std::vector<uint32_t> idx((size_t)m);
+    for (int64_t i = 0; i < m; ++i) idx[i] = (uint32_t)i;
+
+    struct Task { int64_t start, end; int64_t parent; int kind; uint32_t node; };
+    std::vector<Task> st;
+    st.push_back(Task{0, m, -1, 0, 0});
+    uint32_t next_free = 1;
+    while (!st.empty()) {
+        Task t = st.back();
+        st.pop_back();
+        uint32_t node = t.node;
+        if (t.kind == 2) { /* right child: numbered once its left sibling's subtree is done */
+            node = next_free++;
+            pm_photon &par = nodes[(size_t)t.parent];
+            par.bits = (par.bits & 7u) | (node << 3);
+        }
+        if (t.start + 1 == t.end) {
+            nodes[node] = ph[idx[(size_t)t.start]];
+            nodes[node].bits = (3u << 1) | (PM_PHOTON_MAX_RIGHT_CHILD << 3);
+            continue;
+        }
+        float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int64_t i = t.start; i < t.end; ++i) {
+            const float *p = ph[idx[(size_t)i]].p;
+            for (int a = 0; a < 3; ++a) { mn[a] = std::min(mn[a], p[a]); mx[a] = std::max(mx[a], p[a]); }
+        }
+        float dx = mx[0] - mn[0], dy = mx[1] - mn[1], dz = mx[2] - mn[2];
+        int axis = (dx > dy && dx > dz) ? 0 : (dy > dz ? 1 : 2);
+        int64_t mid = (t.start + t.end) / 2;
+        std::nth_element(idx.begin() + t.start, idx.begin() + mid, idx.begin() + t.end,
+                         [&](uint32_t a, uint32_t b) {
+                             float pa = ph[a].p[axis], pb = ph[b].p[axis];
+                             return pa == pb ? a < b : pa < pb;
+                         });
+        nodes[node] = ph[idx[(size_t)mid]];
+        uint32_t bits = ((uint32_t)axis << 1) | (PM_PHOTON_MAX_RIGHT_CHILD << 3);
+        bool has_left = t.start < mid, has_right = mid + 1 < t.end;
+        if (has_left) bits |= 1u;
+        nodes[node].bits = bits;
+        if (has_right) st.push_back(Task{mid + 1, t.end, (int64_t)node, 2, 0});
+        if (has_left) st.push_back(Task{t.start, mid, (int64_t)node, 1, next_free++});
+    }
+    return m;
+}
+
+} // namespace pm

@@ -1,0 +1,39 @@
+/*
+ * pm_build.h — host-side acceleration-structure builders.
+ *
+ *  - build_bvh: binned-SAH binary BVH in the two-children-per-node layout the
+ *    traversal kernels read (replaces OptiX's "Sbvh" build triggered at
+ *    cudarender.cpp:38-75). Depth is capped so the per-lane LDS stack
+ *    (BVH_STACK) can never overflow.
+ *  - build_kdtree_pbrt: the canonical pbrt-v2 KdTree median split in the
+ *    reference's CudaPhoton node layout (CreatePhotonMap,
+ *    photon_mapping/photonmappingrenderer.cpp:150-180). Ties on the split
+ *    coordinate break by position in the valid-photon list, so the tree is
+ *    unique (implementation-independent).
+ */
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+#include "../../include/pm_api.h"
+
+namespace pm {
+
+struct BuildPrim {
+    float lo[3], hi[3];
+    uint32_t ref;
+};
+
+struct BvhOut {
+    std::vector<float> nodes; /* 16 floats per node */
+    std::vector<uint32_t> refs;
+    int depth = 0;
+};
+
+void build_bvh(std::vector<BuildPrim> &prims, int max_depth, BvhOut &out);
+
+/* returns the number of nodes (= valid photons); nodes sized >= that */
+int64_t build_kdtree_pbrt(const pm_photon *slots, int64_t nslots, std::vector<pm_photon> &nodes);
+
+} // namespace pm

@@ -1,0 +1,471 @@
+/*
+ * pm_device.h — device-side building blocks of the MI355X photon mapper:
+ * vector math with the reference's (OptiX) rounding semantics, the scene
+ * layout in HBM, intersectors, BSDFs, lights and Halton sampling.
+ *
+ * Numerics contract: compiled with
+ * -ffp-contract=off; every expression keeps the operation order of the
+ * reference program it restates, so results match the CPU oracle bit for
+ * bit. Transcendentals come from include/pm_detmath.h.
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pm_api.h"
+#include "../../include/pm_detmath.h"
+
+#pragma clang fp contract(off)
+
+#define PMD __device__ __forceinline__
+
+namespace pm {
+
+/* ------------------------------------------------------------------ v3 */
+struct v3 { float x, y, z; };
+PMD v3 mk(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
+PMD v3 operator+(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+PMD v3 operator-(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+PMD v3 operator-(v3 a) { return mk(-a.x, -a.y, -a.z); }
+PMD v3 operator*(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+PMD v3 operator*(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+PMD v3 operator*(float s, v3 a) { return mk(s * a.x, s * a.y, s * a.z); }
+/* OptiX float3 / float multiplies by the reciprocal */
+PMD v3 operator/(v3 a, float s) { float inv = 1.0f / s; return a * inv; }
+PMD float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+PMD v3 cross(v3 a, v3 b) { return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+PMD v3 normalize(v3 v) { float inv = 1.0f / sqrtf(dot(v, v)); return v * inv; }
+PMD float absdot(v3 a, v3 b) { return fabsf(dot(a, b)); }
+PMD bool is_black(v3 s) { return s.x == 0.0f && s.y == 0.0f && s.z == 0.0f; }
+PMD v3 xyz(float4 a) { return mk(a.x, a.y, a.z); }
+PMD float comp(v3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+
+constexpr float INV_PI = 0.31830988618379067154f;
+constexpr float INV_TWOPI = 0.15915494309189533577f;
+constexpr float RT_DEFAULT_MAX = 1.e27f;
+
+/* ---------------------------------------------------------- scene layout */
+/* prim ref = (kind << 30) | index */
+enum : uint32_t { PRIM_TRI = 0u, PRIM_DISK = 1u, PRIM_SPHERE = 2u };
+
+struct LightDev {      /* CudaLightDevice (common.cu.h:47-59), 80 B */
+    float4 o_type;     /* o.xyz, type (int bits) */
+    float4 p1_ns;      /* p1.xyz, nSample (int bits) */
+    float4 p2_r2d;     /* p2.xyz, random2DStart (int bits) */
+    float4 n_area;     /* normal.xyz, area */
+    float4 le;         /* intensity.xyz, 0 */
+};
+
+struct SceneDev {
+    const float4 *nodes;     /* 4 float4 per BVH node */
+    const uint32_t *refs;    /* leaf primitive refs */
+    const float4 *tri_geo;   /* 3 float4 per triangle: (p0, e0.x) (e0.yz, e1.xy) (e1.z, n) */
+    const int4 *tri_info;    /* (v0, v1, v2, mesh) */
+    const uint32_t *tri_id;  /* global primitive id (tie-break) */
+    const float4 *verts;
+    const float4 *norms;
+    const float2 *uvs;
+    const int4 *meshes;      /* (material, light, has_n, has_uv) */
+    const float4 *disks;     /* 5 float4 per disk */
+    const float4 *spheres;   /* 4 float4 per sphere */
+    const float4 *materials; /* (kd.xyz, type bits) */
+    const LightDev *lights;
+    int n_lights;
+    int n_nodes;
+};
+
+struct Ray { v3 o, d; float tmin, tmax; };
+
+constexpr int BVH_STACK_DEPTH = 48; /* LDS stack entries per lane (builder caps depth below it) */
+
+struct Hit {
+    uint32_t ref;   /* prim ref of the winner */
+    uint32_t gid;   /* global id (tie-break) */
+    float t, beta, gamma;
+};
+
+PMD int fbits(float f) { return __float_as_int(f); }
+
+/* ------------------------------------------------------------ samplers */
+/* util.cu.h:23-65 */
+PMD void concentric_sample_disk(float u1, float u2, float *dx, float *dy) {
+    float r, theta;
+    float sx = 2 * u1 - 1;
+    float sy = 2 * u2 - 1;
+    if (sx == 0.0f && sy == 0.0f) { *dx = 0.0f; *dy = 0.0f; return; }
+    if (sx >= -sy) {
+        if (sx > sy) { r = sx; theta = (sy > 0.0f) ? sy / r : 8.0f + sy / r; }
+        else { r = sy; theta = 2.0f - sx / r; }
+    } else {
+        if (sx <= sy) { r = -sx; theta = 4.0f - sy / r; }
+        else { r = -sy; theta = 6.0f + sx / r; }
+    }
+    theta = (float)((double)theta * (M_PI / 4.f));
+    *dx = r * pmdm_cosf(theta);
+    *dy = r * pmdm_sinf(theta);
+}
+
+/* cudalight.cu.h:66-73 */
+PMD v3 uniform_sample_sphere(float u1, float u2) {
+    float z = 1.f - 2.f * u1;
+    float r = sqrtf(fmaxf(0.f, 1.f - z * z));
+    float phi = (float)(2.f * M_PI * (double)u2);
+    return mk(r * pmdm_cosf(phi), r * pmdm_sinf(phi), z);
+}
+
+/* photontracing.cu:19-43 — permutation table in LDS/constant, 28 uints */
+PMD float permuted_radical_inverse(uint32_t n, uint32_t base, const uint32_t *p) {
+    float val = 0;
+    float invBase = 1.f / base, invBi = invBase;
+    while (n > 0) {
+        uint32_t d_i = p[n % base];
+        val += d_i * invBi;
+        n = (uint32_t)((float)n * invBase); /* reference quirk: n *= invBase */
+        invBi *= invBase;
+    }
+    return val;
+}
+
+/* ------------------------------------------------------------ intersect */
+/* OptiX 3 intersect_triangle (cudatrianglemesh.cu:24) on precomputed
+ * e0 = p1-p0, e1 = p0-p2, n = e1 x e0 (identical float values). */
+PMD bool isect_tri(const float4 *g, const Ray &ray, float *t, float *beta, float *gamma) {
+    float4 a = g[0], b = g[1], c = g[2];
+    v3 p0 = mk(a.x, a.y, a.z), e0 = mk(a.w, b.x, b.y), e1 = mk(b.z, b.w, c.x), n = mk(c.y, c.z, c.w);
+    const v3 e2 = (1.0f / dot(n, ray.d)) * (p0 - ray.o);
+    const v3 i = cross(ray.d, e2);
+    *beta = dot(i, e1);
+    *gamma = dot(i, e0);
+    *t = dot(n, e2);
+    return (*t < ray.tmax) & (*t > ray.tmin) & (*beta >= 0.0f) & (*gamma >= 0.0f) & (*beta + *gamma <= 1);
+}
+
+/* cudadisk.cu:18-50 */
+PMD bool isect_disk(const float4 *dk, const Ray &ray, float *thit_out) {
+    float4 a = dk[0], b = dk[1], c = dk[2], d = dk[3], e = dk[4];
+    v3 o = xyz(a), x = xyz(b), y = xyz(c), z = xyz(d);
+    float thit = (c.w - dot(z, ray.o)) / dot(z, ray.d);
+    if (!(thit > ray.tmin && thit < ray.tmax)) return false;
+    v3 phit = ray.o + thit * ray.d;
+    v3 local = phit - o;
+    float localx = dot(local, x) * d.w;
+    float localy = dot(local, y) * e.x;
+    float dist2 = localx * localx + localy * localy;
+    if (dist2 > 1.f || dist2 < a.w * a.w) return false;
+    float phi = pmdm_atan2f(localy, localx);
+    if (phi < 0) phi = (float)((double)phi + 2.f * M_PI);
+    if (phi > b.w) return false;
+    *thit_out = thit;
+    return true;
+}
+
+PMD void xform_ray(const float4 *m, const Ray &r, v3 *o, v3 *d) {
+    float4 r0 = m[0], r1 = m[1], r2 = m[2];
+    *o = mk(((r0.x * r.o.x + r0.y * r.o.y) + r0.z * r.o.z) + r0.w,
+            ((r1.x * r.o.x + r1.y * r.o.y) + r1.z * r.o.z) + r1.w,
+            ((r2.x * r.o.x + r2.y * r.o.y) + r2.z * r.o.z) + r2.w);
+    *d = mk((r0.x * r.d.x + r0.y * r.d.y) + r0.z * r.d.z,
+            (r1.x * r.d.x + r1.y * r.d.y) + r1.z * r.d.z,
+            (r2.x * r.d.x + r2.y * r.d.y) + r2.z * r.d.z);
+}
+/* rtTransformNormal(RT_OBJECT_TO_WORLD, n) = transpose(W2O) n */
+PMD v3 xform_normal(const float4 *m, v3 n) {
+    float4 r0 = m[0], r1 = m[1], r2 = m[2];
+    return mk((r0.x * n.x + r1.x * n.y) + r2.x * n.z,
+              (r0.y * n.x + r1.y * n.y) + r2.y * n.z,
+              (r0.z * n.x + r1.z * n.y) + r2.z * n.z);
+}
+
+/* cudasphere.cu:7-72 */
+PMD bool isect_sphere(const float4 *s, const Ray &ray, float *thit) {
+    v3 o, d;
+    xform_ray(s, ray, &o, &d);
+    float rad = s[3].x;
+    float A = dot(d, d);
+    float B = 2.f * dot(d, o);
+    float C = dot(o, o) - rad * rad;
+    float discrim = B * B - 4.f * A * C;
+    if (discrim < 0.f) return false;
+    float root = sqrtf(discrim);
+    float q = (B < 0) ? -.5f * (B - root) : -.5f * (B + root);
+    float t0 = q / A, t1 = C / q;
+    if (t0 > t1) { float tmp = t0; t0 = t1; t1 = tmp; }
+    if (t0 > ray.tmin && t0 < ray.tmax) { *thit = t0; return true; }
+    if (t1 > ray.tmin && t1 < ray.tmax) { *thit = t1; return true; }
+    return false;
+}
+
+/* ---------------------------------------------------------- traversal */
+/* Slab test of one child box; returns tnear (inf = miss). */
+PMD float box_near(float lx, float ly, float lz, float hx, float hy, float hz, v3 o, v3 inv, float tmin,
+                   float tmax) {
+    float t0x = (lx - o.x) * inv.x, t1x = (hx - o.x) * inv.x;
+    float t0y = (ly - o.y) * inv.y, t1y = (hy - o.y) * inv.y;
+    float t0z = (lz - o.z) * inv.z, t1z = (hz - o.z) * inv.z;
+    float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
+    float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), tmax));
+    return tn <= tf ? tn : __int_as_float(0x7f800000);
+}
+
+PMD v3 safe_inv(v3 d) {
+    const float tiny = 1e-20f;
+    float x = fabsf(d.x) < tiny ? copysignf(tiny, d.x) : d.x;
+    float y = fabsf(d.y) < tiny ? copysignf(tiny, d.y) : d.y;
+    float z = fabsf(d.z) < tiny ? copysignf(tiny, d.z) : d.z;
+    return mk(1.0f / x, 1.0f / y, 1.0f / z);
+}
+
+/* Tests the primitives of one leaf; for ANY=true returns at the first hit. */
+template <bool ANY>
+PMD bool leaf_isect(const SceneDev &S, uint32_t start, uint32_t count, const Ray &ray, Hit &best) {
+    for (uint32_t k = start; k < start + count; ++k) {
+        uint32_t ref = S.refs[k];
+        uint32_t kind = ref >> 30, idx = ref & 0x3fffffffu;
+        float t, b = 0.f, g = 0.f;
+        bool ok;
+        uint32_t gid;
+        if (kind == PRIM_TRI) {
+            ok = isect_tri(S.tri_geo + 3 * idx, ray, &t, &b, &g);
+            if (ANY) { if (ok) return true; continue; }
+            if (!ok || t > best.t) continue;
+            gid = S.tri_id[idx];
+        } else if (kind == PRIM_DISK) {
+            ok = isect_disk(S.disks + 5 * idx, ray, &t);
+            if (ANY) { if (ok) return true; continue; }
+            if (!ok || t > best.t) continue;
+            gid = (uint32_t)fbits(S.disks[5 * idx + 4].w);
+        } else {
+            ok = isect_sphere(S.spheres + 4 * idx, ray, &t);
+            if (ANY) { if (ok) return true; continue; }
+            if (!ok || t > best.t) continue;
+            gid = (uint32_t)fbits(S.spheres[4 * idx + 3].w);
+        }
+        if (t < best.t || gid < best.gid) { /* t <= best.t here: ties -> lowest id */
+            best.t = t; best.beta = b; best.gamma = g; best.ref = ref; best.gid = gid;
+        }
+    }
+    return false;
+}
+
+/* BVH traversal with a per-lane stack column in LDS (stack[depth*stride]).
+ * Closest hit (ANY=false) or occlusion (ANY=true). Node = 4 float4:
+ * (l.lo, l.hi.x) (l.hi.yz, r.lo.xy) (r.lo.z, r.hi) (left, right, lcount, rcount);
+ * child >= 0 internal node, child < 0 leaf with refs start ~child. */
+template <bool ANY>
+PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int stride) {
+    best.t = ray.tmax;
+    best.gid = 0xffffffffu;
+    best.ref = 0xffffffffu;
+    const v3 inv = safe_inv(ray.d);
+    int sp = 0;
+    int cur = 0;
+    /* every node is entered at most once per ray: a bound every lane reaches */
+    for (int guard = 0; guard <= S.n_nodes; ++guard) {
+        const float4 *nd = S.nodes + 4 * cur;
+        float4 a = nd[0], b = nd[1], c = nd[2];
+        int4 ch = *reinterpret_cast<const int4 *>(nd + 3);
+        float tl = box_near(a.x, a.y, a.z, a.w, b.x, b.y, ray.o, inv, ray.tmin, best.t);
+        float tr = box_near(b.z, b.w, c.x, c.y, c.z, c.w, ray.o, inv, ray.tmin, best.t);
+        bool hl = tl != __int_as_float(0x7f800000) && ch.z >= 0;
+        bool hr = tr != __int_as_float(0x7f800000) && ch.w >= 0;
+        if (hl && ch.x < 0) {
+            if (leaf_isect<ANY>(S, (uint32_t)~ch.x, (uint32_t)ch.z, ray, best)) return true;
+            hl = false;
+        }
+        if (hr && ch.y < 0) {
+            if (leaf_isect<ANY>(S, (uint32_t)~ch.y, (uint32_t)ch.w, ray, best)) return true;
+            hr = false;
+        }
+        if (hl && hr && sp < BVH_STACK_DEPTH) {
+            int nearc = ch.x, farc = ch.y;
+            if (tr < tl) { nearc = ch.y; farc = ch.x; }
+            stack[sp * stride] = farc;
+            ++sp;
+            cur = nearc;
+        } else if (hl) {
+            cur = ch.x;
+        } else if (hr) {
+            cur = ch.y;
+        } else {
+            if (sp == 0) break;
+            --sp;
+            cur = stack[sp * stride];
+        }
+    }
+    return ANY ? false : best.ref != 0xffffffffu;
+}
+
+/* ------------------------------------------------------------- shading */
+struct Geo { v3 ns, dpdu; int material, light; };
+
+/* hit attributes (cudatrianglemesh.cu:20-78, cudadisk.cu:36-47,
+ * cudasphere.cu:35-48), transformed and normalized as the closest-hit
+ * programs do (raytracing.cu:110-117, cudamaterial.cu.h:84-85). */
+PMD Geo shade(const SceneDev &S, const Ray &ray, const Hit &h) {
+    Geo g;
+    uint32_t kind = h.ref >> 30, idx = h.ref & 0x3fffffffu;
+    v3 nsw, dpduw;
+    if (kind == PRIM_TRI) {
+        int4 ti = S.tri_info[idx];
+        int4 m = S.meshes[ti.w];
+        v3 p0 = xyz(S.verts[ti.x]), p1 = xyz(S.verts[ti.y]), p2 = xyz(S.verts[ti.z]);
+        const v3 e0 = p1 - p0, e1 = p0 - p2;
+        const v3 n = cross(e1, e0);
+        float uv0x, uv0y, uv1x, uv1y, uv2x, uv2y;
+        if (!m.w) { uv0x = 0.f; uv0y = 0.f; uv1x = 1.f; uv1y = 0.f; uv2x = 0.f; uv2y = 1.f; }
+        else {
+            float2 q0 = S.uvs[ti.x], q1 = S.uvs[ti.y], q2 = S.uvs[ti.z];
+            uv0x = q0.x; uv0y = q0.y; uv1x = q1.x; uv1y = q1.y; uv2x = q2.x; uv2y = q2.y;
+        }
+        float du1 = uv0x - uv2x, du2 = uv1x - uv2x, dv1 = uv0y - uv2y, dv2 = uv1y - uv2y;
+        v3 dp1 = p0 - p2, dp2 = p1 - p2;
+        float determinant = du1 * dv2 - dv1 * du2;
+        v3 dpdu;
+        if (determinant == 0.0f) {
+            if (fabsf(n.x) > fabsf(n.y)) {
+                float invLen = 1.f / sqrtf(n.x * n.x + n.z * n.z);
+                dpdu = mk(-n.z * invLen, 0.f, n.x * invLen);
+            } else {
+                float invLen = 1.f / sqrtf(n.y * n.y + n.z * n.z);
+                dpdu = mk(0.f, n.z * invLen, n.y * invLen);
+            }
+        } else {
+            float invdet = 1.f / determinant;
+            dpdu = (dv2 * dp1 - dv1 * dp2) * invdet;
+        }
+        v3 ns = n;
+        if (m.z) {
+            v3 n0 = xyz(S.norms[ti.x]), n1 = xyz(S.norms[ti.y]), n2 = xyz(S.norms[ti.z]);
+            ns = n1 * h.beta + n2 * h.gamma + n0 * (1.0f - h.beta - h.gamma);
+        }
+        nsw = ns; dpduw = dpdu;
+        g.material = m.x; g.light = m.y;
+    } else if (kind == PRIM_DISK) {
+        const float4 *dk = S.disks + 5 * idx;
+        float4 a = dk[0], b = dk[1], c = dk[2], d = dk[3], e = dk[4];
+        v3 x = xyz(b), y = xyz(c);
+        v3 phit = ray.o + h.t * ray.d;
+        v3 local = phit - xyz(a);
+        float localx = dot(local, x) * d.w;
+        float localy = dot(local, y) * e.x;
+        nsw = xyz(d);
+        dpduw = -localy * x + localx * y;
+        g.material = fbits(e.y); g.light = fbits(e.z);
+    } else {
+        const float4 *s = S.spheres + 4 * idx;
+        v3 o, d;
+        xform_ray(s, ray, &o, &d);
+        float rad = s[3].x;
+        v3 phit = o + h.t * d;
+        if (phit.x == 0.f && phit.y == 0.f) phit.x = 1e-5f * rad;
+        v3 n = phit / rad;
+        v3 dpdu = mk(-n.y, n.x, 0.f);
+        nsw = xform_normal(s, n);
+        dpduw = xform_normal(s, dpdu);
+        g.material = fbits(s[3].y); g.light = fbits(s[3].z);
+    }
+    g.ns = normalize(nsw);
+    g.dpdu = normalize(dpduw);
+    return g;
+}
+
+PMD v3 world_to_local(v3 v, v3 nn, v3 sn, v3 tn) { return mk(dot(v, sn), dot(v, tn), dot(v, nn)); }
+PMD v3 local_to_world(v3 v, v3 nn, v3 sn, v3 tn) {
+    return mk(sn.x * v.x + tn.x * v.y + nn.x * v.z, sn.y * v.x + tn.y * v.y + nn.y * v.z,
+              sn.z * v.x + tn.z * v.y + nn.z * v.z);
+}
+PMD bool is_specular(int type) { return type == PM_GLASS || type == PM_MIRROR; }
+
+/* cudamaterial.cu.h:101-165; false on glass TIR */
+PMD bool material_specular(int type, const Geo &g, v3 wow, v3 *wiw) {
+    const v3 nn = g.ns, sn = g.dpdu, tn = cross(nn, sn);
+    v3 wo = world_to_local(wow, nn, sn, tn);
+    v3 wi;
+    if (type == PM_MIRROR) {
+        wi = mk(-wo.x, -wo.y, wo.z);
+    } else {
+        bool entering = wo.z > 0.f;
+        float sini2 = fmaxf(0.f, 1.f - wo.z * wo.z);
+        float eta = entering ? 1 / 1.5f : 1.5f;
+        float sint2 = eta * eta * sini2;
+        if (sint2 >= 1.0f) return false;
+        float cost = sqrtf(fmaxf(0.f, 1.f - sint2));
+        if (entering) cost = -cost;
+        wi = mk(eta * -wo.x, eta * -wo.y, cost);
+    }
+    *wiw = local_to_world(wi, nn, sn, tn);
+    return true;
+}
+
+/* cudamaterial.cu.h:50-98 (Lambert lobe); returns f = Kd/pi */
+PMD v3 sample_f(v3 kd, const Geo &g, v3 wow, float u1, float u2, v3 *wiw, float *pdf) {
+    const v3 nn = g.ns, sn = g.dpdu, tn = cross(nn, sn);
+    v3 wo = world_to_local(wow, nn, sn, tn);
+    float x, y;
+    concentric_sample_disk(u1, u2, &x, &y);
+    v3 wi = mk(x, y, sqrtf(fmaxf(0.f, 1.f - x * x - y * y)));
+    if (wo.z < 0.f) wi.z *= -1.f;
+    *pdf = (wo.z * wi.z > 0.0f) ? fabsf(wi.z) * INV_PI : 0.f;
+    *wiw = local_to_world(wi, nn, sn, tn);
+    return kd * INV_PI;
+}
+
+/* ------------------------------------------------------------- lights */
+/* cudalight.cu.h:18-64 */
+PMD v3 sample_l_shading(const LightDev &L, v3 point, float u1, float u2, v3 *uwi, float *pdf) {
+    int type = fbits(L.o_type.w);
+    if (type == PM_LIGHT_POINT) {
+        *uwi = xyz(L.o_type) - point;
+        float invlength2 = 1.0f / dot(*uwi, *uwi);
+        *pdf = 1.f;
+        return xyz(L.le) * invlength2;
+    }
+    float x, y;
+    concentric_sample_disk(u1, u2, &x, &y);
+    *uwi = xyz(L.o_type) + x * xyz(L.p1_ns) + y * xyz(L.p2_r2d) - point;
+    v3 wi = normalize(*uwi);
+    float distanceSquared = dot(*uwi, *uwi);
+    float costha = -dot(xyz(L.n_area), wi);
+    *pdf = distanceSquared / (costha * L.n_area.w);
+    return costha > 0.0f ? xyz(L.le) : mk(0.f, 0.f, 0.f);
+}
+
+/* cudalight.cu.h:78-124 — emission */
+PMD v3 sample_le(const LightDev &L, float lu1, float lu2, float u1, float u2, float eps, Ray *ray, v3 *Ns,
+                 float *pdf) {
+    int type = fbits(L.o_type.w);
+    if (type == PM_LIGHT_POINT) {
+        ray->o = xyz(L.o_type);
+        ray->d = uniform_sample_sphere(lu1, lu2);
+        ray->tmin = eps;
+        *Ns = ray->d;
+        *pdf = (float)(1.f / (4.f * M_PI));
+        return xyz(L.le);
+    }
+    float x, y;
+    concentric_sample_disk(lu1, lu2, &x, &y);
+    v3 org = xyz(L.o_type) + x * xyz(L.p1_ns) + y * xyz(L.p2_r2d);
+    v3 dir = uniform_sample_sphere(u1, u2);
+    *Ns = xyz(L.n_area);
+    if (dot(dir, *Ns) < 0.f) dir = dir * -1.f;
+    ray->o = org; ray->d = dir; ray->tmin = 1e-2f;
+    *pdf = INV_TWOPI;
+    return xyz(L.le) * L.n_area.w;
+}
+
+/* cudalight.cu.h:128-138 */
+PMD v3 light_le(const LightDev &L, v3 wow) {
+    if (dot(xyz(L.n_area), wow) > 0.f) return xyz(L.le);
+    return mk(0.f, 0.f, 0.f);
+}
+
+/* record index -> pixel of an 8x8-tile ordering */
+PMD void rec_to_pixel(int64_t r, int W, int *px, int *py) {
+    int64_t tile = r >> 6;
+    int lane = (int)(r & 63);
+    int tilesX = (W + 7) / 8;
+    *px = (int)(tile % tilesX) * 8 + (lane & 7);
+    *py = (int)(tile / tilesX) * 8 + (lane >> 3);
+}
+
+} // namespace pm

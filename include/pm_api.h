@@ -1,0 +1,247 @@
+/*
+ * pm_api.h — C-ABI of the MI355X photon-mapping renderer (libpmhip.so).
+ *
+ * This is the drop-in boundary. The reference exposes a C++ plugin surface to
+ * pbrt-v2 (cuda_render/cudaapi.h:8-19 + class CudaRender : Renderer,
+ * cuda_render/cudarender.h:22-91) whose implementation talks to OptiX. Here
+ * that surface is kept by a thin C++ adapter (cuda-raytrace_amd/adapter/,
+ * see INTEGRATION.md) that flattens pbrt objects into the POD calls below.
+ * Every entry point is `extern "C"`, takes plain pointers and sizes, returns
+ * an int status (PM_OK = 0) and never throws; the message of the last failure
+ * is available from pm_last_error(). Caller-owned input arrays are copied
+ * during the call. A context is single-threaded (like the reference's global
+ * gContext, cudarender.cpp:14) and bound to one HIP device.
+ *
+ * Mapping to the reference (file:line of the function each entry replaces):
+ *   pm_create / pm_destroy        CudaRenderInit        cudaapi.cpp:4-7, cudarender.cpp:17-36
+ *   pm_add_material               CudaMaterial::createCudaMeteral  util/material/cudamaterial.cpp:8-21
+ *   pm_add_trimesh                CudaTriangleMesh::setupGeometry  util/shape/cudatrianglemesh.cpp:16-73
+ *   pm_add_sphere                 CudaSphere::setupTransform       util/shape/cudasphere.cpp:15-40
+ *   pm_add_disk                   CudaDisk::setupGeometry          util/shape/cudadisk.cpp:15-45
+ *   pm_add_light_point            CudaLight::setupLight<PointLight>        util/light/cudalight.cpp:16-24
+ *   pm_add_light_disk             CudaLight::setupLight<DiffuseAreaLight>  util/light/cudalight.cpp:26-59
+ *   pm_set_eye_rays               PbrtCamera::preLaunch (bRays, bRandom2D) util/camera/pbrtcamera.cpp:57-122
+ *   pm_set_pinhole                (on-device eye rays for synthetic benches)
+ *   pm_commit                     CudaRender::Render → assembleNode (Sbvh build)  cudarender.cpp:38-75,112-123
+ *   pm_render                     PhotonMappingRenderer::render    photon_mapping/photonmappingrenderer.cpp:31-45
+ *   pm_eye_pass                   RaytracingPass                   photonmappingrenderer.cpp:108-139 (+ raytracing.cu)
+ *   pm_trace_photons              PhotonTracingPass                photonmappingrenderer.cpp:204-226 (+ photontracing.cu)
+ *   pm_build_photon_map           CreatePhotonMap                  photonmappingrenderer.cpp:150-180
+ *   pm_gather                     PhotonGatheringPass              photonmappingrenderer.cpp:228-232 (+ gathering.cu:104-126)
+ *   pm_final                      FinalGatheringPass               photonmappingrenderer.cpp:234-277 (+ gathering.cu:129-146)
+ */
+#ifndef PM_API_H
+#define PM_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------- */
+#define PM_OK 0
+#define PM_ERR_INVALID 1     /* bad argument / call order */
+#define PM_ERR_HIP 2         /* HIP runtime failure (message has hipGetErrorString) */
+#define PM_ERR_NO_PHOTONS 3  /* 0 valid photons: reference raises Severe, photonmappingrenderer.cpp:165-167 */
+#define PM_ERR_NOMEM 4
+
+/* ---- enums (values equal the reference's) ----------------------------- */
+/* MaterialType, util/common.cu.h:61-63 */
+#define PM_MATTE 0
+#define PM_MIRROR 1
+#define PM_GLASS 2
+/* CudaLightDevice::LightType, util/common.cu.h:48 */
+#define PM_LIGHT_POINT 1
+#define PM_LIGHT_AREA_DISK 3
+/* RayTracingRecord flags, photon_mapping/photonmapping.h:25-26 (+ INVALID for padding) */
+#define PM_REC_EXCEPTION 0x01u
+#define PM_REC_MISS 0x02u
+#define PM_REC_INVALID 0x04u
+/* gather structures */
+#define PM_GATHER_GRID 0   /* hashed uniform grid of photon buckets (default, fastest) */
+#define PM_GATHER_KDTREE 1 /* reference-layout kd-tree (CudaPhoton nodes, pbrt median split) */
+/* multi-GPU photon exchange */
+#define PM_EXCHANGE_REDUCE 0   /* local maps, per-record (M, L) reduce-scatter */
+#define PM_EXCHANGE_ALLGATHER 1 /* all-gather photon slots, replicated map */
+
+/* ---- POD layouts shared with tests / other hosts ----------------------- */
+
+/* Photon slot == kd-node, bit-for-bit the reference's CudaPhoton
+ * (photon_mapping/photonmapping.h:32-41): word = hasLeftChild:1 | splitAxis:2
+ * | rightChild:29 (LSB first). Before the tree is built bit 0 is the valid
+ * bit (photonmapping.h:43-56). 40 bytes. */
+typedef struct pm_photon {
+    uint32_t bits;
+    float p[3];
+    float alpha[3];
+    float wi[3];
+} pm_photon;
+#define PM_PHOTON_MAX_RIGHT_CHILD ((1u << 29) - 1u) /* photonmapping.h:41 */
+
+/* Gather-point record (the subset of RayTracingRecord, photonmapping.h:7-24,
+ * that the gather and final passes read). 64 bytes, AoS for exchange; the
+ * device keeps it as SoA. */
+typedef struct pm_record {
+    float pos[3];
+    uint32_t flags;
+    float ns[3];    /* normalized world shading normal */
+    int32_t material;
+    float flux[3];
+    float radius2;
+    float dl[3];    /* direct light */
+    float photon_count;
+} pm_record;
+
+typedef struct pm_config {
+    int device;          /* HIP device ordinal */
+    int reserved[7];
+} pm_config;
+
+/* Render parameters. Defaults (pm_default_params) are the reference's
+ * hard-coded constants. */
+typedef struct pm_render_params {
+    float scene_epsilon;     /* 0.1   photonmappingrenderer.cpp:52 */
+    float initial_radius2;   /* 4.0   raytracing.cu:123 */
+    float ppm_alpha;         /* 0.7   gathering.cu:115 */
+    int max_photon_count;    /* 4     photonmappingrenderer.cpp:183 (deposits per path) */
+    int64_t paths_per_pass;  /* 262144 = 512*512, photonmappingrenderer.cpp:184-185,214 */
+    int passes;              /* 1     photonmappingrenderer.cpp:38 */
+    int light_source_index;  /* 0     photonmappingrenderer.cpp:211 */
+    int max_specular_depth;  /* 10    raytracing.cu:98 (eye); build cap for photons (SURVEY App.B 5) */
+    uint32_t rng_seed;       /* 777   util/random/cudarandom.h:15 */
+    uint32_t light_rng_seed; /* 2047  (cudalight.cpp:530, commented-out light RNG seed) */
+    int gather_structure;    /* PM_GATHER_GRID */
+    int reserved[6];
+} pm_render_params;
+
+typedef struct pm_stats {
+    int64_t paths_emitted;    /* total over passes */
+    int64_t photons_valid;    /* last pass */
+    int64_t gather_points;    /* active records (not MISS/EXC/INVALID) */
+    int64_t nodes_visited;    /* last gather pass: photons tested (grid) or kd nodes visited */
+    int64_t photons_in_radius;/* last gather pass: sum of M */
+    double ms_eye, ms_trace, ms_build, ms_gather, ms_final; /* device time, summed over passes */
+} pm_stats;
+
+/* ---- lifecycle -------------------------------------------------------- */
+void pm_default_params(pm_render_params *p);
+int pm_create(void **ctx, const pm_config *cfg);
+void pm_destroy(void *ctx);
+const char *pm_last_error(void *ctx);
+const char *pm_version(void);
+
+/* ---- scene ------------------------------------------------------------ */
+/* returns material id in *out_id. rgb = Kd (matte) / Kr (mirror, ignored by
+ * the device as in cudamaterial.cu.h:101-105) / unused (glass). */
+int pm_add_material(void *ctx, int type, const float rgb[3], int *out_id);
+/* World-space mesh (pbrt TriangleMesh::p is already world space,
+ * cudatrianglemesh.cpp:24-30). N and uv may be NULL. light_index = index of
+ * the area light this shape emits for, -1 otherwise. */
+int pm_add_trimesh(void *ctx, const float *P, int nverts, const int *indices, int ntris,
+                   const float *N, const float *uv, int material, int light_index);
+/* Object-space sphere (cudasphere.cpp:15-40): row-major 4x4 matrices. */
+int pm_add_sphere(void *ctx, float radius, const float o2w[16], const float w2o[16],
+                  int material, int light_index);
+/* World-space disk, already flattened as in cudadisk.cpp:24-43: o = O2W(0,0,h),
+ * x = O2W(r,0,0), y = O2W(0,r,0), z = normalize(O2W(0,0,1)),
+ * inner_norm = innerRadius/radius, phi_max in radians. */
+int pm_add_disk(void *ctx, const float o[3], const float x[3], const float y[3],
+                const float z[3], float inner_norm, float phi_max, int material, int light_index);
+int pm_add_light_point(void *ctx, const float pos[3], const float intensity[3]);
+/* Disk area light (cudalight.cpp:34-53): o centre, p1/p2 world radius vectors,
+ * n normal, Le emitted radiance, area, n_samples shadow samples. */
+int pm_add_light_disk(void *ctx, const float o[3], const float p1[3], const float p2[3],
+                      const float n[3], const float Le[3], float area, int n_samples);
+
+/* Eye samples. Either a pinhole camera evaluated on the device (records in
+ * 8x8-pixel tile order, output in raster order) ... */
+int pm_set_pinhole(void *ctx, const float eye[3], const float fwd[3], const float right[3],
+                   const float up[3], int width, int height);
+/* ... or host-generated rays in sampler order, as PbrtCamera::preLaunch
+ * packs them (o.xyz, d.xyz per ray; rand2d = n2d float2 per ray, indexed
+ * [ray][random2DStart + s], cudalight.cu.h:34-35). */
+int pm_set_eye_rays(void *ctx, const float *rays, int64_t nrays, const float *rand2d, int n2d);
+
+/* Builds the BVH and uploads the scene. Must follow the last pm_add_*. */
+int pm_commit(void *ctx);
+
+/* ---- whole render (PhotonMappingRenderer::render) ---------------------- */
+/* out_rgb: host float[3 * nrays] (rays mode) or float[3 * W * H] (pinhole,
+ * raster order), NaN/negative/inf sanitized to black like
+ * photonmappingrenderer.cpp:251-268. stats may be NULL. */
+int pm_render(void *ctx, const pm_render_params *params, float *out_rgb, pm_stats *stats);
+
+/* ---- stage-level API (device-resident state, explicit stream) ---------- */
+/* `stream` is a hipStream_t (NULL = the context's own stream). */
+int pm_eye_pass(void *ctx, const pm_render_params *params, void *stream);
+/* Emits paths [path_begin, path_begin + path_count) of `pass` into the
+ * context's slot buffer at slot offset (path - slot_path_base) * max_photon_count.
+ * Global path ids keep the Halton / Philox streams identical for any sharding. */
+int pm_trace_photons(void *ctx, const pm_render_params *params, int pass, int64_t path_begin,
+                     int64_t path_count, int64_t slot_path_base, void *stream);
+/* Builds the gather structure from the first n_slots slots (n_slots<=0: all). */
+int pm_build_photon_map(void *ctx, const pm_render_params *params, int64_t n_slots, void *stream);
+/* Fused range query + PPM update over all records ... */
+int pm_gather(void *ctx, const pm_render_params *params, void *stream);
+/* ... or over records [rec_begin, rec_begin + rec_count) (tile-owned gather). */
+int pm_gather_range(void *ctx, const pm_render_params *params, int64_t rec_begin, int64_t rec_count,
+                    void *stream);
+/* Range query only: writes per-record (M, L.rgb) as float4 to d_partial
+ * (device pointer, n_records float4). */
+int pm_gather_partial(void *ctx, const pm_render_params *params, void *d_partial, void *stream);
+/* PPM update of records [rec_begin, rec_begin+rec_count) from summed partials
+ * (d_partial points at the partial of rec_begin). */
+int pm_ppm_update(void *ctx, const pm_render_params *params, const void *d_partial,
+                  int64_t rec_begin, int64_t rec_count, void *stream);
+/* Final radiance of records [rec_begin, rec_begin+rec_count) into the device
+ * buffer d_out (float3 per record, RECORD order) — emitted = total paths. */
+int pm_final(void *ctx, double emitted, int64_t rec_begin, int64_t rec_count, void *d_out, void *stream);
+
+/* ---- buffers, sizes, host transfer (tests / distributed glue) ---------- */
+int64_t pm_num_records(void *ctx);
+int pm_record_pixel(void *ctx, int64_t rec, int64_t *pixel); /* -1 if padding */
+/* slot buffer capacity management; returns device pointer of the slots */
+int pm_reserve_slots(void *ctx, int64_t n_slots, void **d_slots);
+/* Use a caller-owned device buffer (n_slots pm_photon) as the slot buffer,
+ * e.g. a torch tensor that an RCCL all-gather fills; NULL reverts to the
+ * context's own buffer. The caller keeps it alive while the context uses it. */
+int pm_set_slot_buffer(void *ctx, void *d_slots, int64_t n_slots);
+int pm_download_slots(void *ctx, pm_photon *out, int64_t n);
+int pm_upload_slots(void *ctx, const pm_photon *in, int64_t n);
+int pm_download_records(void *ctx, pm_record *out, int64_t n);
+int pm_upload_records(void *ctx, const pm_record *in, int64_t n);
+/* kd-tree nodes of the last PM_GATHER_KDTREE build (reference layout) */
+int64_t pm_kdtree_nodes(void *ctx);
+int pm_download_kdtree(void *ctx, pm_photon *out, int64_t n);
+/* counters of the last gather: [0] photons (grid) or kd nodes visited,
+ * [1] photons in radius (sum of M), [2] bucket rows read (grid), [3] active records */
+int pm_gather_counters(void *ctx, int64_t out[4]);
+/* enable/disable visit counters in gather kernels (off by default: costs an atomic per wave) */
+int pm_set_counting(void *ctx, int enabled);
+int pm_synchronize(void *ctx);
+/* Stage timings measured with HIP events recorded on the stream the kernels
+ * run on. Stage names: "eye", "trace", "build", "gather", "update", "final",
+ * "reset". last = most recent launch; total = sum over launches since
+ * pm_timing_reset (synchronizes on the last event only when read). */
+int pm_last_kernel_ms(void *ctx, const char *name, double *ms);
+int pm_timing_reset(void *ctx);
+int pm_timing_total(void *ctx, const char *name, int64_t *count, double *total_ms);
+/* Restores every active record to the eye pass's initial PPM state
+ * (flux 0, photon_count 0, radius2 = initial_radius2). */
+int pm_reset_records(void *ctx, const pm_render_params *params, void *stream);
+
+/* Host-only (no device needed): the canonical pbrt-v2 KdTree over the valid
+ * slots in the reference node layout, i.e. what CreatePhotonMap
+ * (photonmappingrenderer.cpp:150-180) uploads. nodes_out holds >= nslots
+ * entries; returns the node count (= valid photons). */
+int64_t pm_kdtree_build_host(const pm_photon *slots, int64_t nslots, pm_photon *nodes_out);
+
+/* Halton permutation of PermutedHalton(5, RNG(seed)) (28 uints), exposed for tests. */
+int pm_halton_permutation(uint32_t seed, uint32_t out[28]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PM_API_H */

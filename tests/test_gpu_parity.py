@@ -1,0 +1,215 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the CPU oracle
+on the same seeded inputs.
+
+Bars:
+  * eye records, photon slots, kd-tree nodes: bit-exact;
+  * kd-tree gather (reference layout, same visiting order): bit-exact;
+  * photon-bucket gather: per-record photon count / radius exact, flux
+    within 2e-5 relative (fp32 summation order);
+  * final radiance: per-pixel RMSE < 1e-3 (north_star), in practice ~1e-7.
+"""
+import numpy as np
+import pytest
+
+from parity_util import assert_bitexact, compare_gathered_records, rmse
+from pmrender import scenes
+from pmrender.abi import PM_GATHER_GRID, PM_GATHER_KDTREE, PM_REC_INVALID, RenderParams
+
+pytestmark = pytest.mark.gpu
+
+
+def make_pair(scene, oracle_mod, hip_mod):
+    ctx = scene.load_into(hip_mod.Context(0))
+    orc = scene.load_into(oracle_mod.Oracle())
+    return ctx, orc
+
+
+@pytest.fixture(scope="module")
+def cornell(oracle_mod, hip_mod):
+    return make_pair(scenes.cornell_box(64, 64), oracle_mod, hip_mod)
+
+
+def test_eye_pass_bitexact(cornell):
+    ctx, orc = cornell
+    p = RenderParams.defaults()
+    ctx.eye_pass(p)
+    assert_bitexact(ctx.download_records(), orc.eye_pass(p), "eye records")
+
+
+@pytest.mark.parametrize("paths,pass_index", [(4096, 0), (65536, 2)])
+def test_photon_trace_bitexact(cornell, paths, pass_index):
+    ctx, orc = cornell
+    p = RenderParams.defaults(paths_per_pass=paths)
+    ctx.trace_photons(p, pass_index, 0, paths)
+    gpu = ctx.download_slots(paths * 4)
+    ref = orc.trace_photons(p, pass_index, 0, paths)
+    assert (ref["bits"] & 1).sum() > 0.3 * len(ref)
+    assert_bitexact(gpu, ref, "photon slots")
+
+
+def test_photon_trace_sharded_equals_whole(cornell):
+    """Global path ids: two shards traced separately == one launch (owner-writes)."""
+    ctx, orc = cornell
+    p = RenderParams.defaults(paths_per_pass=8192)
+    ref = orc.trace_photons(p, 0, 0, 8192)
+    ctx.trace_photons(p, 0, 4096, 4096, slot_path_base=4096)
+    hi = ctx.download_slots(4096 * 4)
+    ctx.trace_photons(p, 0, 0, 4096, slot_path_base=0)
+    lo = ctx.download_slots(4096 * 4)
+    assert_bitexact(np.concatenate([lo, hi]), ref, "sharded photon slots")
+
+
+def _gather_inputs(orc, paths=16384, radius2=25.0):
+    p = RenderParams.defaults(paths_per_pass=paths, initial_radius2=radius2)
+    recs = orc.eye_pass(p)
+    slots = orc.trace_photons(p, 0, 0, paths)
+    return p, recs, slots
+
+
+def test_kdtree_gather_bitexact(cornell, oracle_mod):
+    ctx, orc = cornell
+    p, recs, slots = _gather_inputs(orc)
+    p.gather_structure = PM_GATHER_KDTREE
+    ctx.upload_records(recs)
+    ctx.upload_slots(slots)
+    ctx.build_photon_map(p, len(slots))
+    nodes_ref = oracle_mod.Oracle.build_kdtree(slots)
+    assert_bitexact(ctx.download_kdtree(), nodes_ref, "kd-tree nodes")
+    ctx.set_counting(True)
+    ctx.gather(p)
+    vis, hits = ctx.gather_counters()
+    ctx.set_counting(False)
+    ref = recs.copy()
+    vis_ref, hits_ref = orc.gather(nodes_ref, ref, p)
+    assert (vis, hits) == (vis_ref, hits_ref)
+    assert_bitexact(ctx.download_records(), ref, "kd gathered records")
+
+
+@pytest.mark.parametrize("radius2", [4.0, 25.0, 0.3])
+def test_grid_gather_parity(cornell, radius2):
+    ctx, orc = cornell
+    p, recs, slots = _gather_inputs(orc, radius2=radius2)
+    ctx.upload_records(recs)
+    ctx.upload_slots(slots)
+    p.gather_structure = PM_GATHER_GRID
+    ctx.build_photon_map(p, len(slots))
+    ctx.set_counting(True)
+    ctx.gather(p)
+    vis, hits = ctx.gather_counters()
+    ctx.set_counting(False)
+    ref = recs.copy()
+    _, hits_ref = orc.gather(orc.build_kdtree(slots), ref, p)
+    assert hits == hits_ref
+    assert vis >= hits
+    compare_gathered_records(ctx.download_records(), ref)
+
+
+def test_partial_plus_update_equals_fused(cornell):
+    torch = pytest.importorskip("torch")
+    ctx, orc = cornell
+    p, recs, slots = _gather_inputs(orc)
+    ctx.upload_slots(slots)
+    ctx.build_photon_map(p, len(slots))
+    ctx.upload_records(recs)
+    ctx.gather(p)
+    fused = ctx.download_records()
+    ctx.upload_records(recs)
+    part = torch.zeros((len(recs), 4), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.gather_partial(p, part.data_ptr())
+    ctx.synchronize()
+    ref_part = orc.gather_partial(orc.build_kdtree(slots), recs)
+    gp = part.cpu().numpy()
+    assert np.array_equal(gp[:, 0], ref_part[:, 0])
+    half = len(recs) // 2
+    ctx.ppm_update(p, part.data_ptr(), 0, half)
+    ctx.ppm_update(p, part[half:].data_ptr(), half, len(recs) - half)
+    assert_bitexact(ctx.download_records(), fused, "partial+update vs fused")
+
+
+@pytest.mark.parametrize("structure", [PM_GATHER_KDTREE, PM_GATHER_GRID])
+def test_render_parity_cornell(cornell, structure):
+    ctx, orc = cornell
+    p = RenderParams.defaults(paths_per_pass=32768, passes=2, gather_structure=structure)
+    img, st = ctx.render(p)
+    ref, st_ref = orc.render(p)
+    assert st["photons_valid"] == st_ref["photons_valid"]
+    assert st["gather_points"] == st_ref["gather_points"]
+    if structure == PM_GATHER_KDTREE:
+        assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+    assert rmse(img, ref) < 1e-3
+    assert np.abs(img - ref).max() <= 1e-4 * max(1.0, float(ref.max()))
+
+
+def test_render_deterministic(cornell):
+    ctx, _ = cornell
+    p = RenderParams.defaults(paths_per_pass=16384)
+    a, _ = ctx.render(p)
+    b, _ = ctx.render(p)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.parametrize("builder", ["caustic", "feature", "soup"])
+def test_scene_parity(builder, oracle_mod, hip_mod):
+    if builder == "caustic":
+        sc = scenes.caustic_scene(96, 64)
+    elif builder == "feature":
+        sc = scenes.feature_scene(72, 40)
+    else:
+        sc = scenes.triangle_soup(20000, 80, 48)
+    ctx, orc = make_pair(sc, oracle_mod, hip_mod)
+    p = RenderParams.defaults(paths_per_pass=16384)
+    ctx.eye_pass(p)
+    recs = ctx.download_records()
+    assert_bitexact(recs, orc.eye_pass(p), f"{builder} eye records")
+    if builder == "feature":
+        assert (recs["flags"] & PM_REC_INVALID).sum() == ctx.num_records() - 72 * 40
+    ctx.trace_photons(p, 1, 0, 16384)
+    assert_bitexact(ctx.download_slots(16384 * 4), orc.trace_photons(p, 1, 0, 16384), f"{builder} slots")
+    p.gather_structure = PM_GATHER_KDTREE
+    img, _ = ctx.render(p)
+    ref, _ = orc.render(p)
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+
+
+def test_eye_rays_mode(oracle_mod, hip_mod):
+    sc = scenes.cornell_box(40, 24, nsamples=3)
+    sc.camera = scenes.rays_from_pinhole(sc)
+    ctx, orc = make_pair(sc, oracle_mod, hip_mod)
+    p = RenderParams.defaults(paths_per_pass=8192, gather_structure=PM_GATHER_KDTREE)
+    img, _ = ctx.render(p)
+    ref, _ = orc.render(p)
+    assert img.shape == (40 * 24, 3)
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+
+
+def test_no_photons_raises(hip_mod):
+    sc = scenes.cornell_box(16, 16)
+    o, x, y, n, Le, area, ns = sc.lights[0][1:]
+    sc.lights[0] = ("disk", o, x, y, n, np.float32([0, 0, 0]), area, ns)  # black light: every path returns early
+    ctx = sc.load_into(hip_mod.Context(0))
+    with pytest.raises(hip_mod.NoPhotonsError):
+        ctx.render(RenderParams.defaults(paths_per_pass=1024))
+
+
+def test_invalid_arguments(hip_mod):
+    ctx = hip_mod.Context(0)
+    with pytest.raises(hip_mod.PMError):
+        ctx.commit()  # no lights / shapes
+    with pytest.raises(hip_mod.PMError):
+        ctx.add_trimesh(np.zeros((3, 3)), np.int32([[0, 1, 5]]), material=0)  # no material 0, bad index
+
+
+def test_full_size_c2_parity(oracle_mod, hip_mod):
+    """BASELINE config 2 at full size (1920x1080, 262,144 paths = 1M slots):
+    slots bit-exact, photon counts exact, radiance RMSE < 1e-3."""
+    sc = scenes.cornell_box(1920, 1080)
+    ctx, orc = make_pair(sc, oracle_mod, hip_mod)
+    p = RenderParams.defaults()
+    img, st = ctx.render(p)
+    slots = ctx.download_slots(262144 * 4)
+    ref_slots = orc.trace_photons(p, 0, 0, 262144)
+    assert_bitexact(slots, ref_slots, "C2 slots")
+    ref, st_ref = orc.render(p)
+    assert st["photons_valid"] == st_ref["photons_valid"]
+    assert rmse(img, ref) < 1e-3

@@ -1,0 +1,289 @@
+"""Known-answer tests that pin the CPU oracle piecewise (the reference ships
+no golden vectors). Each case is derived by hand from the
+reference source cited in the test."""
+import math
+
+import numpy as np
+import pytest
+
+from pmrender.abi import PHOTON_DTYPE, RECORD_DTYPE, PM_MATTE, RenderParams
+
+
+def fp(*v):
+    return np.asarray(v, np.float32)
+
+
+def ulp_diff(a, b):
+    a = np.asarray(a, np.float32).view(np.int32).astype(np.int64)
+    b = np.asarray(b, np.float32).view(np.int32).astype(np.int64)
+    return np.abs(a - b)
+
+
+# ---- RNG -----------------------------------------------------------------
+@pytest.mark.parametrize("ctr,key,expect", [
+    ([0, 0, 0, 0], [0, 0], [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]),
+    ([0xffffffff] * 4, [0xffffffff] * 2, [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]),
+    ([0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344], [0xa4093822, 0x299f31d0],
+     [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]),
+])
+def test_philox_random123_kat(oracle_mod, ctr, key, expect):
+    """Philox4x32-10 known answers published with Random123 (kat_vectors)."""
+    assert oracle_mod.philox(ctr, key) == expect
+
+
+# ---- deterministic transcendentals ---------------------------------------
+def test_sin_cos_within_one_ulp(oracle_mod):
+    lib = oracle_mod.load()
+    xs = np.concatenate([np.linspace(-2 * math.pi, 4 * math.pi, 20001, dtype=np.float32),
+                         np.float32([0.0, -0.0, 1e-30, math.pi / 4, math.pi / 2, math.pi, 2 * math.pi])])
+    s = np.array([lib.orc_sinf(float(x)) for x in xs], np.float32)
+    c = np.array([lib.orc_cosf(float(x)) for x in xs], np.float32)
+    s_ref = np.array([math.sin(float(x)) for x in xs], np.float32)
+    c_ref = np.array([math.cos(float(x)) for x in xs], np.float32)
+    # compare as values: 1 ulp of the result, or tiny absolute near zeros
+    assert np.all((ulp_diff(s, s_ref) <= 1) | (np.abs(s - s_ref) < 1e-12))
+    assert np.all((ulp_diff(c, c_ref) <= 1) | (np.abs(c - c_ref) < 1e-12))
+
+
+def test_atan2_within_one_ulp(oracle_mod):
+    lib = oracle_mod.load()
+    rng = np.random.RandomState(3)
+    ys = rng.uniform(-5, 5, 4000).astype(np.float32)
+    xs = rng.uniform(-5, 5, 4000).astype(np.float32)
+    ys[:4] = [0, 1, -1, 0]
+    xs[:4] = [1, 0, 0, -1]
+    got = np.array([lib.orc_atan2f(float(y), float(x)) for y, x in zip(ys, xs)], np.float32)
+    ref = np.array([math.atan2(float(y), float(x)) for y, x in zip(ys, xs)], np.float32)
+    assert np.all(ulp_diff(got, ref) <= 1)
+
+
+# ---- samplers ------------------------------------------------------------
+def test_concentric_sample_disk(oracle_mod):
+    """util.cu.h:23-65 (pbrt-v2 ConcentricSampleDisk)."""
+    lib = oracle_mod.load()
+    out = np.zeros(2, np.float32)
+    from pmrender.abi import fptr
+    lib.orc_concentric_sample_disk(0.5, 0.5, fptr(out))
+    assert out.tolist() == [0.0, 0.0]          # degenerate origin branch
+    lib.orc_concentric_sample_disk(1.0, 1.0, fptr(out))   # region 2: r=sy=1, theta=1 -> pi/4
+    assert np.allclose(out, [math.sqrt(0.5)] * 2, atol=1e-7)
+    lib.orc_concentric_sample_disk(0.0, 0.0, fptr(out))   # region 3: r=1, theta=5 -> 5pi/4
+    assert np.allclose(out, [-math.sqrt(0.5)] * 2, atol=1e-7)
+    lib.orc_concentric_sample_disk(1.0, 0.5, fptr(out))   # region 1, sy=0: theta = 8 -> 2pi
+    assert np.allclose(out, [1.0, 0.0], atol=1e-6)
+    rng = np.random.RandomState(1)
+    for u in rng.uniform(0, 1, (200, 2)).astype(np.float32):
+        lib.orc_concentric_sample_disk(float(u[0]), float(u[1]), fptr(out))
+        assert out[0] ** 2 + out[1] ** 2 <= 1.0 + 1e-6
+
+
+def test_uniform_sample_sphere(oracle_mod):
+    """cudalight.cu.h:66-73: z = 1-2u1, phi = 2 pi u2."""
+    lib = oracle_mod.load()
+    from pmrender.abi import fptr
+    out = np.zeros(3, np.float32)
+    lib.orc_uniform_sample_sphere(0.0, 0.25, fptr(out))
+    assert np.allclose(out, [0, 0, 1], atol=1e-7)
+    lib.orc_uniform_sample_sphere(0.5, 0.25, fptr(out))
+    assert np.allclose(out, [0, 1, 0], atol=1e-6)
+
+
+# ---- Halton --------------------------------------------------------------
+def _radical_inverse_quirk(n, base, perm):
+    """Python replica of photontracing.cu:19-31 in float32, incl. n *= invBase."""
+    val = np.float32(0)
+    inv = np.float32(1) / np.float32(base)
+    invbi = inv
+    while n > 0:
+        d = perm[n % base]
+        val = np.float32(val + np.float32(np.float32(d) * invbi))
+        n = int(np.float32(np.float32(n) * inv))
+        invbi = np.float32(invbi * inv)
+    return val
+
+
+def test_radical_inverse_identity_permutation(oracle_mod):
+    ident = np.concatenate([np.arange(b, dtype=np.uint32) for b in (2, 3, 5, 7, 11)])
+    for n, expect in [(1, [1 / 2, 1 / 3, 1 / 5, 1 / 7]), (2, [1 / 4, 2 / 3, 2 / 5, 2 / 7]),
+                      (6, [3 / 8, 2 / 9, 6 / 25, 6 / 7])]:
+        assert np.allclose(oracle_mod.halton_sample(n, ident), expect, atol=1e-7)
+
+
+def test_halton_matches_float_quirk_replica(oracle_mod):
+    perm = oracle_mod.halton_permutation(0)
+    offs = {2: 0, 3: 2, 5: 5, 7: 10}
+    rng = np.random.RandomState(7)
+    for n in list(rng.randint(0, 1 << 20, 200)) + [12582911, 12582912, 16777212, 33554428]:
+        got = oracle_mod.halton_sample(int(n), perm)
+        want = [_radical_inverse_quirk(int(n), b, perm[offs[b]:offs[b] + b]) for b in (2, 3, 5, 7)]
+        assert np.array_equal(got, np.float32(want)), n
+
+
+def test_halton_permutation_tables(oracle_mod):
+    for seed in (0, 1, 5489):
+        p = oracle_mod.halton_permutation(seed)
+        o = 0
+        for b in (2, 3, 5, 7, 11):
+            assert sorted(p[o:o + b].tolist()) == list(range(b))
+            o += b
+    assert not np.array_equal(oracle_mod.halton_permutation(0), oracle_mod.halton_permutation(1))
+
+
+# ---- intersectors ----------------------------------------------------------
+def test_triangle_intersection_kat(oracle_mod):
+    """OptiX intersect_triangle as used at cudatrianglemesh.cu:24."""
+    lib = oracle_mod.load()
+    from pmrender.abi import fptr
+    out = np.zeros(3, np.float32)
+    p0, p1, p2 = fp(0, 0, 0), fp(1, 0, 0), fp(0, 1, 0)
+    hit = lib.orc_intersect_triangle(fptr(p0), fptr(p1), fptr(p2), fptr(fp(0.25, 0.25, 1)), fptr(fp(0, 0, -1)),
+                                     0.0, 1e27, fptr(out))
+    assert hit == 1 and out.tolist() == [1.0, 0.25, 0.25]   # t, beta (p1 weight), gamma (p2 weight)
+    assert lib.orc_intersect_triangle(fptr(p0), fptr(p1), fptr(p2), fptr(fp(0.8, 0.8, 1)), fptr(fp(0, 0, -1)),
+                                      0.0, 1e27, fptr(out)) == 0   # beta+gamma > 1
+    assert lib.orc_intersect_triangle(fptr(p0), fptr(p1), fptr(p2), fptr(fp(0.25, 0.25, 1)), fptr(fp(0, 0, -1)),
+                                      0.0, 0.5, fptr(out)) == 0    # beyond tmax
+    assert lib.orc_intersect_triangle(fptr(p0), fptr(p1), fptr(p2), fptr(fp(0.25, 0.25, 1)), fptr(fp(0, 0, -1)),
+                                      1.5, 1e27, fptr(out)) == 0   # before tmin
+
+
+def test_sphere_intersection_kat(oracle_mod):
+    """cudasphere.cu:27-72: nearest root in (tmin, tmax), object space."""
+    lib = oracle_mod.load()
+    from pmrender.abi import fptr
+    I = np.eye(4, dtype=np.float32).reshape(-1)
+    t = np.zeros(1, np.float32)
+    assert lib.orc_intersect_sphere(1.0, fptr(I), fptr(I), fptr(fp(0, 0, -5)), fptr(fp(0, 0, 1)), 0.1, 1e27,
+                                    fptr(t)) == 1 and t[0] == 4.0
+    assert lib.orc_intersect_sphere(1.0, fptr(I), fptr(I), fptr(fp(0, 0, -5)), fptr(fp(0, 0, 1)), 4.5, 1e27,
+                                    fptr(t)) == 1 and t[0] == 6.0
+    assert lib.orc_intersect_sphere(1.0, fptr(I), fptr(I), fptr(fp(0, 2, -5)), fptr(fp(0, 0, 1)), 0.1, 1e27,
+                                    fptr(t)) == 0
+    T = np.eye(4, dtype=np.float32)
+    T[:3, 3] = (10, 0, 0)
+    Ti = np.eye(4, dtype=np.float32)
+    Ti[:3, 3] = (-10, 0, 0)
+    assert lib.orc_intersect_sphere(2.0, fptr(T.reshape(-1)), fptr(Ti.reshape(-1)), fptr(fp(10, 0, -5)),
+                                    fptr(fp(0, 0, 1)), 0.1, 1e27, fptr(t)) == 1 and t[0] == 3.0
+
+
+def test_disk_intersection_kat(oracle_mod):
+    """cudadisk.cu:18-50 with the uniforms of cudadisk.cpp:24-43."""
+    lib = oracle_mod.load()
+    from pmrender.abi import fptr
+    t = np.zeros(1, np.float32)
+    o, x, y, z = fp(0, 0, 0), fp(2, 0, 0), fp(0, 2, 0), fp(0, 0, 1)
+    down = fptr(fp(0, 0, -1))
+
+    def hit(inner, phimax, ro):
+        return lib.orc_intersect_disk(fptr(o), fptr(x), fptr(y), fptr(z), inner, phimax, fptr(ro), down, 0.1, 1e27,
+                                      fptr(t))
+    assert hit(0.0, 2 * math.pi, fp(1, 0, 5)) == 1 and t[0] == 5.0
+    assert hit(0.0, 2 * math.pi, fp(3, 0, 5)) == 0                # outside radius
+    assert hit(0.6, 2 * math.pi, fp(1, 0, 5)) == 0                # inside inner radius (0.5 < 0.6)
+    assert hit(0.0, math.pi, fp(0, -1, 5)) == 0                   # phi = 3pi/2 > phiMax
+    assert hit(0.0, math.pi, fp(0, 1, 5)) == 1
+
+
+# ---- PPM estimator -------------------------------------------------------
+@pytest.mark.parametrize("N,M,Nn,ratio", [(0, 10, 7, 0.7), (0, 1, 0, 0.0), (7, 3, 9, 0.9), (9, 0, 9, None)])
+def test_ppm_update_kat(oracle_mod, N, M, Nn, ratio):
+    """gathering.cu:115-125: int N' = N + 0.7 M; ratio = N'/(N+M)."""
+    lib = oracle_mod.load()
+    from pmrender.abi import fptr
+    r2, n, flux, L = fp(4.0), fp(N), fp(1, 2, 3), fp(10, 20, 30)
+    lib.orc_ppm_update(fptr(r2), fptr(n), fptr(flux), M, fptr(L), 0.7)
+    assert n[0] == Nn
+    if ratio is None:
+        assert r2[0] == 4.0 and flux.tolist() == [1, 2, 3]
+    else:
+        rt = np.float32(np.float32(Nn) / np.float32(N + M))
+        assert r2[0] == np.float32(np.float32(4.0) * rt)
+        assert np.array_equal(flux, (fp(1, 2, 3) + fp(10, 20, 30)) * rt)
+
+
+# ---- kd-tree ---------------------------------------------------------------
+def _random_photons(n, seed, valid_frac=0.8):
+    rng = np.random.RandomState(seed)
+    ph = np.zeros(n, dtype=PHOTON_DTYPE)
+    ph["bits"] = (rng.uniform(size=n) < valid_frac).astype(np.uint32)
+    ph["p"] = rng.uniform(0, 20, (n, 3)).astype(np.float32)
+    ph["p"][: n // 10, 2] = 5.0  # ties on one axis
+    ph["alpha"] = rng.uniform(0, 1, (n, 3)).astype(np.float32)
+    w = rng.normal(size=(n, 3))
+    ph["wi"] = (w / np.linalg.norm(w, axis=1, keepdims=True)).astype(np.float32)
+    return ph
+
+
+def _check_kd_invariants(nodes):
+    """pbrt KdTree: left child = node+1, subtree order by split coordinate."""
+    n = len(nodes)
+    bits = nodes["bits"]
+    axis, has_left, right = (bits >> 1) & 3, bits & 1, bits >> 3
+
+    def subtree(i):
+        out, st = [], [i]
+        while st:
+            k = st.pop()
+            out.append(k)
+            if has_left[k]:
+                st.append(k + 1)
+            if right[k] != (1 << 29) - 1:
+                st.append(int(right[k]))
+        return out
+    seen = subtree(0)
+    assert sorted(seen) == list(range(n))
+    for i in range(0, n, max(1, n // 200)):
+        if axis[i] == 3:
+            assert not has_left[i] and right[i] == (1 << 29) - 1
+            continue
+        a, s = axis[i], nodes["p"][i][axis[i]]
+        if has_left[i]:
+            assert all(nodes["p"][k][a] <= s for k in subtree(i + 1))
+        if right[i] != (1 << 29) - 1:
+            assert all(nodes["p"][k][a] >= s for k in subtree(int(right[i])))
+
+
+def test_kdtree_structure(oracle_mod):
+    ph = _random_photons(3000, 1)
+    nodes = oracle_mod.Oracle.build_kdtree(ph)
+    assert len(nodes) == int((ph["bits"] & 1).sum())
+    _check_kd_invariants(nodes)
+
+
+def test_kdtree_range_query_matches_brute_force(oracle_mod):
+    ph = _random_photons(4000, 2)
+    nodes = oracle_mod.Oracle.build_kdtree(ph)
+    valid = ph[(ph["bits"] & 1) == 1]
+    orc = oracle_mod.Oracle(nthreads=2)
+    orc.add_material(PM_MATTE, (0.5, 0.25, 1.0))
+    rng = np.random.RandomState(3)
+    recs = np.zeros(500, dtype=RECORD_DTYPE)
+    recs["pos"] = rng.uniform(0, 20, (500, 3)).astype(np.float32)
+    recs["pos"][:50] = valid["p"][:50]                       # queries exactly on photons
+    ns = rng.normal(size=(500, 3))
+    recs["ns"] = (ns / np.linalg.norm(ns, axis=1, keepdims=True)).astype(np.float32)
+    recs["radius2"] = rng.uniform(0.1, 4.0, 500).astype(np.float32)
+    part = orc.gather_partial(nodes, recs)
+    kd = np.float32([0.5, 0.25, 1.0]) * np.float32(0.31830988618379067154)
+    for i in range(len(recs)):
+        diff = recs["pos"][i][None, :] - valid["p"]           # float32, no FMA: same rounding as the oracle
+        d2 = (diff[:, 0] * diff[:, 0] + diff[:, 1] * diff[:, 1]) + diff[:, 2] * diff[:, 2]
+        inside = d2 < recs["radius2"][i]
+        assert part[i, 0] == inside.sum()
+        c = np.abs(valid["wi"][inside] @ recs["ns"][i].astype(np.float64))[:, None] * kd * valid["alpha"][inside]
+        assert np.allclose(part[i, 1:], c.sum(axis=0), rtol=1e-5, atol=1e-6)
+
+
+def test_oracle_render_deterministic_and_sane(oracle_mod):
+    from pmrender import scenes
+    sc = scenes.cornell_box(32, 32)
+    a = sc.load_into(oracle_mod.Oracle(nthreads=1))
+    b = sc.load_into(oracle_mod.Oracle(nthreads=4))
+    p = RenderParams.defaults(paths_per_pass=4096)
+    ia, sa = a.render(p)
+    ib, sb = b.render(p)
+    assert np.array_equal(ia.view(np.uint32), ib.view(np.uint32))   # thread-count independent
+    assert sa["photons_valid"] == sb["photons_valid"] > 0
+    assert np.isfinite(ia).all() and (ia >= 0).all()
+    assert ia.max() == pytest.approx(17.0)   # pixels seeing the emitter: Le = 17 (lightL, cudalight.cu.h:128-138)
