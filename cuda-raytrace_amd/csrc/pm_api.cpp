@@ -73,6 +73,7 @@ struct Ctx {
         d_spheres, d_materials, d_lights, d_rays, d_rand2d;
     SceneDev S{};
     float bbox_lo[3] = {0, 0, 0}, bbox_hi[3] = {0, 0, 0};
+    double emit_max = 1.0, kd_max = 1.0; /* bounds for the fixed-point flux scale */
     int bvh_depth = 0;
     /* records */
     DevBuf d_pos, d_nrm, d_state, d_n, d_dl;
@@ -81,8 +82,7 @@ struct Ctx {
     DevBuf d_slots;
     int64_t slots_used = 0;
     /* photon buckets */
-    DevBuf d_keys, d_vals, d_keys2, d_vals2, d_cell_count, d_cell_start, d_nvalid, d_pha, d_phb, d_phc,
-        d_sort_tmp, d_scan_tmp;
+    DevBuf d_count, d_cell_start, d_scratch, d_pha, d_phb, d_phc;
     GridDesc grid{};
     int map_kind = -1;
     int64_t map_slots = 0;
@@ -210,6 +210,15 @@ GatherParams gather_params(Ctx *c, const pm_render_params *p) {
     G.ph_a = c->d_pha.as<float4>(); G.ph_b = c->d_phb.as<float4>(); G.ph_c = c->d_phc.as<float>();
     G.kd_nodes = c->d_kd.as<pm_photon>(); G.kd_count = c->kd_count;
     G.counters = c->d_counters.as<unsigned long long>();
+    /* fixed-point scale 2^S: a single contribution is bounded by
+     * alpha_max * Kd_max / pi with alpha_max = emission * Kd_max^mpc (Lambert
+     * weight ~Kd, specular weight 1); x4 headroom; 2^40 per contribution
+     * leaves 2^23 contributions per record before int64 overflow */
+    double cmax = c->emit_max * std::pow(c->kd_max, (double)p->max_photon_count) * (c->kd_max / M_PI) * 4.0;
+    int S = (int)std::floor(std::log2(std::ldexp(1.0, 40) / std::max(cmax, 1e-30)));
+    S = std::max(-60, std::min(60, S));
+    G.fx_scale = (float)std::ldexp(1.0, S);
+    G.fx_inv = std::ldexp(1.0, -S);
     return G;
 }
 
@@ -284,9 +293,9 @@ void pm_destroy(void *ptr) {
     DevBuf *bufs[] = {&c->d_nodes, &c->d_refs, &c->d_tri_geo, &c->d_tri_info, &c->d_tri_id, &c->d_verts,
                       &c->d_norms, &c->d_uvs, &c->d_meshes, &c->d_disks, &c->d_spheres, &c->d_materials,
                       &c->d_lights, &c->d_rays, &c->d_rand2d, &c->d_pos, &c->d_nrm, &c->d_state, &c->d_n,
-                      &c->d_dl, &c->d_slots, &c->d_keys, &c->d_vals, &c->d_keys2, &c->d_vals2,
-                      &c->d_cell_count, &c->d_cell_start, &c->d_nvalid, &c->d_pha, &c->d_phb, &c->d_phc,
-                      &c->d_sort_tmp, &c->d_scan_tmp, &c->d_kd, &c->d_out, &c->d_counters};
+                      &c->d_dl, &c->d_slots, &c->d_count, &c->d_scratch,
+                      &c->d_cell_start, &c->d_pha, &c->d_phb, &c->d_phc,
+                      &c->d_kd, &c->d_out, &c->d_counters};
     for (DevBuf *b : bufs) b->release();
     hipStreamDestroy(c->stream);
     delete c;
@@ -550,7 +559,19 @@ int pm_commit(void *ptr) {
     S.meshes = c->d_meshes.as<int4>(); S.disks = c->d_disks.as<float4>(); S.spheres = c->d_spheres.as<float4>();
     S.materials = c->d_materials.as<float4>(); S.lights = c->d_lights.as<LightDev>();
     S.n_lights = (int)c->lights.size(); S.n_nodes = (int)nodes4.size() / 4;
+    /* a push happens only when descending a level, so depth + 1 entries suffice;
+     * sizing the LDS stack by the actual tree keeps occupancy VGPR-bound */
+    S.stack_depth = std::min(BVH_STACK, std::max(2, c->bvh_depth + 2));
     for (int a = 0; a < 3; ++a) { c->bbox_lo[a] = blo[a]; c->bbox_hi[a] = bhi[a]; }
+    double em = 0.0, kd = 1.0;
+    for (const LightDev &L : c->lights) {
+        double le = std::max({std::fabs(L.le.x), std::fabs(L.le.y), std::fabs(L.le.z)});
+        em = std::max(em, fbits_h(L.o_type.w) == PM_LIGHT_POINT ? le * 4.0 * M_PI : le * L.n_area.w * 2.0 * M_PI);
+    }
+    for (const float4 &m : c->materials)
+        if (fbits_h(m.w) == PM_MATTE) kd = std::max({kd, (double)m.x, (double)m.y, (double)m.z});
+    c->emit_max = std::max(em, 1e-30);
+    c->kd_max = kd;
     c->committed = true;
     return PM_OK;
 }
@@ -686,34 +707,21 @@ int pm_build_photon_map(void *ptr, const pm_render_params *p, int64_t n_slots, v
     g.inv_cs = 1.0f / cs;
     g.dx = (int)dims[0]; g.dy = (int)dims[1]; g.dz = (int)dims[2];
     g.ncells = (uint32_t)(dims[0] * dims[1] * dims[2]);
-    int end_bit = 1;
-    while (end_bit < 32 && ((uint64_t)1 << end_bit) <= g.ncells) ++end_bit;
     const size_t n = (size_t)n_slots;
-    HIPCHK(c, c->d_keys.ensure(n * 4)); HIPCHK(c, c->d_vals.ensure(n * 4));
-    HIPCHK(c, c->d_keys2.ensure(n * 4)); HIPCHK(c, c->d_vals2.ensure(n * 4));
-    HIPCHK(c, c->d_cell_count.ensure(((size_t)g.ncells + 1) * 4));
+    HIPCHK(c, c->d_count.ensure(((size_t)g.ncells + 1) * 4));
     HIPCHK(c, c->d_cell_start.ensure(((size_t)g.ncells + 1) * 4));
-    HIPCHK(c, c->d_nvalid.ensure(16));
+    HIPCHK(c, c->d_scratch.ensure(bucket_scratch_words(n_slots, g.ncells) * 4));
     HIPCHK(c, c->d_pha.ensure(n * 16)); HIPCHK(c, c->d_phb.ensure(n * 16)); HIPCHK(c, c->d_phc.ensure(n * 4));
-    size_t sort_b = grid_sort_temp_bytes((int64_t)n, g.ncells), scan_b = grid_scan_temp_bytes(g.ncells);
-    HIPCHK(c, c->d_sort_tmp.ensure(sort_b)); HIPCHK(c, c->d_scan_tmp.ensure(scan_b));
     timer_begin(c, "build", s);
-    HIPCHK(c, hipMemsetAsync(c->d_cell_count.p, 0, ((size_t)g.ncells + 1) * 4, s));
-    HIPCHK(c, hipMemsetAsync(c->d_nvalid.p, 0, 4, s));
-    HIPCHK(c, launch_grid_keys(c->d_slots.as<pm_photon>(), n_slots, g, c->d_keys.as<uint32_t>(), c->d_vals.as<uint32_t>(),
-                               c->d_cell_count.as<uint32_t>(), c->d_nvalid.as<uint32_t>(), s));
-    HIPCHK(c, launch_grid_sort(c->d_sort_tmp.p, c->d_sort_tmp.bytes, c->d_keys.as<uint32_t>(), c->d_keys2.as<uint32_t>(),
-                               c->d_vals.as<uint32_t>(), c->d_vals2.as<uint32_t>(), n_slots, end_bit, s));
-    HIPCHK(c, launch_grid_scan(c->d_scan_tmp.p, c->d_scan_tmp.bytes, c->d_cell_count.as<uint32_t>(),
-                               c->d_cell_start.as<uint32_t>(), g.ncells, s));
-    HIPCHK(c, launch_grid_scatter(c->d_slots.as<pm_photon>(), c->d_vals2.as<uint32_t>(), c->d_nvalid.as<uint32_t>(),
-                                  n_slots, c->d_pha.as<float4>(), c->d_phb.as<float4>(), c->d_phc.as<float>(), s));
+    HIPCHK(c, launch_bucket_build(c->d_slots.as<pm_photon>(), n_slots, g, c->d_count.as<uint32_t>(),
+                                  c->d_cell_start.as<uint32_t>(), c->d_scratch.as<uint32_t>(), c->d_pha.as<float4>(),
+                                  c->d_phb.as<float4>(), c->d_phc.as<float>(), s));
     timer_end(c, "build", s);
     c->map_kind = PM_GATHER_GRID;
     return PM_OK;
 }
 
-static int gather_common(Ctx *c, const pm_render_params *p, float4 *partial, int64_t rec_begin, int64_t rec_count,
+static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, int64_t rec_begin, int64_t rec_count,
                          void *stream) {
     int rc;
     if ((rc = check_params(c, p))) return rc;
@@ -745,7 +753,7 @@ int pm_gather_range(void *ptr, const pm_render_params *p, int64_t rec_begin, int
 int pm_gather_partial(void *ptr, const pm_render_params *p, void *d_partial, void *stream) {
     GETCTX(ptr);
     if (!d_partial) FAIL(c, PM_ERR_INVALID, "null partial buffer");
-    return gather_common(c, p, (float4 *)d_partial, 0, c->nrec, stream);
+    return gather_common(c, p, (long long *)d_partial, 0, c->nrec, stream);
 }
 
 int pm_ppm_update(void *ptr, const pm_render_params *p, const void *d_partial, int64_t rec_begin, int64_t rec_count,
@@ -758,8 +766,24 @@ int pm_ppm_update(void *ptr, const pm_render_params *p, const void *d_partial, i
     hipStream_t s = pick(c, stream);
     GatherParams G = gather_params(c, p);
     timer_begin(c, "update", s);
-    HIPCHK(c, launch_ppm_update(G, (const float4 *)d_partial, rec_begin, rec_count, s));
+    HIPCHK(c, launch_ppm_update(G, (const long long *)d_partial, rec_begin, rec_count, s));
     timer_end(c, "update", s);
+    return PM_OK;
+}
+
+int pm_get_radius2(void *ptr, int64_t rec_begin, int64_t rec_count, void *d_out, void *stream) {
+    GETCTX(ptr);
+    if (!d_out || rec_begin < 0 || rec_count < 0 || rec_begin + rec_count > c->nrec)
+        FAIL(c, PM_ERR_INVALID, "bad radius2 range");
+    HIPCHK(c, launch_radius2_io(recs(c), (float *)d_out, rec_begin, rec_count, 0, pick(c, stream)));
+    return PM_OK;
+}
+
+int pm_set_radius2(void *ptr, const void *d_in, int64_t rec_begin, int64_t rec_count, void *stream) {
+    GETCTX(ptr);
+    if (!d_in || rec_begin < 0 || rec_count < 0 || rec_begin + rec_count > c->nrec)
+        FAIL(c, PM_ERR_INVALID, "bad radius2 range");
+    HIPCHK(c, launch_radius2_io(recs(c), (float *)d_in, rec_begin, rec_count, 1, pick(c, stream)));
     return PM_OK;
 }
 
@@ -798,7 +822,7 @@ int pm_render(void *ptr, const pm_render_params *p, float *out_rgb, pm_stats *st
         t_build += timer_ms(c, "build");
         if (p->gather_structure == PM_GATHER_GRID) {
             uint32_t nv = 0;
-            HIPCHK(c, hipMemcpyAsync(&nv, c->d_nvalid.p, 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipMemcpyAsync(&nv, c->d_cell_start.as<uint32_t>() + c->grid.ncells, 4, hipMemcpyDeviceToHost, s));
             HIPCHK(c, hipStreamSynchronize(s));
             nvalid = nv;
         } else {

@@ -1,0 +1,183 @@
+/*
+ * pm_bucket.hip — photon-map build on the GPU (replaces CreatePhotonMap,
+ * photon_mapping/photonmappingrenderer.cpp:150-180, which copies the slots to
+ * the host and builds a pbrt KdTree there).
+ *
+ * Photon buckets = a dense uniform grid over the scene box, cell edge
+ * >= 2 r_max, photons stored cell-contiguously:
+ *   1. k_bucket_count  cell key of each valid slot; rank = returning atomicAdd
+ *                      on that cell's counter (atomics spread over ~10^5
+ *                      cells; there is no single hot word)
+ *   2. exclusive scan  of the ncells+1 counters (reduce / top / down kernels,
+ *                      16-B vector loads) -> cell_start; cell_start[ncells] =
+ *                      number of valid photons
+ *   3. k_bucket_fill   slot -> cell_start[key] + rank, written straight into
+ *                      the SoA arrays the gather streams (ph_a, ph_b, ph_c)
+ * The order inside a bucket depends on atomic arrival order. Results do not:
+ * the bucket gather (pm_gather.hip) sums flux in exact 64-bit fixed point
+ * and counts photons as integers, so any order gives identical bits.
+ */
+#include <hip/hip_runtime.h>
+
+#include "pm_kernels.h"
+
+#pragma clang fp contract(off)
+
+namespace pm {
+
+constexpr int SCAN_BLOCK = 256, SCAN_ITEMS = 16, SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS; /* 4096 u32 per block */
+
+__global__ __launch_bounds__(256) void k_bucket_count(const pm_photon *slots, int64_t n, GridDesc g,
+                                                      uint32_t *count, uint32_t *key_out, uint32_t *rank_out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float2 *q = reinterpret_cast<const float2 *>(slots + i);
+    const float2 a = q[0], b = q[1];
+    uint32_t key = 0xffffffffu, rank = 0u;
+    if ((uint32_t)__float_as_int(a.x) & 1u) {
+        const uint32_t cx = cell_axis(a.y, g.gx, g.inv_cs, g.dx);
+        const uint32_t cy = cell_axis(b.x, g.gy, g.inv_cs, g.dy);
+        const uint32_t cz = cell_axis(b.y, g.gz, g.inv_cs, g.dz);
+        key = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx + cx;
+        rank = atomicAdd(&count[key], 1u);
+    }
+    key_out[i] = key;
+    rank_out[i] = rank;
+}
+
+PMD uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t t = __shfl_up(v, off);
+        if (lane >= off) v += t;
+    }
+    return v;
+}
+
+/* block-wide exclusive scan of one value per thread; returns the block total */
+PMD uint32_t block_excl_scan(uint32_t v, uint32_t *excl, uint32_t *lds /* >= 4 */) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) lds[wave] = inc;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < SCAN_BLOCK / 64; ++w) {
+        uint32_t s = lds[w];
+        if (w < wave) off += s;
+        tot += s;
+    }
+    __syncthreads();
+    *excl = off + inc - v;
+    return tot;
+}
+
+/* per-tile sums; thread t owns 16 contiguous words (four 16-B loads) */
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_reduce(const uint32_t *in, int64_t n, uint32_t *sums) {
+    __shared__ uint32_t lds[4];
+    const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
+    uint32_t s = 0;
+    if (base + SCAN_ITEMS <= n) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(in + base);
+#pragma unroll
+        for (int k = 0; k < SCAN_ITEMS / 4; ++k) { uint4 v = p[k]; s += v.x + v.y + v.z + v.w; }
+    } else {
+        for (int64_t k = base; k < n; ++k) s += in[k];
+    }
+    uint32_t excl;
+    uint32_t tot = block_excl_scan(s, &excl, lds);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+/* exclusive scan of the tile sums, one block, any count */
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_top(uint32_t *sums, int nt) {
+    __shared__ uint32_t lds[4];
+    uint32_t carry = 0;
+    for (int b = 0; b < nt; b += SCAN_BLOCK) {
+        const int i = b + threadIdx.x;
+        const uint32_t v = i < nt ? sums[i] : 0u;
+        uint32_t excl;
+        const uint32_t tot = block_excl_scan(v, &excl, lds);
+        if (i < nt) sums[i] = carry + excl;
+        carry += tot;
+    }
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_down(const uint32_t *in, int64_t n, const uint32_t *sums,
+                                                          uint32_t *out) {
+    __shared__ uint32_t lds[4];
+    const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
+    uint32_t v[SCAN_ITEMS];
+    const bool full = base + SCAN_ITEMS <= n;
+    if (full) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(in + base);
+#pragma unroll
+        for (int k = 0; k < SCAN_ITEMS / 4; ++k) {
+            uint4 q = p[k];
+            v[4 * k] = q.x; v[4 * k + 1] = q.y; v[4 * k + 2] = q.z; v[4 * k + 3] = q.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < SCAN_ITEMS; ++k) v[k] = (base + k < n) ? in[base + k] : 0u;
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) s += v[k];
+    uint32_t excl;
+    block_excl_scan(s, &excl, lds);
+    uint32_t run = sums[blockIdx.x] + excl;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) { uint32_t t = v[k]; v[k] = run; run += t; }
+    if (full) {
+        uint4 *p = reinterpret_cast<uint4 *>(out + base);
+#pragma unroll
+        for (int k = 0; k < SCAN_ITEMS / 4; ++k) p[k] = make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < SCAN_ITEMS; ++k)
+            if (base + k < n) out[base + k] = v[k];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_bucket_fill(const pm_photon *slots, int64_t n, const uint32_t *key,
+                                                     const uint32_t *rank, const uint32_t *cell_start, float4 *ph_a,
+                                                     float4 *ph_b, float *ph_c) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = key[i];
+    if (k == 0xffffffffu) return;
+    const uint32_t dst = cell_start[k] + rank[i];
+    const float2 *q = reinterpret_cast<const float2 *>(slots + i);
+    const float2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
+    /* a = (bits, p.x) b = (p.y, p.z) c = (alpha.x, alpha.y) d = (alpha.z, wi.x) e = (wi.y, wi.z) */
+    ph_a[dst] = make_float4(a.y, b.x, b.y, d.y);
+    ph_b[dst] = make_float4(c.x, c.y, d.x, e.x);
+    ph_c[dst] = e.y;
+}
+
+size_t bucket_scratch_words(int64_t n_slots, uint32_t ncells) {
+    const int64_t ntile = ((int64_t)ncells + 1 + SCAN_TILE - 1) / SCAN_TILE;
+    return (size_t)(2 * n_slots + ntile + 16);
+}
+
+hipError_t launch_bucket_build(const pm_photon *slots, int64_t n, GridDesc g, uint32_t *count, uint32_t *cell_start,
+                               uint32_t *scratch, float4 *ph_a, float4 *ph_b, float *ph_c, hipStream_t s) {
+    const int64_t nc = (int64_t)g.ncells + 1; /* last counter stays 0 -> cell_start[ncells] = total */
+    hipError_t e = hipMemsetAsync(count, 0, (size_t)nc * 4, s);
+    if (e != hipSuccess) return e;
+    uint32_t *key = scratch, *rank = scratch + n, *sums = scratch + 2 * n;
+    if (n > 0)
+        hipLaunchKernelGGL(k_bucket_count, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slots, n, g, count, key,
+                           rank);
+    const int ntile = (int)((nc + SCAN_TILE - 1) / SCAN_TILE);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(ntile), dim3(SCAN_BLOCK), 0, s, count, nc, sums);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_BLOCK), 0, s, sums, ntile);
+    hipLaunchKernelGGL(k_scan_down, dim3(ntile), dim3(SCAN_BLOCK), 0, s, count, nc, sums, cell_start);
+    if (n > 0)
+        hipLaunchKernelGGL(k_bucket_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slots, n, key, rank,
+                           cell_start, ph_a, ph_b, ph_c);
+    return hipGetLastError();
+}
+
+} // namespace pm

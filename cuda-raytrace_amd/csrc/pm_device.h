@@ -72,6 +72,7 @@ struct SceneDev {
     const LightDev *lights;
     int n_lights;
     int n_nodes;
+    int stack_depth; /* LDS stack entries per lane (>= BVH depth, <= BVH_STACK_DEPTH) */
 };
 
 struct Ray { v3 o, d; float tmin, tmax; };
@@ -101,8 +102,10 @@ PMD void concentric_sample_disk(float u1, float u2, float *dx, float *dy) {
         else { r = -sy; theta = 6.0f + sx / r; }
     }
     theta = (float)((double)theta * (M_PI / 4.f));
-    *dx = r * pmdm_cosf(theta);
-    *dy = r * pmdm_sinf(theta);
+    float st, ct;
+    pmdm_sincosf(theta, &st, &ct);
+    *dx = r * ct;
+    *dy = r * st;
 }
 
 /* cudalight.cu.h:66-73 */
@@ -110,7 +113,9 @@ PMD v3 uniform_sample_sphere(float u1, float u2) {
     float z = 1.f - 2.f * u1;
     float r = sqrtf(fmaxf(0.f, 1.f - z * z));
     float phi = (float)(2.f * M_PI * (double)u2);
-    return mk(r * pmdm_cosf(phi), r * pmdm_sinf(phi), z);
+    float sp, cp;
+    pmdm_sincosf(phi, &sp, &cp);
+    return mk(r * cp, r * sp, z);
 }
 
 /* photontracing.cu:19-43 — permutation table in LDS/constant, 28 uints */
@@ -276,7 +281,7 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
             if (leaf_isect<ANY>(S, (uint32_t)~ch.y, (uint32_t)ch.w, ray, best)) return true;
             hr = false;
         }
-        if (hl && hr && sp < BVH_STACK_DEPTH) {
+        if (hl && hr && sp < S.stack_depth) {
             int nearc = ch.x, farc = ch.y;
             if (tr < tl) { nearc = ch.y; farc = ch.x; }
             stack[sp * stride] = farc;

@@ -1,0 +1,329 @@
+/*
+ * pm_gather.hip — fixed-radius range query + PPM update (gathering.cu:17-126)
+ * over photon buckets (grid) or the reference kd-tree layout, the PPM update
+ * of reduced partials, final radiance + sanitisation (gathering.cu:129-146,
+ * photonmappingrenderer.cpp:251-268) and the per-step record reset.
+ *
+ * wave64; 8x8 pixel tiles map onto one wave so a wave's gather points are
+ * spatially coherent and share photon buckets in L1/L2.
+ */
+#include <hip/hip_runtime.h>
+
+#include "pm_kernels.h"
+
+#pragma clang fp contract(off)
+
+namespace pm {
+/* ====================================================================== */
+/* gather                                                                 */
+/* ====================================================================== */
+PMD unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+/* census counters [visited, in radius, bucket rows, active records]: one
+ * atomic per wave (only in counting launches, never in timed ones) */
+PMD void count4(unsigned long long *c, unsigned long long a, unsigned long long b, unsigned long long d,
+                unsigned long long e) {
+    a = wave_sum(a); b = wave_sum(b); d = wave_sum(d); e = wave_sum(e);
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&c[0], a); atomicAdd(&c[1], b); atomicAdd(&c[2], d); atomicAdd(&c[3], e);
+    }
+}
+
+/* gathering.cu:104-126 PPM update */
+PMD void ppm_apply(float4 &st, float &N, int M, v3 L, float alpha) {
+    if (M > 0) {
+        int totalPhotons = N + alpha * M;
+        float ratio = totalPhotons / (N + M);
+        st.w = st.w * ratio;
+        v3 flux = (xyz(st) + L) * ratio;
+        st.x = flux.x; st.y = flux.y; st.z = flux.z;
+        N = totalPhotons;
+    }
+}
+
+/* Exact, order-independent flux sums for the bucket gather: each photon's
+ * contribution is rounded once to a 64-bit fixed-point integer (scale 2^S
+ * chosen per scene so that 2^23 maximal contributions fit, pm_api.cpp
+ * fx_scale) and integers add associatively. The bucket order (atomic
+ * arrival order in pm_bucket.hip) and the number of GPUs that hold the
+ * photons therefore never change a bit of the result. */
+struct Fx3 { long long x, y, z; };
+PMD long long to_fx(float c, float scale) { return (long long)rintf(c * scale); }
+PMD void write_partial(long long *p, int M, Fx3 L) {
+    longlong2 *q = reinterpret_cast<longlong2 *>(p);
+    q[0] = make_longlong2((long long)M, L.x);
+    q[1] = make_longlong2(L.y, L.z);
+}
+
+/* Fixed-radius query over photon buckets. Every photon with
+ * d^2 < r^2 is inside the visited cells because the cell range is taken
+ * over [p - r', p + r'] with r' slightly larger than sqrt(r^2). */
+template <int PARTIAL, int COUNT>
+__global__ __launch_bounds__(GATHER_BLOCK) void k_gather_grid(GatherParams P) {
+    const int64_t r = P.rec_begin + (int64_t)blockIdx.x * GATHER_BLOCK + threadIdx.x;
+    unsigned long long vis = 0, hits = 0, rows = 0, act = 0;
+    if (r < P.rec_end) {
+        float4 pos = P.R.pos[r];
+        uint32_t flags = (uint32_t)__float_as_int(pos.w);
+        if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) {
+            if (PARTIAL) write_partial(P.partial + 4 * r, 0, Fx3{0, 0, 0});
+        } else {
+            float4 st = P.R.state[r];
+            float4 nrm = P.R.nrm[r];
+            const float r2 = st.w;
+            float4 m = P.materials[__float_as_int(nrm.w)];
+            v3 fv = __float_as_int(m.w) == PM_MATTE ? xyz(m) * INV_PI : mk(0.f, 0.f, 0.f);
+            const v3 p = xyz(pos), ns = xyz(nrm);
+            int M = 0;
+            Fx3 Lf{0, 0, 0};
+            const float sc = P.fx_scale;
+            if (r2 > 0.f) {
+                const GridDesc &g = P.grid;
+                const float rq = sqrtf(r2) * 1.0001f + 1e-4f;
+                uint32_t x0 = cell_axis(p.x - rq, g.gx, g.inv_cs, g.dx), x1 = cell_axis(p.x + rq, g.gx, g.inv_cs, g.dx);
+                uint32_t y0 = cell_axis(p.y - rq, g.gy, g.inv_cs, g.dy), y1 = cell_axis(p.y + rq, g.gy, g.inv_cs, g.dy);
+                uint32_t z0 = cell_axis(p.z - rq, g.gz, g.inv_cs, g.dz), z1 = cell_axis(p.z + rq, g.gz, g.inv_cs, g.dz);
+                for (uint32_t cz = z0; cz <= z1; ++cz) {
+                    for (uint32_t cy = y0; cy <= y1; ++cy) {
+                        uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+                        uint32_t b = P.cell_start[row + x0], e = P.cell_start[row + x1 + 1];
+                        if (COUNT) { vis += e - b; rows++; }
+                        for (uint32_t j = b; j < e; ++j) {
+                            float4 a = P.ph_a[j];
+                            v3 diff = p - xyz(a);
+                            float dist2 = diff.x * diff.x + diff.y * diff.y + diff.z * diff.z;
+                            if (dist2 < r2) {
+                                M++;
+                                float4 bb = P.ph_b[j];
+                                float wz = P.ph_c[j];
+                                v3 wi = mk(a.w, bb.w, wz);
+                                v3 c = fabsf(dot(ns, wi)) * fv * xyz(bb); /* processPhoton, gathering.cu:17-23 */
+                                Lf.x += to_fx(c.x, sc); Lf.y += to_fx(c.y, sc); Lf.z += to_fx(c.z, sc);
+                            }
+                        }
+                    }
+                }
+            }
+            if (COUNT) { hits += (unsigned long long)M; act++; }
+            if (PARTIAL) {
+                write_partial(P.partial + 4 * r, M, Lf);
+            } else {
+                const double inv = P.fx_inv;
+                v3 L = mk((float)((double)Lf.x * inv), (float)((double)Lf.y * inv), (float)((double)Lf.z * inv));
+                float N = P.R.n[r];
+                ppm_apply(st, N, M, L, P.ppm_alpha);
+                if (M > 0) { P.R.state[r] = st; P.R.n[r] = N; }
+            }
+        }
+    }
+    if (COUNT) count4(P.counters, vis, hits, rows, act);
+}
+
+/* kd-tree range query in the reference layout (gathering.cu:25-96):
+ * same visiting order, same accumulation order -> bit-exact with it. */
+template <int PARTIAL, int COUNT>
+__global__ __launch_bounds__(GATHER_BLOCK) void k_gather_kd(GatherParams P) {
+    __shared__ uint32_t stk[KD_STACK * GATHER_BLOCK];
+    uint32_t *stack = stk + threadIdx.x;
+    const int64_t r = P.rec_begin + (int64_t)blockIdx.x * GATHER_BLOCK + threadIdx.x;
+    unsigned long long vis = 0, hits = 0, rows = 0, act = 0;
+    if (r < P.rec_end) {
+        float4 pos = P.R.pos[r];
+        uint32_t flags = (uint32_t)__float_as_int(pos.w);
+        if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) {
+            if (PARTIAL) write_partial(P.partial + 4 * r, 0, Fx3{0, 0, 0});
+        } else {
+            float4 st = P.R.state[r];
+            float4 nrm = P.R.nrm[r];
+            const float maxDist2 = st.w;
+            float4 m = P.materials[__float_as_int(nrm.w)];
+            v3 fv = __float_as_int(m.w) == PM_MATTE ? xyz(m) * INV_PI : mk(0.f, 0.f, 0.f);
+            const v3 p = xyz(pos), ns = xyz(nrm);
+            int M = 0;
+            v3 L = mk(0.f, 0.f, 0.f);
+            if (P.kd_count > 0) {
+                int sp = 0;
+                uint32_t nodeNum = 0;
+                stack[0] = 0; sp = 1;
+                int64_t guard = 0; /* each node is visited at most once */
+                do {
+                    if (++guard > P.kd_count || nodeNum >= (uint64_t)P.kd_count) break;
+                    const float2 *q = reinterpret_cast<const float2 *>(P.kd_nodes + nodeNum);
+                    float2 q0 = q[0], q1 = q[1];
+                    uint32_t bits = (uint32_t)__float_as_int(q0.x);
+                    uint32_t axis = (bits >> 1) & 3u, hasLeft = bits & 1u, right = bits >> 3;
+                    v3 np = mk(q0.y, q1.x, q1.y);
+                    v3 diff = p - np;
+                    float dist2 = diff.x * diff.x + diff.y * diff.y + diff.z * diff.z;
+                    if (COUNT) vis++;
+                    if (dist2 < maxDist2) {
+                        M++;
+                        float2 q2 = q[2], q3 = q[3], q4 = q[4];
+                        v3 al = mk(q2.x, q2.y, q3.x), wi = mk(q3.y, q4.x, q4.y);
+                        L = L + fabsf(dot(ns, wi)) * fv * al;
+                    }
+                    if (axis < 3) {
+                        float pa = comp(p, (int)axis), na = comp(np, (int)axis);
+                        float d2 = (pa - na) * (pa - na);
+                        if (pa <= na) {
+                            if (d2 < maxDist2 && right < PM_PHOTON_MAX_RIGHT_CHILD && sp < KD_STACK) { stack[sp * GATHER_BLOCK] = right; ++sp; }
+                            if (hasLeft) nodeNum = nodeNum + 1; else { --sp; nodeNum = stack[sp * GATHER_BLOCK]; }
+                        } else {
+                            if (d2 < maxDist2 && hasLeft && sp < KD_STACK) { stack[sp * GATHER_BLOCK] = nodeNum + 1; ++sp; }
+                            if (right < PM_PHOTON_MAX_RIGHT_CHILD) nodeNum = right;
+                            else { --sp; nodeNum = stack[sp * GATHER_BLOCK]; }
+                        }
+                    } else {
+                        --sp;
+                        nodeNum = stack[sp * GATHER_BLOCK];
+                    }
+                } while (nodeNum);
+            }
+            if (COUNT) { hits += (unsigned long long)M; act++; }
+            if (PARTIAL) {
+                const float sc = P.fx_scale;
+                write_partial(P.partial + 4 * r, M, Fx3{to_fx(L.x, sc), to_fx(L.y, sc), to_fx(L.z, sc)});
+            } else {
+                float N = P.R.n[r];
+                ppm_apply(st, N, M, L, P.ppm_alpha);
+                if (M > 0) { P.R.state[r] = st; P.R.n[r] = N; }
+            }
+        }
+    }
+    if (COUNT) count4(P.counters, vis, hits, rows, act);
+}
+
+template <int STRUCT, int PARTIAL, int COUNT>
+static void launch_g(const GatherParams &p, hipStream_t s) {
+    unsigned grid = (unsigned)((p.rec_end - p.rec_begin + GATHER_BLOCK - 1) / GATHER_BLOCK);
+    if (STRUCT == PM_GATHER_GRID)
+        hipLaunchKernelGGL((k_gather_grid<PARTIAL, COUNT>), dim3(grid), dim3(GATHER_BLOCK), 0, s, p);
+    else
+        hipLaunchKernelGGL((k_gather_kd<PARTIAL, COUNT>), dim3(grid), dim3(GATHER_BLOCK), 0, s, p);
+}
+
+hipError_t launch_gather(const GatherParams &p, int structure, int partial, int count, hipStream_t s) {
+    if (p.rec_end <= p.rec_begin) return hipSuccess;
+    int key = (structure ? 4 : 0) | (partial ? 2 : 0) | (count ? 1 : 0);
+    switch (key) {
+    case 0: launch_g<0, 0, 0>(p, s); break;
+    case 1: launch_g<0, 0, 1>(p, s); break;
+    case 2: launch_g<0, 1, 0>(p, s); break;
+    case 3: launch_g<0, 1, 1>(p, s); break;
+    case 4: launch_g<1, 0, 0>(p, s); break;
+    case 5: launch_g<1, 0, 1>(p, s); break;
+    case 6: launch_g<1, 1, 0>(p, s); break;
+    default: launch_g<1, 1, 1>(p, s); break;
+    }
+    return hipGetLastError();
+}
+
+/* radius^2 of a record range to / from a contiguous float array: after the
+ * owner's PPM update every rank needs the new radii for the next pass's
+ * range queries (pmrender/dist.py, "reduce" exchange) */
+__global__ __launch_bounds__(256) void k_radius2_io(RecordsDev R, float *buf, int64_t rec_begin, int64_t rec_count,
+                                                    int to_records) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= rec_count) return;
+    const int64_t r = rec_begin + i;
+    if (to_records) R.state[r].w = buf[i];
+    else buf[i] = R.state[r].w;
+}
+
+hipError_t launch_radius2_io(const RecordsDev &R, float *buf, int64_t rec_begin, int64_t rec_count, int to_records,
+                             hipStream_t s) {
+    if (rec_count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_radius2_io, dim3((unsigned)((rec_count + 255) / 256)), dim3(256), 0, s, R, buf, rec_begin,
+                       rec_count, to_records);
+    return hipGetLastError();
+}
+
+/* PPM update from summed partials (M, L in fixed point), record chunk */
+__global__ __launch_bounds__(256) void k_ppm_update(RecordsDev R, const long long *partial, int64_t rec_begin,
+                                                    int64_t rec_count, float alpha, double inv) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= rec_count) return;
+    const int64_t r = rec_begin + i;
+    uint32_t flags = (uint32_t)__float_as_int(R.pos[r].w);
+    if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) return;
+    const longlong2 *q = reinterpret_cast<const longlong2 *>(partial + 4 * i);
+    const longlong2 a = q[0], b = q[1];
+    const int M = (int)a.x;
+    if (M <= 0) return;
+    float4 st = R.state[r];
+    float N = R.n[r];
+    v3 L = mk((float)((double)a.y * inv), (float)((double)b.x * inv), (float)((double)b.y * inv));
+    ppm_apply(st, N, M, L, alpha);
+    R.state[r] = st;
+    R.n[r] = N;
+}
+
+hipError_t launch_ppm_update(const GatherParams &p, const long long *partial, int64_t rec_begin, int64_t rec_count,
+                             hipStream_t s) {
+    if (rec_count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ppm_update, dim3((unsigned)((rec_count + 255) / 256)), dim3(256), 0, s, p.R, partial,
+                       rec_begin, rec_count, p.ppm_alpha, p.fx_inv);
+    return hipGetLastError();
+}
+
+/* ====================================================================== */
+/* final gathering                                                        */
+/* ====================================================================== */
+__global__ __launch_bounds__(256) void k_final(FinalParams P) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= P.rec_count) return;
+    const int64_t r = P.rec_begin + i;
+    int64_t o = i;
+    if (P.raster) {
+        int px, py;
+        rec_to_pixel(r, P.W, &px, &py);
+        uint32_t fl = (uint32_t)__float_as_int(P.R.pos[r].w);
+        if (fl & PM_REC_INVALID) return;
+        o = (int64_t)py * P.W + px;
+    }
+    float4 pos = P.R.pos[r];
+    uint32_t flags = (uint32_t)__float_as_int(pos.w);
+    v3 out = mk(0.f, 0.f, 0.f);
+    if (!(flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID))) {
+        float4 dl = P.R.dl[r], st = P.R.state[r];
+        float N = P.R.n[r];
+        v3 IDL = mk(0.f, 0.f, 0.f);
+        if (N != 0) IDL = xyz(st) * INV_PI / (st.w * P.emitted);
+        out = xyz(dl) + IDL;
+        float y = 0.212671f * out.x + 0.715160f * out.y + 0.072169f * out.z;
+        if (isnan(out.x) || isnan(out.y) || isnan(out.z) || y < -1e-5f || isinf(y)) out = mk(0.f, 0.f, 0.f);
+    }
+    P.out[3 * o + 0] = out.x;
+    P.out[3 * o + 1] = out.y;
+    P.out[3 * o + 2] = out.z;
+}
+
+hipError_t launch_final(const FinalParams &p, hipStream_t s) {
+    if (p.rec_count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_final, dim3((unsigned)((p.rec_count + 255) / 256)), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+/* restore the eye pass's initial PPM state (flux 0, N 0, r^2 init;
+ * raytracing.cu:121-123) so that every benchmark step gathers the same
+ * workload as the reference's single pass */
+__global__ __launch_bounds__(256) void k_reset_records(RecordsDev R, float r2init) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= R.count) return;
+    uint32_t flags = (uint32_t)__float_as_int(R.pos[r].w);
+    if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) return;
+    R.state[r] = make_float4(0.f, 0.f, 0.f, r2init);
+    R.n[r] = 0.f;
+}
+
+hipError_t launch_reset_records(const RecordsDev &R, float r2init, hipStream_t s) {
+    if (R.count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_reset_records, dim3((unsigned)((R.count + 255) / 256)), dim3(256), 0, s, R, r2init);
+    return hipGetLastError();
+}
+
+} // namespace pm

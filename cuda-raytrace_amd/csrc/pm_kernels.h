@@ -54,6 +54,14 @@ struct GridDesc {
     uint32_t ncells;
 };
 
+/* bucket coordinate along one axis, clamped (points outside the scene box
+ * map to the border cells on both the build and the query side) */
+PMD uint32_t cell_axis(float v, float g0, float inv_cs, int dim) {
+    int c = (int)floorf((v - g0) * inv_cs);
+    c = c < 0 ? 0 : (c >= dim ? dim - 1 : c);
+    return (uint32_t)c;
+}
+
 struct GatherParams {
     RecordsDev R;
     int64_t rec_begin, rec_end; /* records gathered by this launch */
@@ -68,8 +76,11 @@ struct GatherParams {
     /* kd-tree (reference layout) */
     const pm_photon *kd_nodes;
     int64_t kd_count;
-    /* partial mode */
-    float4 *partial;
+    /* fixed-point flux: contribution c -> rint(c * fx_scale), fx_inv = 1/fx_scale (2^-S) */
+    float fx_scale;
+    double fx_inv;
+    /* partial mode: per record int64 (M, L.x, L.y, L.z) in fixed point */
+    long long *partial;
     unsigned long long *counters; /* [0] visited, [1] in radius */
 };
 
@@ -84,22 +95,19 @@ struct FinalParams {
 
 hipError_t launch_eye(const EyeParams &p, hipStream_t s);
 hipError_t launch_trace(const TraceParams &p, hipStream_t s);
-/* grid build */
-hipError_t launch_grid_keys(const pm_photon *slots, int64_t n, GridDesc g, uint32_t *keys, uint32_t *vals,
-                            uint32_t *cell_count, uint32_t *n_valid, hipStream_t s);
-size_t grid_sort_temp_bytes(int64_t n, uint32_t ncells);
-hipError_t launch_grid_sort(void *temp, size_t temp_bytes, uint32_t *keys_in, uint32_t *keys_out,
-                            uint32_t *vals_in, uint32_t *vals_out, int64_t n, int end_bit, hipStream_t s);
-size_t grid_scan_temp_bytes(uint32_t ncells);
-hipError_t launch_grid_scan(void *temp, size_t temp_bytes, const uint32_t *cell_count, uint32_t *cell_start,
-                            uint32_t ncells, hipStream_t s);
-hipError_t launch_grid_scatter(const pm_photon *slots, const uint32_t *sorted_vals, const uint32_t *n_valid,
-                               int64_t n, float4 *ph_a, float4 *ph_b, float *ph_c, hipStream_t s);
+/* photon-bucket build (pm_bucket.hip): count + rank, scan, fill.
+ * count and cell_start have ncells + 1 entries; cell_start[ncells] = valid
+ * photons; scratch holds bucket_scratch_words() uint32 */
+size_t bucket_scratch_words(int64_t n_slots, uint32_t ncells);
+hipError_t launch_bucket_build(const pm_photon *slots, int64_t n, GridDesc g, uint32_t *count, uint32_t *cell_start,
+                               uint32_t *scratch, float4 *ph_a, float4 *ph_b, float *ph_c, hipStream_t s);
 /* gather: structure 0 grid, 1 kd; mode 0 fused PPM, 1 partial */
 hipError_t launch_gather(const GatherParams &p, int structure, int partial, int count, hipStream_t s);
-hipError_t launch_ppm_update(const GatherParams &p, const float4 *partial, int64_t rec_begin, int64_t rec_count,
+hipError_t launch_ppm_update(const GatherParams &p, const long long *partial, int64_t rec_begin, int64_t rec_count,
                              hipStream_t s);
 hipError_t launch_final(const FinalParams &p, hipStream_t s);
+hipError_t launch_radius2_io(const RecordsDev &R, float *buf, int64_t rec_begin, int64_t rec_count, int to_records,
+                             hipStream_t s);
 hipError_t launch_reset_records(const RecordsDev &R, float r2init, hipStream_t s);
 
 } // namespace pm

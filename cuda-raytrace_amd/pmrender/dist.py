@@ -11,10 +11,11 @@ Work split:
 Two exchange strategies:
   * "reduce" (default): each rank builds a map of ITS photons and gathers all
     records against it; the PPM estimator's sums (M, L) are linear in the
-    photon set, so a reduce-scatter of one float4 per record gives every
-    owner the global (M, L) of its chunk, then it applies the PPM update.
-    Bytes on xGMI per pass: 16 B x records (33 MB at 1080p), independent of
-    the photon count.
+    photon set, so a reduce-scatter of one int64x4 per record (M and the
+    flux in the gather's exact fixed point) gives every owner the global
+    (M, L) of its chunk, bit-identical to a 1-GPU gather; the owner then
+    applies the PPM update. Bytes on xGMI per pass: 32 B x records (66 MB at
+    1080p), independent of the photon count.
   * "allgather": the reference-style exchange: all-gather the
     40-B photon slots into a replicated map, gather locally owned chunks.
     Bytes per pass: 40 B x slots x (N-1)/N per rank.
@@ -78,6 +79,12 @@ class HipEngine:
     def ppm_update(self, p, partial, rec_begin, rec_count):
         self.ctx.ppm_update(p, partial.data_ptr(), rec_begin, rec_count, self._s())
 
+    def get_radius2(self, rec_begin, rec_count, out):
+        self.ctx.get_radius2(rec_begin, rec_count, out.data_ptr(), self._s())
+
+    def set_radius2(self, src, rec_begin, rec_count):
+        self.ctx.set_radius2(src.data_ptr(), rec_begin, rec_count, self._s())
+
     def final(self, emitted, rec_begin, rec_count, out):
         self.ctx.final(emitted, rec_begin, rec_count, out.data_ptr(), self._s())
 
@@ -98,8 +105,10 @@ class PassRunner:
         self.chunk = None
         self.slot_buf = None
         if world > 1 and exchange == "reduce":
-            self.partial = engine.alloc((self.padded, 4), torch.float32)
-            self.chunk = engine.alloc((self.rec_per, 4), torch.float32)
+            # per record (M, L.rgb) as int64 fixed point: the sum over ranks is exact
+            self.partial = engine.alloc((self.padded, 4), torch.int64)
+            self.chunk = engine.alloc((self.rec_per, 4), torch.int64)
+            self.r2_all = engine.alloc((self.padded,), torch.float32)
         if world > 1 and exchange == "allgather":
             self.slot_buf = engine.alloc((world * self.slots_per_rank * PHOTON_DTYPE.itemsize,), torch.uint8)
             engine.use_slot_buffer(self.slot_buf)
@@ -131,6 +140,11 @@ class PassRunner:
             e.gather_partial(p, self.partial)
             self._reduce_scatter()
             e.ppm_update(p, self.chunk, self.rec_begin, self.rec_count)
+            # publish the owners' new radii: every rank queries the next pass with them
+            mine = self.r2_all[self.rank * self.rec_per:(self.rank + 1) * self.rec_per]
+            e.get_radius2(self.rec_begin, self.rec_count, mine)
+            dist.all_gather_into_tensor(self.r2_all, mine)
+            e.set_radius2(self.r2_all, 0, self.n_records)
         else:
             e.trace_photons(p, pass_index, self.path_begin, self.paths, 0)
             mine = self.slot_buf[self.rank * self.slots_per_rank * PHOTON_DTYPE.itemsize:

@@ -80,6 +80,8 @@ def load_library(path=None):
         "pm_timing_reset": (c_int, [vp]),
         "pm_gather_range": (c_int, [vp, ctypes.POINTER(RenderParams), i64, i64, vp]),
         "pm_set_slot_buffer": (c_int, [vp, vp, i64]),
+        "pm_get_radius2": (c_int, [vp, i64, i64, vp, vp]),
+        "pm_set_radius2": (c_int, [vp, vp, i64, i64, vp]),
         "pm_timing_total": (c_int, [vp, ctypes.c_char_p, ctypes.POINTER(i64), ctypes.POINTER(c_double)]),
         "pm_reset_records": (c_int, [vp, ctypes.POINTER(RenderParams), vp]),
     }
@@ -221,6 +223,12 @@ class Context:
     def ppm_update(self, params, d_partial, rec_begin, rec_count, stream=None):
         self._chk(self.lib.pm_ppm_update(self.h, ctypes.byref(params), ctypes.c_void_p(d_partial), int(rec_begin),
                                          int(rec_count), stream))
+
+    def get_radius2(self, rec_begin, rec_count, d_out, stream=None):
+        self._chk(self.lib.pm_get_radius2(self.h, int(rec_begin), int(rec_count), ctypes.c_void_p(d_out), stream))
+
+    def set_radius2(self, d_in, rec_begin, rec_count, stream=None):
+        self._chk(self.lib.pm_set_radius2(self.h, ctypes.c_void_p(d_in), int(rec_begin), int(rec_count), stream))
 
     def final(self, emitted, rec_begin, rec_count, d_out, stream=None):
         self._chk(self.lib.pm_final(self.h, float(emitted), int(rec_begin), int(rec_count), ctypes.c_void_p(d_out),

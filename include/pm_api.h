@@ -188,13 +188,20 @@ int pm_gather(void *ctx, const pm_render_params *params, void *stream);
 /* ... or over records [rec_begin, rec_begin + rec_count) (tile-owned gather). */
 int pm_gather_range(void *ctx, const pm_render_params *params, int64_t rec_begin, int64_t rec_count,
                     void *stream);
-/* Range query only: writes per-record (M, L.rgb) as float4 to d_partial
- * (device pointer, n_records float4). */
+/* Range query only: writes per record four int64 (M, L.r, L.g, L.b) to
+ * d_partial (device pointer, 32 B x n_records); L is in the gather's exact
+ * fixed point, so partials of photon shards sum to the 1-GPU result. */
 int pm_gather_partial(void *ctx, const pm_render_params *params, void *d_partial, void *stream);
 /* PPM update of records [rec_begin, rec_begin+rec_count) from summed partials
  * (d_partial points at the partial of rec_begin). */
 int pm_ppm_update(void *ctx, const pm_render_params *params, const void *d_partial,
                   int64_t rec_begin, int64_t rec_count, void *stream);
+/* radius^2 of records [rec_begin, rec_begin+rec_count) to / from a device
+ * float array (d_out[i] / d_in[i] is record rec_begin + i). The owner of a
+ * record chunk publishes its updated radii so every rank queries the next
+ * pass with the current radius (multi-GPU "reduce" exchange). */
+int pm_get_radius2(void *ctx, int64_t rec_begin, int64_t rec_count, void *d_out, void *stream);
+int pm_set_radius2(void *ctx, const void *d_in, int64_t rec_begin, int64_t rec_count, void *stream);
 /* Final radiance of records [rec_begin, rec_begin+rec_count) into the device
  * buffer d_out (float3 per record, RECORD order) — emitted = total paths. */
 int pm_final(void *ctx, double emitted, int64_t rec_begin, int64_t rec_count, void *d_out, void *stream);

@@ -97,6 +97,16 @@ PMDM_FN float pmdm_cosf(float xf) {
     return (float)v;
 }
 
+/* sin and cos of one angle with a single reduction; bit-identical to
+ * pmdm_sinf / pmdm_cosf (same operations). */
+PMDM_FN void pmdm_sincosf(float xf, float *sf, float *cf) {
+    int q;
+    double r = pmdm_reduce((double)xf, &q);
+    double s = pmdm_sin_kern(r), c = pmdm_cos_kern(r);
+    *sf = (float)((q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c);
+    *cf = (float)((q == 0) ? c : (q == 1) ? -s : (q == 2) ? -c : s);
+}
+
 /* atan on [0, tan(pi/16)]: odd Taylor series to t^27. */
 PMDM_FN double pmdm_atan_small(double t) {
     double z = t * t;

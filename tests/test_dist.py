@@ -1,0 +1,168 @@
+"""World-size-2 gloo tests of the multi-GPU pass runner (pmrender/dist.py) on
+CPU: the same PassRunner that bench.py drives over RCCL, here over gloo with
+an oracle-backed engine. Checks both photon exchanges against a
+single-process run over the same global paths."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+from pmrender.abi import PHOTON_DTYPE, RECORD_DTYPE, RenderParams  # noqa: E402
+
+PATHS = 4096  # per rank
+
+
+class OracleEngine:
+    """PassRunner engine on the CPU oracle (test infrastructure only)."""
+    FX = 2.0 ** 12  # fixed-point scale of the int64 partials
+
+    def __init__(self, scene, params):
+        import oracle
+        self.oracle = oracle
+        self.orc = scene.load_into(oracle.Oracle(nthreads=2))
+        self.init = self.orc.eye_pass(params)
+        self.recs = self.init.copy()
+        self.slots = None
+        self.slot_buf = None
+        self.nodes = None
+
+    def num_records(self):
+        return len(self.recs)
+
+    def alloc(self, shape, dtype):
+        return torch.zeros(shape, dtype=dtype)
+
+    def use_slot_buffer(self, t):
+        self.slot_buf = t
+
+    def reset_records(self, p):
+        self.recs = self.init.copy()
+
+    def trace_photons(self, p, pass_index, path_begin, path_count, slot_path_base):
+        s = self.orc.trace_photons(p, pass_index, path_begin, path_count)
+        if self.slot_buf is None:
+            self.slots = s
+            return
+        off = (path_begin - slot_path_base) * p.max_photon_count * PHOTON_DTYPE.itemsize
+        self.slot_buf.numpy()[off:off + s.nbytes] = s.view(np.uint8)
+
+    def build_photon_map(self, p, n_slots):
+        if self.slot_buf is None:
+            src = self.slots[:n_slots]
+        else:
+            src = np.frombuffer(self.slot_buf.numpy()[: n_slots * PHOTON_DTYPE.itemsize].tobytes(), PHOTON_DTYPE)
+        self.nodes = self.oracle.Oracle.build_kdtree(src)
+
+    def gather(self, p):
+        self.orc.gather(self.nodes, self.recs, p)
+
+    def gather_range(self, p, b, n):
+        sub = self.recs[b:b + n].copy()
+        self.orc.gather(self.nodes, sub, p)
+        self.recs[b:b + n] = sub
+
+    def gather_partial(self, p, out):
+        part = self.orc.gather_partial(self.nodes, self.recs)
+        n = len(part)
+        out[:n, 0] = torch.from_numpy(part[:, 0].astype(np.int64))
+        out[:n, 1:] = torch.from_numpy(np.rint(part[:, 1:].astype(np.float64) * self.FX).astype(np.int64))
+
+    def ppm_update(self, p, partial, b, n):
+        import ctypes
+        lib = self.oracle.load()
+        P = partial.numpy()
+        for i in range(n):
+            r = self.recs[b + i]
+            if r["flags"] & 7:
+                continue
+            r2 = np.float32([r["radius2"]])
+            N = np.float32([r["photon_count"]])
+            flux = np.ascontiguousarray(r["flux"], np.float32)
+            L = (P[i, 1:].astype(np.float64) / self.FX).astype(np.float32)
+            fp = ctypes.POINTER(ctypes.c_float)
+            lib.orc_ppm_update(r2.ctypes.data_as(fp), N.ctypes.data_as(fp), flux.ctypes.data_as(fp), int(P[i, 0]),
+                               L.ctypes.data_as(fp), float(p.ppm_alpha))
+            self.recs[b + i]["radius2"], self.recs[b + i]["photon_count"] = r2[0], N[0]
+            self.recs[b + i]["flux"] = flux
+
+    def get_radius2(self, b, n, out):
+        out[:n] = torch.from_numpy(self.recs["radius2"][b:b + n].copy())
+
+    def set_radius2(self, src, b, n):
+        self.recs["radius2"][b:b + n] = src[:n].numpy()
+
+    def final(self, emitted, b, n, out):
+        img = self.orc.final(self.recs, emitted)
+        out.copy_(torch.from_numpy(img[b:b + n]))
+
+
+def _scene():
+    from pmrender import scenes
+    sc = scenes.cornell_box(40, 24)
+    sc.camera = scenes.rays_from_pinhole(sc)
+    return sc
+
+
+def _worker(rank, world, port, exchange, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "cuda-raytrace_amd"), os.path.join(root, "oracle")]
+    from pmrender.dist import PassRunner
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    p = RenderParams.defaults(paths_per_pass=PATHS, initial_radius2=25.0)
+    eng = OracleEngine(_scene(), p)
+    runner = PassRunner(eng, p, rank, world, exchange)
+    for pass_index in range(2):
+        runner.step(pass_index)
+    out = torch.zeros((runner.n_records, 3), dtype=torch.float32)
+    runner.final_gather(float(runner.emitted_per_pass * 2), out)
+    np.save(os.path.join(outdir, f"recs{rank}.npy"), eng.recs[runner.rec_begin:runner.rec_begin + runner.rec_count])
+    np.save(os.path.join(outdir, f"img{rank}.npy"), out.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _single_process_reference(world):
+    """1 process, the union of both ranks' global paths, kd gather."""
+    import oracle
+    p = RenderParams.defaults(paths_per_pass=PATHS * world, initial_radius2=25.0)
+    orc = _scene().load_into(oracle.Oracle(nthreads=2))
+    recs = orc.eye_pass(p)
+    for pass_index in range(2):
+        slots = orc.trace_photons(p, pass_index, 0, PATHS * world)
+        orc.gather(oracle.Oracle.build_kdtree(slots), recs, p)
+    return recs, orc.final(recs, float(PATHS * world * 2))
+
+
+@pytest.mark.parametrize("exchange", ["allgather", "reduce"])
+def test_two_rank_pass_matches_single_process(exchange, tmp_path):
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), exchange, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    ref_recs, ref_img = _single_process_reference(world)
+    recs = np.concatenate([np.load(tmp_path / f"recs{r}.npy") for r in range(world)]).view(RECORD_DTYPE)
+    assert len(recs) == len(ref_recs)
+    assert np.array_equal(recs["photon_count"], ref_recs["photon_count"])
+    assert np.array_equal(recs["radius2"].view(np.uint32), ref_recs["radius2"].view(np.uint32))
+    img = np.load(tmp_path / "img0.npy")
+    assert np.array_equal(img, np.load(tmp_path / "img1.npy"))        # every rank holds the full image
+    if exchange == "allgather":
+        # replicated map over identical slots + canonical kd-tree: bit-exact
+        assert np.array_equal(recs["flux"].view(np.uint32), ref_recs["flux"].view(np.uint32))
+        assert np.array_equal(img.view(np.uint32), ref_img.view(np.uint32))
+    else:
+        # per-rank partial sums: exact M, flux within the fixed-point/fp32 rounding
+        np.testing.assert_allclose(recs["flux"], ref_recs["flux"], rtol=1e-5, atol=1e-3)
+        np.testing.assert_allclose(img, ref_img, rtol=1e-5, atol=1e-6)

@@ -114,17 +114,63 @@ def test_partial_plus_update_equals_fused(cornell):
     ctx.gather(p)
     fused = ctx.download_records()
     ctx.upload_records(recs)
-    part = torch.zeros((len(recs), 4), dtype=torch.float32, device="cuda")
+    part = torch.zeros((len(recs), 4), dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
     ctx.gather_partial(p, part.data_ptr())
     ctx.synchronize()
     ref_part = orc.gather_partial(orc.build_kdtree(slots), recs)
     gp = part.cpu().numpy()
-    assert np.array_equal(gp[:, 0], ref_part[:, 0])
+    assert np.array_equal(gp[:, 0], ref_part[:, 0].astype(np.int64))
     half = len(recs) // 2
     ctx.ppm_update(p, part.data_ptr(), 0, half)
     ctx.ppm_update(p, part[half:].data_ptr(), half, len(recs) - half)
     assert_bitexact(ctx.download_records(), fused, "partial+update vs fused")
+
+
+def test_sharded_reduce_exchange_bitexact(oracle_mod, hip_mod):
+    """The multi-GPU "reduce" exchange emulated on one device: two contexts
+    each trace half of the global paths, gather all records against their
+    own photon buckets, the int64 partials are summed (what RCCL
+    reduce_scatter does), owners update, radii are exchanged. The records
+    must equal a single context over all paths bit for bit."""
+    torch = pytest.importorskip("torch")
+    sc = scenes.cornell_box(64, 48)
+    paths = 8192
+    p = RenderParams.defaults(paths_per_pass=paths)
+    ref = sc.load_into(hip_mod.Context(0))
+    pr = RenderParams.defaults(paths_per_pass=2 * paths)
+    ref.eye_pass(pr)
+    shards = [sc.load_into(hip_mod.Context(0)) for _ in range(2)]
+    for c in shards:
+        c.eye_pass(p)
+    n = ref.num_records()
+    half = n // 2
+    for pass_index in range(3):
+        ref.trace_photons(pr, pass_index, 0, 2 * paths)
+        ref.build_photon_map(pr)
+        ref.gather(pr)
+        parts = []
+        for rank, c in enumerate(shards):
+            c.trace_photons(p, pass_index, rank * paths, paths, rank * paths)
+            c.build_photon_map(p, paths * 4)
+            t = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+            torch.cuda.synchronize()
+            c.gather_partial(p, t.data_ptr())
+            c.synchronize()
+            parts.append(t)
+        total = parts[0] + parts[1]
+        torch.cuda.synchronize()
+        r2 = torch.zeros(n, dtype=torch.float32, device="cuda")
+        for rank, c in enumerate(shards):
+            b, cnt = (0, half) if rank == 0 else (half, n - half)
+            c.ppm_update(p, total[b:].data_ptr(), b, cnt)
+            c.get_radius2(b, cnt, r2[b:].data_ptr())
+            c.synchronize()
+        for c in shards:
+            c.set_radius2(r2.data_ptr(), 0, n)
+            c.synchronize()
+    got = np.concatenate([shards[0].download_records()[:half], shards[1].download_records()[half:]])
+    assert_bitexact(got, ref.download_records(), "2-shard reduce exchange vs 1 context")
 
 
 @pytest.mark.parametrize("structure", [PM_GATHER_KDTREE, PM_GATHER_GRID])
@@ -142,11 +188,28 @@ def test_render_parity_cornell(cornell, structure):
 
 
 def test_render_deterministic(cornell):
+    """Bucket order comes from atomic arrival order; the fixed-point gather
+    makes the image independent of it."""
     ctx, _ = cornell
-    p = RenderParams.defaults(paths_per_pass=16384)
+    p = RenderParams.defaults(paths_per_pass=65536, passes=2)
     a, _ = ctx.render(p)
-    b, _ = ctx.render(p)
-    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    for _ in range(3):
+        b, _ = ctx.render(p)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_grid_gather_independent_of_photon_order(cornell):
+    """Permuting the slot array (hence every bucket's order) changes no bit."""
+    ctx, orc = cornell
+    p, recs, slots = _gather_inputs(orc)
+    outs = []
+    for perm in (np.arange(len(slots)), np.random.RandomState(4).permutation(len(slots))):
+        ctx.upload_records(recs)
+        ctx.upload_slots(slots[perm])
+        ctx.build_photon_map(p, len(slots))
+        ctx.gather(p)
+        outs.append(ctx.download_records())
+    assert_bitexact(outs[0], outs[1], "records after permuted-photon gather")
 
 
 @pytest.mark.parametrize("builder", ["caustic", "feature", "soup"])

@@ -24,4 +24,11 @@ timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$O/pmc_write" -o run --output-f
 cd "$R"
 python3 tools/pmc_traffic.py "$O/pmc_fetch" "$O/pmc_write" "$O/pmc_traffic.json" > /dev/null 2>&1; ok $? pmc_summary
 find "$O/prof" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats.csv" \;
+
+# optional: SQ counters of every kernel (issue/wait anatomy), its own pass
+if [ "${PM_SQ:-0}" = "1" ]; then
+  cd /tmp
+  timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAIT_ANY -d "$O/pmc_sq" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-census "$@" > "$O/pmc_sq.log" 2>&1; ok $? pmc_sq
+  cd "$R"
+fi
 echo done | tee -a "$O/steps.log"
