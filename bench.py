@@ -142,13 +142,14 @@ def main():
         gather_launches, gather_ms_total = ctx.timing_total("gather")
         gather_ms = gather_ms_total / max(gather_launches, 1)
 
-        census = canonical = None
+        census = canonical = tcensus = None
         if not args.no_census:
             # untimed counting launch of the same step: algorithmic-byte units
             ctx.set_counting(True)
             runner.step(0, reset=True)
             torch.cuda.synchronize()
             census = ctx.gather_counters(full=True)
+            tcensus = ctx.trace_counters()
             ctx.set_counting(False)
             if rank == 0 and world == 1 and structure == PM_GATHER_GRID:
                 # SURVEY.md §8d's per-unit figure counts V on the canonical pbrt kd-tree
@@ -211,6 +212,21 @@ def main():
                 "bytes_per_launch": int(survey_bytes), "V_kd": cv, "H": ch,
                 "GBs_at_measured_time": round(survey_bytes / (gather_ms * 1e-3) / 1e9, 1)}
 
+    trace_roofline = None
+    if tcensus is not None and "trace" in stages:
+        rays, nodes, prims, deposits = tcensus
+        # SURVEY.md §8d (reported, not graded): 40 B per deposit + 32 B per BVH
+        # node entered + 36 B per primitive test (RNG is inline Philox: 0 B)
+        tbytes = 40 * deposits + 32 * nodes + 36 * prims
+        tach = tbytes / (stages["trace"] * 1e-3) / 1e9
+        trace_roofline = {
+            "bound": "hbm", "kernel": "k_trace<0>", "achieved": round(tach, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(tach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": int(tbytes),
+            "formula": "40*deposits + 32*bvh_nodes + 36*prim_tests (SURVEY.md §8d B_trace)",
+            "units": {"rays": rays, "bvh_nodes": nodes, "prim_tests": prims, "deposits": deposits},
+            "avg_launch_ms": stages["trace"],
+            "note": "VALU-bound: the BVH and scene of C2 stay in L2/MALL, so B_trace is mostly cache traffic"}
+
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -242,6 +258,7 @@ def main():
         "stages_ms": stages,
         "setup_s": round(setup_s, 3),
         "roofline": roofline,
+        "trace_roofline": trace_roofline,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

@@ -32,14 +32,14 @@ struct DevBuf {
     size_t bytes = 0;
     hipError_t ensure(size_t n) {
         if (n <= bytes && p) return hipSuccess;
-        if (p) { hipFree(p); p = nullptr; bytes = 0; }
+        if (p) { (void)hipFree(p); p = nullptr; bytes = 0; }
         if (n == 0) n = 16;
         hipError_t e = hipMalloc(&p, n);
         if (e == hipSuccess) bytes = n;
         return e;
     }
     bool external = false; /* caller-owned memory: never freed or grown here */
-    void release() { if (p && !external) hipFree(p); p = nullptr; bytes = 0; external = false; }
+    void release() { if (p && !external) (void)hipFree(p); p = nullptr; bytes = 0; external = false; }
     template <class T> T *as() const { return (T *)p; }
 };
 
@@ -69,8 +69,7 @@ struct Ctx {
     int n2d = 0;
     bool committed = false;
     /* device scene */
-    DevBuf d_nodes, d_refs, d_tri_geo, d_tri_info, d_tri_id, d_verts, d_norms, d_uvs, d_meshes, d_disks,
-        d_spheres, d_materials, d_lights, d_rays, d_rand2d;
+    DevBuf d_scene, d_rays, d_rand2d; /* d_scene: the scene blob (SceneDev) */
     SceneDev S{};
     float bbox_lo[3] = {0, 0, 0}, bbox_hi[3] = {0, 0, 0};
     double emit_max = 1.0, kd_max = 1.0; /* bounds for the fixed-point flux scale */
@@ -92,6 +91,7 @@ struct Ctx {
     /* misc */
     DevBuf d_out, d_counters;
     bool counting = false;
+    int64_t trace_per_block = TRACE_BLOCK; /* env PM_TRACE_PATHS_PER_BLOCK (tuning) */
     std::map<std::string, TimerPool> timers;
 };
 
@@ -123,20 +123,20 @@ int timer_begin(Ctx *c, const char *name, hipStream_t s) {
     TimerPool &tp = c->timers[name];
     if (tp.used == tp.ev.size()) {
         Timer t;
-        hipEventCreate(&t.a);
-        hipEventCreate(&t.b);
+        (void)hipEventCreate(&t.a);
+        (void)hipEventCreate(&t.b);
         tp.ev.push_back(t);
     }
-    hipEventRecord(tp.ev[tp.used].a, s);
+    (void)hipEventRecord(tp.ev[tp.used].a, s);
     return 0;
 }
 void timer_end(Ctx *c, const char *name, hipStream_t s) {
     TimerPool &tp = c->timers[name];
-    hipEventRecord(tp.ev[tp.used].b, s);
+    (void)hipEventRecord(tp.ev[tp.used].b, s);
     tp.used++;
 }
 double pair_ms(const Timer &t) {
-    hipEventSynchronize(t.b);
+    (void)hipEventSynchronize(t.b);
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, t.a, t.b) != hipSuccess) return -1.0;
     return ms;
@@ -151,6 +151,45 @@ double timer_ms(Ctx *c, const char *name) {
 inline float4 f4(float x, float y, float z, float w) { return make_float4(x, y, z, w); }
 inline float ibits(int v) { float f; std::memcpy(&f, &v, 4); return f; }
 inline int fbits_h(float f) { int v; std::memcpy(&v, &f, 4); return v; }
+inline float bits_f(uint32_t v) { float f; std::memcpy(&f, &v, 4); return f; }
+
+/* Normalized shading frame of one triangle: the same IEEE float operations
+ * in the same order as the closest-hit program (cudatrianglemesh.cu:36-78,
+ * then normalize as cudamaterial.cu.h:84-85), so the device reads values
+ * bit-identical to computing them per hit. n = e1 x e0 as in tri_geo. */
+void tri_frame(const float *p0, const float *p1, const float *p2, const float *UV, const int *v, const float *n,
+               float *ns, float *dpdu) {
+    float uv0x = 0.f, uv0y = 0.f, uv1x = 1.f, uv1y = 0.f, uv2x = 0.f, uv2y = 1.f;
+    if (UV) {
+        uv0x = UV[2 * v[0]]; uv0y = UV[2 * v[0] + 1];
+        uv1x = UV[2 * v[1]]; uv1y = UV[2 * v[1] + 1];
+        uv2x = UV[2 * v[2]]; uv2y = UV[2 * v[2] + 1];
+    }
+    const float du1 = uv0x - uv2x, du2 = uv1x - uv2x, dv1 = uv0y - uv2y, dv2 = uv1y - uv2y;
+    const float determinant = du1 * dv2 - dv1 * du2;
+    float d[3];
+    if (determinant == 0.0f) {
+        if (std::fabs(n[0]) > std::fabs(n[1])) {
+            float invLen = 1.f / std::sqrt(n[0] * n[0] + n[2] * n[2]);
+            d[0] = -n[2] * invLen; d[1] = 0.f; d[2] = n[0] * invLen;
+        } else {
+            float invLen = 1.f / std::sqrt(n[1] * n[1] + n[2] * n[2]);
+            d[0] = 0.f; d[1] = n[2] * invLen; d[2] = n[1] * invLen;
+        }
+    } else {
+        const float invdet = 1.f / determinant;
+        for (int a = 0; a < 3; ++a) {
+            float dp1 = p0[a] - p2[a], dp2 = p1[a] - p2[a];
+            d[a] = (dv2 * dp1 - dv1 * dp2) * invdet;
+        }
+    }
+    auto normalize3 = [](const float *x, float *out) {
+        float inv = 1.0f / std::sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+        for (int a = 0; a < 3; ++a) out[a] = x[a] * inv;
+    };
+    normalize3(n, ns);
+    normalize3(d, dpdu);
+}
 
 int64_t num_records(const Ctx *c) {
     if (c->pinhole) return (int64_t)((c->W + 7) / 8) * ((c->H + 7) / 8) * 64;
@@ -203,7 +242,7 @@ RecordsDev recs(Ctx *c) {
 GatherParams gather_params(Ctx *c, const pm_render_params *p) {
     GatherParams G{};
     G.R = recs(c);
-    G.materials = c->d_materials.as<float4>();
+    G.materials = c->S.materials;
     G.ppm_alpha = p->ppm_alpha;
     G.grid = c->grid;
     G.cell_start = c->d_cell_start.as<uint32_t>();
@@ -265,13 +304,14 @@ int pm_create(void **out, const pm_config *cfg) {
     if (dev < 0 || dev >= ndev) FAIL((Ctx *)nullptr, PM_ERR_INVALID, "device %d out of range (%d devices)", dev, ndev);
     Ctx *c = new Ctx();
     c->device = dev;
-    hipSetDevice(dev);
+    if (const char *e = getenv("PM_TRACE_PATHS_PER_BLOCK")) c->trace_per_block = std::max(1LL, atoll(e));
+    (void)hipSetDevice(dev);
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
         FAIL((Ctx *)nullptr, PM_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
     }
-    e = c->d_counters.ensure(4 * sizeof(unsigned long long));
+    e = c->d_counters.ensure(8 * sizeof(unsigned long long)); /* [gather x4][trace x4] */
     if (e != hipSuccess) {
         delete c;
         FAIL((Ctx *)nullptr, PM_ERR_HIP, "hipMalloc: %s", hipGetErrorString(e));
@@ -283,21 +323,19 @@ int pm_create(void **out, const pm_config *cfg) {
 void pm_destroy(void *ptr) {
     Ctx *c = (Ctx *)ptr;
     if (!c) return;
-    hipSetDevice(c->device);
-    hipStreamSynchronize(c->stream);
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
     for (auto &kv : c->timers)
         for (Timer &t : kv.second.ev) {
-            hipEventDestroy(t.a);
-            hipEventDestroy(t.b);
+            (void)hipEventDestroy(t.a);
+            (void)hipEventDestroy(t.b);
         }
-    DevBuf *bufs[] = {&c->d_nodes, &c->d_refs, &c->d_tri_geo, &c->d_tri_info, &c->d_tri_id, &c->d_verts,
-                      &c->d_norms, &c->d_uvs, &c->d_meshes, &c->d_disks, &c->d_spheres, &c->d_materials,
-                      &c->d_lights, &c->d_rays, &c->d_rand2d, &c->d_pos, &c->d_nrm, &c->d_state, &c->d_n,
+    DevBuf *bufs[] = {&c->d_scene, &c->d_rays, &c->d_rand2d, &c->d_pos, &c->d_nrm, &c->d_state, &c->d_n,
                       &c->d_dl, &c->d_slots, &c->d_count, &c->d_scratch,
                       &c->d_cell_start, &c->d_pha, &c->d_phb, &c->d_phc,
                       &c->d_kd, &c->d_out, &c->d_counters};
     for (DevBuf *b : bufs) b->release();
-    hipStreamDestroy(c->stream);
+    (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -500,19 +538,24 @@ int pm_commit(void *ptr) {
         add_box(lo, hi, (PRIM_SPHERE << 30) | (uint32_t)i);
     }
     BvhOut bvh;
-    build_bvh(prims, BVH_STACK - 2, bvh);
+    BvhCost cost;
+    if (const char *e = getenv("PM_BVH_LEAF_MAX")) cost.leaf_max = std::max(1, atoi(e));
+    if (const char *e = getenv("PM_BVH_CTRAV")) cost.c_trav = (float)atof(e);
+    build_bvh(prims, BVH_STACK - 2, bvh, cost);
     c->bvh_depth = bvh.depth;
     if (bvh.depth >= BVH_STACK) FAIL(c, PM_ERR_INVALID, "BVH too deep (%d)", bvh.depth);
 
-    /* triangles in leaf order; per-triangle precomputed (p0, e0, e1, n) */
-    std::vector<float4> tri_geo;
+    /* triangles in leaf order; per-triangle precomputed (p0, e0, e1, n) for the
+     * intersector and the normalized shading frame for hits */
+    std::vector<float4> tri_geo, tri_shade;
     std::vector<int4> tri_info;
     std::vector<uint32_t> tri_id;
-    tri_geo.reserve(3 * nt); tri_info.reserve(nt); tri_id.reserve(nt);
+    tri_geo.reserve(3 * nt); tri_shade.reserve(2 * nt); tri_info.reserve(nt); tri_id.reserve(nt);
     for (uint32_t &ref : bvh.refs) {
         if ((ref >> 30) != PRIM_TRI) continue;
         uint32_t t = ref & 0x3fffffffu;
         const HTri &tr = c->tris[t];
+        const HMesh &m = c->meshes[tr.mesh];
         const float *p0 = V + 3 * tr.v[0], *p1 = V + 3 * tr.v[1], *p2 = V + 3 * tr.v[2];
         float e0[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
         float e1[3] = {p0[0] - p2[0], p0[1] - p2[1], p0[2] - p2[2]};
@@ -521,43 +564,54 @@ int pm_commit(void *ptr) {
         tri_geo.push_back(f4(p0[0], p0[1], p0[2], e0[0]));
         tri_geo.push_back(f4(e0[1], e0[2], e1[0], e1[1]));
         tri_geo.push_back(f4(e1[2], n[0], n[1], n[2]));
+        float ns[3], dpdu[3];
+        tri_frame(p0, p1, p2, m.has_uv ? &c->UV[0] : nullptr, tr.v, n, ns, dpdu);
+        tri_shade.push_back(f4(ns[0], ns[1], ns[2], bits_f((uint32_t)m.material | (m.has_n ? 0x80000000u : 0u))));
+        tri_shade.push_back(f4(dpdu[0], dpdu[1], dpdu[2], bits_f((uint32_t)m.light)));
         tri_info.push_back(make_int4(tr.v[0], tr.v[1], tr.v[2], tr.mesh));
         tri_id.push_back(t);
         ref = (PRIM_TRI << 30) | k;
     }
-    std::vector<float4> verts(c->P.size() / 3), norms(c->P.size() / 3);
-    std::vector<float2> uvs(c->P.size() / 3);
-    for (size_t i = 0; i < verts.size(); ++i) {
-        verts[i] = f4(c->P[3 * i], c->P[3 * i + 1], c->P[3 * i + 2], 0.f);
-        norms[i] = f4(c->N[3 * i], c->N[3 * i + 1], c->N[3 * i + 2], 0.f);
-        uvs[i] = make_float2(c->UV[2 * i], c->UV[2 * i + 1]);
-    }
-    std::vector<int4> meshes;
-    for (auto &m : c->meshes) meshes.push_back(make_int4(m.material, m.light, m.has_n, m.has_uv));
+    std::vector<float4> norms(c->N.size() / 3);
+    for (size_t i = 0; i < norms.size(); ++i) norms[i] = f4(c->N[3 * i], c->N[3 * i + 1], c->N[3 * i + 2], 0.f);
     std::vector<float4> nodes4(bvh.nodes.size() / 4);
     std::memcpy(nodes4.data(), bvh.nodes.data(), bvh.nodes.size() * sizeof(float));
 
+    /* one blob of 16-B aligned sections: the same offsets address it in HBM
+     * and, for scenes that fit (SceneDev::lds_bytes), in each block's LDS copy */
+    std::vector<unsigned char> blob;
+    auto put = [&](const void *src, size_t n) -> size_t {
+        size_t off = (blob.size() + 15) & ~(size_t)15;
+        blob.resize(off + n, 0);
+        if (n) std::memcpy(&blob[off], src, n);
+        return off;
+    };
+    const size_t o_nodes = put(nodes4.data(), nodes4.size() * sizeof(float4));
+    const size_t o_refs = put(bvh.refs.data(), bvh.refs.size() * sizeof(uint32_t));
+    const size_t o_geo = put(tri_geo.data(), tri_geo.size() * sizeof(float4));
+    const size_t o_shade = put(tri_shade.data(), tri_shade.size() * sizeof(float4));
+    const size_t o_tid = put(tri_id.data(), tri_id.size() * sizeof(uint32_t));
+    const size_t o_info = put(tri_info.data(), tri_info.size() * sizeof(int4));
+    const size_t o_norms = put(norms.data(), norms.size() * sizeof(float4));
+    const size_t o_disks = put(c->disks.data(), c->disks.size() * sizeof(float4));
+    const size_t o_spheres = put(c->spheres.data(), c->spheres.size() * sizeof(float4));
+    const size_t o_mats = put(c->materials.data(), c->materials.size() * sizeof(float4));
+    const size_t o_lights = put(c->lights.data(), c->lights.size() * sizeof(LightDev));
+    blob.resize(std::max<size_t>((blob.size() + 15) & ~(size_t)15, 16), 0);
     int rc;
-    if ((rc = upload(c, c->d_nodes, nodes4))) return rc;
-    if ((rc = upload(c, c->d_refs, bvh.refs))) return rc;
-    if ((rc = upload(c, c->d_tri_geo, tri_geo))) return rc;
-    if ((rc = upload(c, c->d_tri_info, tri_info))) return rc;
-    if ((rc = upload(c, c->d_tri_id, tri_id))) return rc;
-    if ((rc = upload(c, c->d_verts, verts))) return rc;
-    if ((rc = upload(c, c->d_norms, norms))) return rc;
-    if ((rc = upload(c, c->d_uvs, uvs))) return rc;
-    if ((rc = upload(c, c->d_meshes, meshes))) return rc;
-    if ((rc = upload(c, c->d_disks, c->disks))) return rc;
-    if ((rc = upload(c, c->d_spheres, c->spheres))) return rc;
-    if ((rc = upload(c, c->d_materials, c->materials))) return rc;
-    if ((rc = upload(c, c->d_lights, c->lights))) return rc;
+    if ((rc = upload(c, c->d_scene, blob))) return rc;
 
     SceneDev &S = c->S;
-    S.nodes = c->d_nodes.as<float4>(); S.refs = c->d_refs.as<uint32_t>();
-    S.tri_geo = c->d_tri_geo.as<float4>(); S.tri_info = c->d_tri_info.as<int4>(); S.tri_id = c->d_tri_id.as<uint32_t>();
-    S.verts = c->d_verts.as<float4>(); S.norms = c->d_norms.as<float4>(); S.uvs = c->d_uvs.as<float2>();
-    S.meshes = c->d_meshes.as<int4>(); S.disks = c->d_disks.as<float4>(); S.spheres = c->d_spheres.as<float4>();
-    S.materials = c->d_materials.as<float4>(); S.lights = c->d_lights.as<LightDev>();
+    const char *base = c->d_scene.as<char>();
+    S.blob = base;
+    S.blob_bytes = (uint32_t)std::min<size_t>(blob.size(), 0xffffffffu);
+    S.lds_bytes = blob.size() <= LDS_SCENE_MAX ? (uint32_t)blob.size() : 0u;
+    S.nodes = (const float4 *)(base + o_nodes); S.refs = (const uint32_t *)(base + o_refs);
+    S.tri_geo = (const float4 *)(base + o_geo); S.tri_shade = (const float4 *)(base + o_shade);
+    S.tri_id = (const uint32_t *)(base + o_tid); S.tri_info = (const int4 *)(base + o_info);
+    S.norms = (const float4 *)(base + o_norms); S.disks = (const float4 *)(base + o_disks);
+    S.spheres = (const float4 *)(base + o_spheres); S.materials = (const float4 *)(base + o_mats);
+    S.lights = (const LightDev *)(base + o_lights);
     S.n_lights = (int)c->lights.size(); S.n_nodes = (int)nodes4.size() / 4;
     /* a push happens only when descending a level, so depth + 1 entries suffice;
      * sizing the LDS stack by the actual tree keeps occupancy VGPR-bound */
@@ -653,13 +707,14 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
     T.slots = c->d_slots.as<pm_photon>();
     halton_perm((uint32_t)pass, T.perm);
     T.path_begin = path_begin; T.path_count = path_count; T.slot_path_base = slot_path_base;
+    T.per_block = c->trace_per_block;
     T.pass = pass; T.mpc = (int)mpc; T.max_spec = p->max_specular_depth; T.light_index = p->light_source_index;
     T.eps = p->scene_epsilon; T.seed = p->rng_seed;
+    T.counters = c->d_counters.as<unsigned long long>() + 4;
+    if (c->counting) HIPCHK(c, hipMemsetAsync(T.counters, 0, 32, s));
     timer_begin(c, "trace", s);
-    /* invalid = zero (build divergence: the reference leaves early-return slots stale) */
-    HIPCHK(c, hipMemsetAsync(c->d_slots.as<pm_photon>() + (path_begin - slot_path_base) * mpc, 0,
-                             (size_t)(path_count * mpc) * sizeof(pm_photon), s));
-    HIPCHK(c, launch_trace(T, s));
+    /* the kernel writes all path_count * mpc slots: deposits, then zeros */
+    HIPCHK(c, launch_trace(T, c->counting, s));
     timer_end(c, "trace", s);
     c->slots_used = std::max(c->slots_used, end_slot);
     return PM_OK;
@@ -966,6 +1021,15 @@ int pm_gather_counters(void *ptr, int64_t out[4]) {
     unsigned long long h[4];
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(h, c->d_counters.p, 32, hipMemcpyDeviceToHost));
+    for (int i = 0; i < 4; ++i) out[i] = (int64_t)h[i];
+    return PM_OK;
+}
+
+int pm_trace_counters(void *ptr, int64_t out[4]) {
+    GETCTX(ptr);
+    unsigned long long h[4];
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(h, c->d_counters.as<unsigned long long>() + 4, 32, hipMemcpyDeviceToHost));
     for (int i = 0; i < 4; ++i) out[i] = (int64_t)h[i];
     return PM_OK;
 }

@@ -11,8 +11,7 @@ namespace pm {
 
 namespace {
 
-constexpr int LEAF_MAX = 4;
-constexpr int NBINS = 16;
+constexpr int NBINS = 32;
 
 struct Box {
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -33,6 +32,7 @@ struct BvhBuilder {
     std::vector<BuildPrim> &P;
     std::vector<float> &nodes;
     int max_depth;
+    BvhCost cost;
     int depth_seen = 0;
 
     int alloc() {
@@ -94,10 +94,11 @@ struct BvhBuilder {
         float A = full.half_area();
         if (best_axis < 0) {
             /* all centroids coincide: median split by index */
-            return n > LEAF_MAX ? b + n / 2 : -1;
+            return n > cost.leaf_max ? b + n / 2 : -1;
         }
-        float split_cost = 0.125f + (A > 0.f ? best_cost / A : (float)n);
-        if (n <= 8 && (float)n <= split_cost) return -1;
+        /* SAH: C_trav + sum_child (A_child / A) N_child C_isect vs a leaf's N C_isect */
+        float split_cost = cost.c_trav + (A > 0.f ? best_cost / A : (float)n) * cost.c_isect;
+        if (n <= cost.leaf_max && (float)n * cost.c_isect <= split_cost) return -1;
         float ext = cb.hi[best_axis] - cb.lo[best_axis];
         float k = NBINS / ext;
         int a = best_axis;
@@ -119,7 +120,7 @@ struct BvhBuilder {
         box = Box();
         for (int i = b; i < e; ++i) box.grow(P[i].lo, P[i].hi);
         int split = -1;
-        if (e - b > LEAF_MAX && depth < max_depth) split = find_split(b, e);
+        if (e - b > 1 && depth < max_depth) split = find_split(b, e);
         if (split < 0) { code = ~b; count = e - b; return; }
         int id = alloc();
         depth_seen = std::max(depth_seen, depth + 1);
@@ -134,10 +135,10 @@ struct BvhBuilder {
 
 } // namespace
 
-void build_bvh(std::vector<BuildPrim> &prims, int max_depth, BvhOut &out) {
+void build_bvh(std::vector<BuildPrim> &prims, int max_depth, BvhOut &out, const BvhCost &cost) {
     out.nodes.clear();
     out.refs.clear();
-    BvhBuilder B{prims, out.nodes, max_depth};
+    BvhBuilder B{prims, out.nodes, max_depth, cost};
     int n = (int)prims.size();
     Box empty;
     if (n == 0) {
@@ -145,7 +146,7 @@ void build_bvh(std::vector<BuildPrim> &prims, int max_depth, BvhOut &out) {
         B.write_node(id, empty, ~0, -1, empty, ~0, -1);
     } else {
         int root = B.alloc();
-        int split = n > LEAF_MAX ? B.find_split(0, n) : -1;
+        int split = n > 1 ? B.find_split(0, n) : -1;
         if (split < 0) {
             Box all;
             for (auto &p : prims) all.grow(p.lo, p.hi);
@@ -159,6 +160,35 @@ void build_bvh(std::vector<BuildPrim> &prims, int max_depth, BvhOut &out) {
         }
     }
     out.depth = B.depth_seen + 1;
+    /* renumber nodes breadth-first: the first K nodes are then the top levels
+     * of the tree, which the traversal kernels stage in LDS */
+    {
+        const size_t nn = out.nodes.size() / 16;
+        std::vector<int> order, newidx(nn, -1);
+        order.reserve(nn);
+        order.push_back(0);
+        newidx[0] = 0;
+        for (size_t h = 0; h < order.size(); ++h) {
+            const float *nd = &out.nodes[(size_t)order[h] * 16];
+            int ints[4];
+            std::memcpy(ints, &nd[12], sizeof(ints));
+            for (int k = 0; k < 2; ++k)
+                if (ints[2 + k] == 0 && ints[k] >= 0) { /* internal child */
+                    newidx[ints[k]] = (int)order.size();
+                    order.push_back(ints[k]);
+                }
+        }
+        std::vector<float> bfs(order.size() * 16);
+        for (size_t i = 0; i < order.size(); ++i) {
+            std::memcpy(&bfs[i * 16], &out.nodes[(size_t)order[i] * 16], 16 * sizeof(float));
+            int ints[4];
+            std::memcpy(ints, &bfs[i * 16 + 12], sizeof(ints));
+            for (int k = 0; k < 2; ++k)
+                if (ints[2 + k] == 0 && ints[k] >= 0) ints[k] = newidx[ints[k]];
+            std::memcpy(&bfs[i * 16 + 12], ints, sizeof(ints));
+        }
+        out.nodes.swap(bfs);
+    }
     out.refs.resize(prims.size());
     for (size_t i = 0; i < prims.size(); ++i) out.refs[i] = prims[i].ref;
 }

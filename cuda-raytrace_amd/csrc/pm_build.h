@@ -31,7 +31,13 @@ struct BvhOut {
     int depth = 0;
 };
 
-void build_bvh(std::vector<BuildPrim> &prims, int max_depth, BvhOut &out);
+/* SAH cost model: a node visit (two box tests) costs c_trav, a primitive
+ * test c_isect; leaves hold at most leaf_max primitives */
+struct BvhCost {
+    float c_trav = 1.0f, c_isect = 1.0f;
+    int leaf_max = 1;
+};
+void build_bvh(std::vector<BuildPrim> &prims, int max_depth, BvhOut &out, const BvhCost &cost = BvhCost());
 
 /* returns the number of nodes (= valid photons); nodes sized >= that */
 int64_t build_kdtree_pbrt(const pm_photon *slots, int64_t nslots, std::vector<pm_photon> &nodes);

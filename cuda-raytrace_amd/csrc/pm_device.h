@@ -62,10 +62,12 @@ struct SceneDev {
     const float4 *tri_geo;   /* 3 float4 per triangle: (p0, e0.x) (e0.yz, e1.xy) (e1.z, n) */
     const int4 *tri_info;    /* (v0, v1, v2, mesh) */
     const uint32_t *tri_id;  /* global primitive id (tie-break) */
-    const float4 *verts;
+    /* 2 float4 per triangle, computed on the host with the device's exact
+     * IEEE operations (pm_commit): (normalize(n).xyz, material | has_n<<31)
+     * (normalize(dpdu).xyz, light). Hit shading is two loads, not ~60 VALU
+     * ops + 2 sqrt + 3 divides behind a tri_info -> mesh -> vertex chain. */
+    const float4 *tri_shade;
     const float4 *norms;
-    const float2 *uvs;
-    const int4 *meshes;      /* (material, light, has_n, has_uv) */
     const float4 *disks;     /* 5 float4 per disk */
     const float4 *spheres;   /* 4 float4 per sphere */
     const float4 *materials; /* (kd.xyz, type bits) */
@@ -73,7 +75,15 @@ struct SceneDev {
     int n_lights;
     int n_nodes;
     int stack_depth; /* LDS stack entries per lane (>= BVH depth, <= BVH_STACK_DEPTH) */
+    /* all arrays above are 16-B aligned sections of one blob in HBM */
+    const char *blob;
+    uint32_t blob_bytes;
+    uint32_t lds_bytes; /* = blob_bytes when the blob fits LDS_SCENE_MAX (LDS-resident mode), else 0 */
 };
+
+/* Scenes up to this size are copied into each block's LDS and traversed from
+ * there (Cornell C2: ~4 KB); larger ones are traversed from HBM/L2. */
+constexpr uint32_t LDS_SCENE_MAX = 16384;
 
 struct Ray { v3 o, d; float tmin, tmax; };
 
@@ -157,9 +167,13 @@ PMD bool isect_disk(const float4 *dk, const Ray &ray, float *thit_out) {
     float localy = dot(local, y) * e.x;
     float dist2 = localx * localx + localy * localy;
     if (dist2 > 1.f || dist2 < a.w * a.w) return false;
-    float phi = pmdm_atan2f(localy, localx);
-    if (phi < 0) phi = (float)((double)phi + 2.f * M_PI);
-    if (phi > b.w) return false;
+    /* phi <= (float)2pi always, so a full disk (phiMax >= (float)2pi) can
+     * never reject here: skip the double-precision atan2 (same result) */
+    if (b.w < 6.28318548202514648438f) {
+        float phi = pmdm_atan2f(localy, localx);
+        if (phi < 0) phi = (float)((double)phi + 2.f * M_PI);
+        if (phi > b.w) return false;
+    }
     *thit_out = thit;
     return true;
 }
@@ -217,13 +231,46 @@ PMD v3 safe_inv(v3 d) {
     float x = fabsf(d.x) < tiny ? copysignf(tiny, d.x) : d.x;
     float y = fabsf(d.y) < tiny ? copysignf(tiny, d.y) : d.y;
     float z = fabsf(d.z) < tiny ? copysignf(tiny, d.z) : d.z;
-    return mk(1.0f / x, 1.0f / y, 1.0f / z);
+    /* hardware reciprocal (<= 1 ulp): the slab test only culls, and every
+     * prim box is padded by 1e-4 relative at commit, so an ulp in 1/d never
+     * drops a box holding the closest hit (which is order-independent) */
+    return mk(__builtin_amdgcn_rcpf(x), __builtin_amdgcn_rcpf(y), __builtin_amdgcn_rcpf(z));
+}
+
+/* per-lane traversal census (bench roofline / DESIGN.md): nodes entered and
+ * primitive tests; NoCensus compiles to nothing */
+struct NoCensus { PMD void node() {} PMD void prim() {} };
+struct Census {
+    uint32_t nodes = 0, prims = 0;
+    PMD void node() { ++nodes; }
+    PMD void prim() { ++prims; }
+};
+
+/* The scene as a kernel sees it. LDS=true: the whole blob is copied into
+ * `lds` by the block (every thread calls; __syncthreads() before use) and
+ * every pointer is rebased into it. The rebased pointers derive from a
+ * __shared__ array, so the compiler emits ds_read (not flat) loads. */
+template <bool LDS>
+PMD SceneDev scene_view(const SceneDev &S, uint4 *lds, int tid, int nthreads) {
+    if (!LDS) return S;
+    const uint4 *src = reinterpret_cast<const uint4 *>(S.blob);
+    for (int i = tid; i < (int)(S.lds_bytes / 16); i += nthreads) lds[i] = src[i];
+    SceneDev V = S;
+    const char *b = reinterpret_cast<const char *>(lds);
+#define PM_REBASE(f) V.f = reinterpret_cast<decltype(V.f)>(b + (reinterpret_cast<const char *>(S.f) - S.blob))
+    PM_REBASE(nodes); PM_REBASE(refs); PM_REBASE(tri_geo); PM_REBASE(tri_info); PM_REBASE(tri_id);
+    PM_REBASE(tri_shade); PM_REBASE(norms); PM_REBASE(disks); PM_REBASE(spheres); PM_REBASE(materials);
+    PM_REBASE(lights);
+#undef PM_REBASE
+    V.blob = b;
+    return V;
 }
 
 /* Tests the primitives of one leaf; for ANY=true returns at the first hit. */
-template <bool ANY>
-PMD bool leaf_isect(const SceneDev &S, uint32_t start, uint32_t count, const Ray &ray, Hit &best) {
+template <bool ANY, class C>
+PMD bool leaf_isect(const SceneDev &S, uint32_t start, uint32_t count, const Ray &ray, Hit &best, C &cen) {
     for (uint32_t k = start; k < start + count; ++k) {
+        cen.prim();
         uint32_t ref = S.refs[k];
         uint32_t kind = ref >> 30, idx = ref & 0x3fffffffu;
         float t, b = 0.f, g = 0.f;
@@ -256,8 +303,8 @@ PMD bool leaf_isect(const SceneDev &S, uint32_t start, uint32_t count, const Ray
  * Closest hit (ANY=false) or occlusion (ANY=true). Node = 4 float4:
  * (l.lo, l.hi.x) (l.hi.yz, r.lo.xy) (r.lo.z, r.hi) (left, right, lcount, rcount);
  * child >= 0 internal node, child < 0 leaf with refs start ~child. */
-template <bool ANY>
-PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int stride) {
+template <bool ANY, class C>
+PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int stride, C &cen) {
     best.t = ray.tmax;
     best.gid = 0xffffffffu;
     best.ref = 0xffffffffu;
@@ -266,6 +313,7 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
     int cur = 0;
     /* every node is entered at most once per ray: a bound every lane reaches */
     for (int guard = 0; guard <= S.n_nodes; ++guard) {
+        cen.node();
         const float4 *nd = S.nodes + 4 * cur;
         float4 a = nd[0], b = nd[1], c = nd[2];
         int4 ch = *reinterpret_cast<const int4 *>(nd + 3);
@@ -274,11 +322,11 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
         bool hl = tl != __int_as_float(0x7f800000) && ch.z >= 0;
         bool hr = tr != __int_as_float(0x7f800000) && ch.w >= 0;
         if (hl && ch.x < 0) {
-            if (leaf_isect<ANY>(S, (uint32_t)~ch.x, (uint32_t)ch.z, ray, best)) return true;
+            if (leaf_isect<ANY>(S, (uint32_t)~ch.x, (uint32_t)ch.z, ray, best, cen)) return true;
             hl = false;
         }
         if (hr && ch.y < 0) {
-            if (leaf_isect<ANY>(S, (uint32_t)~ch.y, (uint32_t)ch.w, ray, best)) return true;
+            if (leaf_isect<ANY>(S, (uint32_t)~ch.y, (uint32_t)ch.w, ray, best, cen)) return true;
             hr = false;
         }
         if (hl && hr && sp < S.stack_depth) {
@@ -299,6 +347,11 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
     }
     return ANY ? false : best.ref != 0xffffffffu;
 }
+template <bool ANY>
+PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int stride) {
+    NoCensus none;
+    return traverse<ANY>(S, ray, best, stack, stride, none);
+}
 
 /* ------------------------------------------------------------- shading */
 struct Geo { v3 ns, dpdu; int material, light; };
@@ -311,40 +364,16 @@ PMD Geo shade(const SceneDev &S, const Ray &ray, const Hit &h) {
     uint32_t kind = h.ref >> 30, idx = h.ref & 0x3fffffffu;
     v3 nsw, dpduw;
     if (kind == PRIM_TRI) {
-        int4 ti = S.tri_info[idx];
-        int4 m = S.meshes[ti.w];
-        v3 p0 = xyz(S.verts[ti.x]), p1 = xyz(S.verts[ti.y]), p2 = xyz(S.verts[ti.z]);
-        const v3 e0 = p1 - p0, e1 = p0 - p2;
-        const v3 n = cross(e1, e0);
-        float uv0x, uv0y, uv1x, uv1y, uv2x, uv2y;
-        if (!m.w) { uv0x = 0.f; uv0y = 0.f; uv1x = 1.f; uv1y = 0.f; uv2x = 0.f; uv2y = 1.f; }
-        else {
-            float2 q0 = S.uvs[ti.x], q1 = S.uvs[ti.y], q2 = S.uvs[ti.z];
-            uv0x = q0.x; uv0y = q0.y; uv1x = q1.x; uv1y = q1.y; uv2x = q2.x; uv2y = q2.y;
-        }
-        float du1 = uv0x - uv2x, du2 = uv1x - uv2x, dv1 = uv0y - uv2y, dv2 = uv1y - uv2y;
-        v3 dp1 = p0 - p2, dp2 = p1 - p2;
-        float determinant = du1 * dv2 - dv1 * du2;
-        v3 dpdu;
-        if (determinant == 0.0f) {
-            if (fabsf(n.x) > fabsf(n.y)) {
-                float invLen = 1.f / sqrtf(n.x * n.x + n.z * n.z);
-                dpdu = mk(-n.z * invLen, 0.f, n.x * invLen);
-            } else {
-                float invLen = 1.f / sqrtf(n.y * n.y + n.z * n.z);
-                dpdu = mk(0.f, n.z * invLen, n.y * invLen);
-            }
-        } else {
-            float invdet = 1.f / determinant;
-            dpdu = (dv2 * dp1 - dv1 * dp2) * invdet;
-        }
-        v3 ns = n;
-        if (m.z) {
-            v3 n0 = xyz(S.norms[ti.x]), n1 = xyz(S.norms[ti.y]), n2 = xyz(S.norms[ti.z]);
-            ns = n1 * h.beta + n2 * h.gamma + n0 * (1.0f - h.beta - h.gamma);
-        }
-        nsw = ns; dpduw = dpdu;
-        g.material = m.x; g.light = m.y;
+        /* per-triangle frame (cudatrianglemesh.cu:36-78 + normalize), see tri_shade */
+        const float4 s0 = S.tri_shade[2 * idx], s1 = S.tri_shade[2 * idx + 1];
+        const int mb = fbits(s0.w);
+        g.material = mb & 0x7fffffff; g.light = fbits(s1.w);
+        g.dpdu = xyz(s1);
+        if (mb >= 0) { g.ns = xyz(s0); return g; }
+        const int4 ti = S.tri_info[idx]; /* shading normals: interpolated per hit */
+        v3 n0 = xyz(S.norms[ti.x]), n1 = xyz(S.norms[ti.y]), n2 = xyz(S.norms[ti.z]);
+        g.ns = normalize(n1 * h.beta + n2 * h.gamma + n0 * (1.0f - h.beta - h.gamma));
+        return g;
     } else if (kind == PRIM_DISK) {
         const float4 *dk = S.disks + 5 * idx;
         float4 a = dk[0], b = dk[1], c = dk[2], d = dk[3], e = dk[4];
@@ -462,6 +491,23 @@ PMD v3 sample_le(const LightDev &L, float lu1, float lu2, float u1, float u2, fl
 PMD v3 light_le(const LightDev &L, v3 wow) {
     if (dot(xyz(L.n_area), wow) > 0.f) return xyz(L.le);
     return mk(0.f, 0.f, 0.f);
+}
+
+/* ------------------------------------------------------------- census */
+PMD unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+/* four census counters summed over the wave, one atomic each per wave (only
+ * in counting launches, never in timed ones); every lane of the wave calls */
+PMD void count4(unsigned long long *c, unsigned long long a, unsigned long long b, unsigned long long d,
+                unsigned long long e) {
+    a = wave_sum(a); b = wave_sum(b); d = wave_sum(d); e = wave_sum(e);
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&c[0], a); atomicAdd(&c[1], b); atomicAdd(&c[2], d); atomicAdd(&c[3], e);
+    }
 }
 
 /* record index -> pixel of an 8x8-tile ordering */

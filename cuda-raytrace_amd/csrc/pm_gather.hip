@@ -17,22 +17,6 @@ namespace pm {
 /* ====================================================================== */
 /* gather                                                                 */
 /* ====================================================================== */
-PMD unsigned long long wave_sum(unsigned long long v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    return v;
-}
-
-/* census counters [visited, in radius, bucket rows, active records]: one
- * atomic per wave (only in counting launches, never in timed ones) */
-PMD void count4(unsigned long long *c, unsigned long long a, unsigned long long b, unsigned long long d,
-                unsigned long long e) {
-    a = wave_sum(a); b = wave_sum(b); d = wave_sum(d); e = wave_sum(e);
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&c[0], a); atomicAdd(&c[1], b); atomicAdd(&c[2], d); atomicAdd(&c[3], e);
-    }
-}
-
 /* gathering.cu:104-126 PPM update */
 PMD void ppm_apply(float4 &st, float &N, int M, v3 L, float alpha) {
     if (M > 0) {

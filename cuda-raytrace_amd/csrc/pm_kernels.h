@@ -1,6 +1,6 @@
 /*
  * pm_kernels.h — kernel parameter blocks and launcher declarations shared by
- * the host orchestration (pm_api.cpp) and the HIP kernels (pm_kernels.hip).
+ * the host orchestration (pm_api.cpp) and the HIP kernels (pm_trace.hip, pm_bucket.hip, pm_gather.hip).
  */
 #pragma once
 #include <hip/hip_runtime.h>
@@ -11,7 +11,7 @@
 namespace pm {
 
 constexpr int EYE_BLOCK = 128;     /* traversal kernels: LDS stack column per lane */
-constexpr int TRACE_BLOCK = 128;
+constexpr int TRACE_BLOCK = 256;    /* k_trace: 4 waves compact paths together */
 constexpr int BVH_STACK = BVH_STACK_DEPTH; /* >= max BVH depth (builder enforces it) */
 constexpr int GATHER_BLOCK = 256;
 constexpr int KD_STACK = 32;       /* >= pbrt median kd-tree depth for < 2^31 photons */
@@ -43,9 +43,11 @@ struct TraceParams {
     pm_photon *slots;
     uint32_t perm[28];
     int64_t path_begin, path_count, slot_path_base;
+    int64_t per_block; /* paths in each block's pool (>= 1; TRACE_BLOCK = no refills) */
     int pass, mpc, max_spec, light_index;
     float eps;
     uint32_t seed;
+    unsigned long long *counters; /* census [rays, nodes, prim tests, deposits] */
 };
 
 struct GridDesc {
@@ -94,7 +96,8 @@ struct FinalParams {
 };
 
 hipError_t launch_eye(const EyeParams &p, hipStream_t s);
-hipError_t launch_trace(const TraceParams &p, hipStream_t s);
+/* writes every slot of its paths (deposits, then zeros); count: census */
+hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s);
 /* photon-bucket build (pm_bucket.hip): count + rank, scan, fill.
  * count and cell_start have ncells + 1 entries; cell_start[ncells] = valid
  * photons; scratch holds bucket_scratch_words() uint32 */

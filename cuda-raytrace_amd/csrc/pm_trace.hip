@@ -9,6 +9,8 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "pm_kernels.h"
 
 #pragma clang fp contract(off)
@@ -18,12 +20,15 @@ namespace pm {
 /* ====================================================================== */
 /* eye pass                                                               */
 /* ====================================================================== */
+template <bool LDS>
 __global__ __launch_bounds__(EYE_BLOCK) void k_eye(EyeParams P) {
-    extern __shared__ int stk[]; /* stack_depth x EYE_BLOCK */
+    extern __shared__ __attribute__((aligned(16))) int stk[]; /* [stack_depth x EYE_BLOCK][scene blob (LDS)] */
     int *stack = stk + threadIdx.x;
+    const SceneDev S = scene_view<LDS>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * EYE_BLOCK),
+                                       threadIdx.x, EYE_BLOCK);
+    if (LDS) __syncthreads();
     const int64_t r = (int64_t)blockIdx.x * EYE_BLOCK + threadIdx.x;
     if (r >= P.R.count) return;
-    const SceneDev &S = P.S;
 
     Ray ray;
     int64_t pixel;
@@ -123,7 +128,9 @@ __global__ __launch_bounds__(EYE_BLOCK) void k_eye(EyeParams P) {
 hipError_t launch_eye(const EyeParams &p, hipStream_t s) {
     if (p.R.count <= 0) return hipSuccess;
     unsigned grid = (unsigned)((p.R.count + EYE_BLOCK - 1) / EYE_BLOCK);
-    hipLaunchKernelGGL(k_eye, dim3(grid), dim3(EYE_BLOCK), (size_t)p.S.stack_depth * EYE_BLOCK * 4, s, p);
+    const size_t lds = (size_t)p.S.stack_depth * EYE_BLOCK * 4 + p.S.lds_bytes;
+    if (p.S.lds_bytes) hipLaunchKernelGGL(k_eye<true>, dim3(grid), dim3(EYE_BLOCK), lds, s, p);
+    else hipLaunchKernelGGL(k_eye<false>, dim3(grid), dim3(EYE_BLOCK), lds, s, p);
     return hipGetLastError();
 }
 
@@ -140,20 +147,21 @@ PMD void store_photon(pm_photon *dst, v3 p, v3 a, v3 wi) {
     q[4] = make_float2(wi.y, wi.z);
 }
 
-__global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceParams P) {
-    extern __shared__ int stk[]; /* stack_depth x TRACE_BLOCK */
-    __shared__ uint32_t perm[28];
-    if (threadIdx.x < 28) perm[threadIdx.x] = P.perm[threadIdx.x];
-    __syncthreads();
-    int *stack = stk + threadIdx.x;
-    const int64_t i = (int64_t)blockIdx.x * TRACE_BLOCK + threadIdx.x;
-    if (i >= P.path_count) return;
-    const SceneDev &S = P.S;
-    const uint64_t path = (uint64_t)(P.path_begin + i);
-    const uint32_t mpc = (uint32_t)P.mpc;
-    pm_photon *slots = P.slots + (size_t)(path - (uint64_t)P.slot_path_base) * mpc;
-    const uint32_t pm_index = (uint32_t)(path * mpc);
+/* Photon paths (photontracing.cu:80-185) split into ray steps so a block can
+ * compact its live paths between steps. Per-path state (12 words) lives in
+ * registers and moves through LDS only at compaction. */
+struct PathState {
+    Ray ray;         /* tmax is RT_DEFAULT_MAX at every step */
+    v3 alpha;
+    uint32_t pid;    /* global path id */
+    uint32_t nI;     /* photons-in-path counter (reference nI) */
+    uint32_t spec;   /* specular bounces so far */
+    uint32_t stored; /* slots [0, stored) written */
+};
 
+/* emission: Halton light sample -> first ray (photontracing.cu:88-117) */
+PMD bool emit_path(const TraceParams &P, const SceneDev &S, const uint32_t *perm, uint32_t pid, PathState &st) {
+    const uint32_t pm_index = pid * (uint32_t)P.mpc;
     float smp[4];
     {
         const uint32_t b[4] = {2, 3, 5, 7};
@@ -162,48 +170,176 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceParams P) {
         for (int k = 0; k < 4; ++k) smp[k] = permuted_radical_inverse(pm_index, b[k], perm + off[k]);
     }
     const LightDev Lt = S.lights[P.light_index];
-    Ray ray; v3 N1; float pdf;
-    v3 Le = sample_le(Lt, smp[0], smp[1], smp[2], smp[3], P.eps, &ray, &N1, &pdf);
-    if (pdf == 0.0f || is_black(Le)) return;
-    ray.tmax = RT_DEFAULT_MAX;
-    v3 alpha = (absdot(N1, ray.d) * Le) / pdf;
-    uint32_t nI = 0;
-    int spec = 0;
+    v3 N1; float pdf;
+    v3 Le = sample_le(Lt, smp[0], smp[1], smp[2], smp[3], P.eps, &st.ray, &N1, &pdf);
+    st.pid = pid; st.nI = 0; st.spec = 0; st.stored = 0;
+    if (pdf == 0.0f || is_black(Le)) return false;
+    st.ray.tmax = RT_DEFAULT_MAX;
+    st.alpha = (absdot(N1, st.ray.d) * Le) / pdf;
+    return true;
+}
+
+/* one ray of a path: trace, then specular continuation or diffuse deposit +
+ * Lambert bounce (photontracing.cu:119-183); false when the path ends */
+template <class C>
+PMD bool path_step(const TraceParams &P, const SceneDev &S, int *stack, PathState &st, C &cen) {
+    const uint32_t mpc = (uint32_t)P.mpc;
     Hit h;
-    while (true) {
-        if (!traverse<false>(S, ray, h, stack, TRACE_BLOCK)) return;
-        Geo g = shade(S, ray, h);
-        v3 hit_point = ray.o + h.t * ray.d;
-        float4 m = S.materials[g.material];
-        int mtype = fbits(m.w);
-        if (is_specular(mtype)) {
-            v3 wi;
-            if (!material_specular(mtype, g, -ray.d, &wi)) return;
-            if (++spec > P.max_spec) return;
-            if (nI == 0) nI++;
-            ray.o = hit_point; ray.d = wi; ray.tmin = P.eps; ray.tmax = RT_DEFAULT_MAX;
-            continue;
-        }
-        v3 wo = -ray.d;
-        if (nI >= 1) store_photon(slots + (nI - 1), hit_point, alpha, wo);
-        if (nI >= mpc) return;
-        uint32_t o4[4];
-        pmdm_philox4x32_10(pm_index + nI, (uint32_t)P.pass, 0u, 0u, P.seed, 0u, o4);
-        float u1 = pmdm_u01(o4[0]), u2 = pmdm_u01(o4[1]);
-        v3 wiw; float bpdf;
-        v3 fr = sample_f(xyz(m), g, wo, u1, u2, &wiw, &bpdf);
-        if (is_black(fr) || bpdf == 0.f) return;
-        v3 anew = alpha * fr * absdot(wiw, g.ns) / bpdf;
-        alpha = anew;
-        nI++;
-        ray.o = hit_point; ray.d = wiw; ray.tmin = P.eps; ray.tmax = RT_DEFAULT_MAX;
+    if (!traverse<false>(S, st.ray, h, stack, TRACE_BLOCK, cen)) return false;
+    Geo g = shade(S, st.ray, h);
+    v3 hit_point = st.ray.o + h.t * st.ray.d;
+    float4 m = S.materials[g.material];
+    int mtype = fbits(m.w);
+    if (is_specular(mtype)) {
+        v3 wi;
+        if (!material_specular(mtype, g, -st.ray.d, &wi)) return false;
+        if ((int)++st.spec > P.max_spec) return false;
+        if (st.nI == 0) st.nI++;
+        st.ray.o = hit_point; st.ray.d = wi; st.ray.tmin = P.eps; st.ray.tmax = RT_DEFAULT_MAX;
+        return true;
+    }
+    v3 wo = -st.ray.d;
+    if (st.nI >= 1) {
+        pm_photon *slots = P.slots + (size_t)(st.pid - (uint64_t)P.slot_path_base) * mpc;
+        store_photon(slots + (st.nI - 1), hit_point, st.alpha, wo);
+        st.stored = st.nI;
+    }
+    if (st.nI >= mpc) return false;
+    const uint32_t pm_index = st.pid * mpc;
+    uint32_t o4[4];
+    pmdm_philox4x32_10(pm_index + st.nI, (uint32_t)P.pass, 0u, 0u, P.seed, 0u, o4);
+    float u1 = pmdm_u01(o4[0]), u2 = pmdm_u01(o4[1]);
+    v3 wiw; float bpdf;
+    v3 fr = sample_f(xyz(m), g, wo, u1, u2, &wiw, &bpdf);
+    if (is_black(fr) || bpdf == 0.f) return false;
+    v3 anew = st.alpha * fr * absdot(wiw, g.ns) / bpdf;
+    st.alpha = anew;
+    st.nI++;
+    st.ray.o = hit_point; st.ray.d = wiw; st.ray.tmin = P.eps; st.ray.tmax = RT_DEFAULT_MAX;
+    return true;
+}
+
+/* a finished path's unused slots are invalid = zero (the reference leaves
+ * them stale, DESIGN.md divergences); written here instead of a memset pass */
+PMD void finish_path(const TraceParams &P, const PathState &st) {
+    const uint32_t mpc = (uint32_t)P.mpc;
+    pm_photon *slots = P.slots + (size_t)(st.pid - (uint64_t)P.slot_path_base) * mpc;
+    const float2 z = make_float2(0.f, 0.f);
+    for (uint32_t k = st.stored; k < mpc; ++k) {
+        float2 *q = reinterpret_cast<float2 *>(slots + k);
+        q[0] = z; q[1] = z; q[2] = z; q[3] = z; q[4] = z;
     }
 }
 
-hipError_t launch_trace(const TraceParams &p, hipStream_t s) {
+constexpr int STATE_WORDS = 13;
+
+PMD void state_put(uint32_t (*lds)[TRACE_BLOCK], int slot, const PathState &st) {
+    lds[0][slot] = __float_as_uint(st.ray.o.x); lds[1][slot] = __float_as_uint(st.ray.o.y);
+    lds[2][slot] = __float_as_uint(st.ray.o.z); lds[3][slot] = __float_as_uint(st.ray.d.x);
+    lds[4][slot] = __float_as_uint(st.ray.d.y); lds[5][slot] = __float_as_uint(st.ray.d.z);
+    lds[6][slot] = __float_as_uint(st.ray.tmin); lds[7][slot] = __float_as_uint(st.alpha.x);
+    lds[8][slot] = __float_as_uint(st.alpha.y); lds[9][slot] = __float_as_uint(st.alpha.z);
+    lds[10][slot] = st.pid; lds[11][slot] = st.nI | (st.stored << 8); lds[12][slot] = st.spec;
+}
+
+PMD void state_get(uint32_t (*lds)[TRACE_BLOCK], int slot, PathState &st) {
+    st.ray.o = mk(__uint_as_float(lds[0][slot]), __uint_as_float(lds[1][slot]), __uint_as_float(lds[2][slot]));
+    st.ray.d = mk(__uint_as_float(lds[3][slot]), __uint_as_float(lds[4][slot]), __uint_as_float(lds[5][slot]));
+    st.ray.tmin = __uint_as_float(lds[6][slot]);
+    st.ray.tmax = RT_DEFAULT_MAX;
+    st.alpha = mk(__uint_as_float(lds[7][slot]), __uint_as_float(lds[8][slot]), __uint_as_float(lds[9][slot]));
+    st.pid = lds[10][slot];
+    st.nI = lds[11][slot] & 0xffu; st.stored = lds[11][slot] >> 8;
+    st.spec = lds[12][slot];
+}
+
+/* Block-compacting photon tracer. Block b owns paths
+ * [b*per_block, (b+1)*per_block) of the launch. Each iteration every live
+ * thread advances its path by one ray; then live paths are compacted to the
+ * front of the block (wave ballot + popcount ranks, LDS state exchange) and
+ * the tail is refilled with fresh paths from the block's pool. Dead lanes
+ * thus retire whole waves instead of idling inside them: the kernel is
+ * VALU-issue bound, and a wave otherwise runs until its longest path ends.
+ * Results are identical to one-thread-per-path (path math unchanged).
+ * COUNT: census [rays traced, BVH nodes entered, primitive tests, photons
+ * deposited], one atomic per wave (counting launches only, never timed). */
+template <int COUNT, bool LDS>
+__global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceParams P) {
+    extern __shared__ __attribute__((aligned(16))) int stk[]; /* [stack_depth x TRACE_BLOCK][scene blob (LDS)] */
+    __shared__ uint32_t perm[28];
+    __shared__ uint32_t sstate[STATE_WORDS][TRACE_BLOCK];
+    __shared__ uint32_t wcount[TRACE_BLOCK / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < 28) perm[tid] = P.perm[tid];
+    const SceneDev S = scene_view<LDS>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * TRACE_BLOCK), tid,
+                                       TRACE_BLOCK);
+    __syncthreads();
+    int *stack = stk + tid;
+    typename std::conditional<COUNT != 0, Census, NoCensus>::type cen;
+    uint32_t rays = 0, deposits = 0;
+
+    const int64_t pool_begin = (int64_t)blockIdx.x * P.per_block;
+    const int64_t pool_end = pool_begin + P.per_block < P.path_count ? pool_begin + P.per_block : P.path_count;
+    int64_t next = pool_begin;
+    int live = 0;
+    PathState st;
+    while (true) {
+        const int64_t left = pool_end - next;
+        const int n_new = (int)((int64_t)(TRACE_BLOCK - live) < left ? (int64_t)(TRACE_BLOCK - live) : left);
+        if (live + n_new == 0) break; /* block-uniform: every wave leaves together */
+        bool alive = false;
+        if (tid < live) {
+            alive = true;
+        } else if (tid < live + n_new) {
+            alive = emit_path(P, S, perm, (uint32_t)(P.path_begin + next + (tid - live)), st);
+            if (!alive) finish_path(P, st);
+        }
+        if (alive) {
+            ++rays;
+            alive = path_step(P, S, stack, st, cen);
+            if (!alive) {
+                if (COUNT) deposits += st.stored;
+                finish_path(P, st);
+            }
+        }
+        next += n_new;
+        /* compaction: rank = live paths before this thread in the block */
+        const unsigned long long bal = __ballot(alive);
+        if (lane == 0) wcount[wave] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        int base = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < TRACE_BLOCK / 64; ++w) {
+            const int c = (int)wcount[w];
+            base += w < wave ? c : 0;
+            total += c;
+        }
+        if (alive) state_put(sstate, base + __popcll(bal & ((1ull << lane) - 1ull)), st);
+        __syncthreads();
+        live = total;
+        if (tid < live) state_get(sstate, tid, st);
+        /* the next writes of wcount / sstate follow the next barrier, which
+         * every thread reaches only after these reads */
+    }
+    if (COUNT) {
+        uint32_t nodes = 0, prims = 0;
+        if constexpr (COUNT != 0) { nodes = cen.nodes; prims = cen.prims; }
+        count4(P.counters, rays, nodes, prims, deposits);
+    }
+}
+
+hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s) {
     if (p.path_count <= 0) return hipSuccess;
-    unsigned grid = (unsigned)((p.path_count + TRACE_BLOCK - 1) / TRACE_BLOCK);
-    hipLaunchKernelGGL(k_trace, dim3(grid), dim3(TRACE_BLOCK), (size_t)p.S.stack_depth * TRACE_BLOCK * 4, s, p);
+    if (p.per_block <= 0) return hipErrorInvalidValue;
+    unsigned grid = (unsigned)((p.path_count + p.per_block - 1) / p.per_block);
+    const size_t lds = (size_t)p.S.stack_depth * TRACE_BLOCK * 4 + p.S.lds_bytes;
+    if (p.S.lds_bytes) {
+        if (count) hipLaunchKernelGGL((k_trace<1, true>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
+        else hipLaunchKernelGGL((k_trace<0, true>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
+    } else {
+        if (count) hipLaunchKernelGGL((k_trace<1, false>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
+        else hipLaunchKernelGGL((k_trace<0, false>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
+    }
     return hipGetLastError();
 }
 

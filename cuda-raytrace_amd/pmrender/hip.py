@@ -72,6 +72,7 @@ def load_library(path=None):
         "pm_kdtree_nodes": (i64, [vp]),
         "pm_download_kdtree": (c_int, [vp, vp, i64]),
         "pm_gather_counters": (c_int, [vp, ctypes.POINTER(i64)]),
+        "pm_trace_counters": (c_int, [vp, ctypes.POINTER(i64)]),
         "pm_set_counting": (c_int, [vp, c_int]),
         "pm_synchronize": (c_int, [vp]),
         "pm_last_kernel_ms": (c_int, [vp, ctypes.c_char_p, ctypes.POINTER(c_double)]),
@@ -284,6 +285,13 @@ class Context:
         self._chk(self.lib.pm_gather_counters(self.h, out))
         vals = tuple(int(v) for v in out)
         return vals if full else vals[:2]
+
+    def trace_counters(self):
+        """(rays traced, BVH nodes entered, primitive tests, photons deposited) of the last
+        trace_photons launched with counting on."""
+        out = (ctypes.c_int64 * 4)()
+        self._chk(self.lib.pm_trace_counters(self.h, out))
+        return tuple(int(v) for v in out)
 
     def synchronize(self):
         self._chk(self.lib.pm_synchronize(self.h))

@@ -225,7 +225,12 @@ int pm_download_kdtree(void *ctx, pm_photon *out, int64_t n);
 /* counters of the last gather: [0] photons (grid) or kd nodes visited,
  * [1] photons in radius (sum of M), [2] bucket rows read (grid), [3] active records */
 int pm_gather_counters(void *ctx, int64_t out[4]);
-/* enable/disable visit counters in gather kernels (off by default: costs an atomic per wave) */
+/* counters of the last pm_trace_photons with counting on: [0] rays traced,
+ * [1] BVH nodes entered, [2] primitive intersection tests, [3] photons
+ * deposited (the traffic census behind the trace roofline) */
+int pm_trace_counters(void *ctx, int64_t out[4]);
+/* enable/disable census counters in the trace and gather kernels (off by
+ * default: costs an atomic per wave) */
 int pm_set_counting(void *ctx, int enabled);
 int pm_synchronize(void *ctx);
 /* Stage timings measured with HIP events recorded on the stream the kernels

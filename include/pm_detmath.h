@@ -76,8 +76,9 @@ PMDM_FN double pmdm_cos_kern(double r) {
  * arguments are angles in [-2pi, 4pi]). */
 PMDM_FN double pmdm_reduce(double x, int *quadrant) {
     double kf = x * PMDM_TWO_OVER_PI;
-    kf = (kf >= 0.0) ? (double)(int64_t)(kf + 0.5) : -(double)(int64_t)(0.5 - kf);
-    *quadrant = (int)((int64_t)kf & 3);
+    /* round half away from zero; trunc == (double)(int64_t) here, one op on gfx950 */
+    kf = (kf >= 0.0) ? __builtin_trunc(kf + 0.5) : -__builtin_trunc(0.5 - kf);
+    *quadrant = (int)kf & 3;
     return (x - kf * PMDM_PIO2_HI) - kf * PMDM_PIO2_LO;
 }
 

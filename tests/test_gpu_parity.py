@@ -59,6 +59,36 @@ def test_photon_trace_sharded_equals_whole(cornell):
     assert_bitexact(np.concatenate([lo, hi]), ref, "sharded photon slots")
 
 
+def test_photon_trace_overwrites_stale_slots(cornell):
+    """The trace kernel writes every slot of its paths: unused ones become zero
+    even over garbage left by an earlier pass (no separate memset)."""
+    from pmrender.abi import PHOTON_DTYPE
+    ctx, orc = cornell
+    p = RenderParams.defaults(paths_per_pass=4096)
+    ctx.upload_slots(np.frombuffer(b"\xa5" * (4096 * 4 * PHOTON_DTYPE.itemsize), PHOTON_DTYPE))
+    ctx.trace_photons(p, 1, 0, 4096)
+    assert_bitexact(ctx.download_slots(4096 * 4), orc.trace_photons(p, 1, 0, 4096), "photon slots over garbage")
+
+
+def test_trace_census(cornell):
+    """Counting launch: same slots; census consistent with the deposits."""
+    ctx, orc = cornell
+    p = RenderParams.defaults(paths_per_pass=16384)
+    ctx.trace_photons(p, 0, 0, 16384)
+    plain = ctx.download_slots(16384 * 4)
+    ctx.set_counting(True)
+    try:
+        ctx.trace_photons(p, 0, 0, 16384)
+        rays, nodes, prims, deposits = ctx.trace_counters()
+    finally:
+        ctx.set_counting(False)
+    counted = ctx.download_slots(16384 * 4)
+    assert_bitexact(counted, plain, "slots of a counting launch")
+    assert deposits == int((plain["bits"] & 1).sum())
+    assert 16384 <= rays <= 16384 * (4 + 1 + 10)
+    assert nodes >= rays and prims >= deposits
+
+
 def _gather_inputs(orc, paths=16384, radius2=25.0):
     p = RenderParams.defaults(paths_per_pass=paths, initial_radius2=radius2)
     recs = orc.eye_pass(p)

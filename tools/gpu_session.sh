@@ -19,6 +19,10 @@ timeout -k 10 900 python -m pytest tests -q -m gpu -p no:cacheprovider > "$O/pyt
 timeout -k 10 600 python bench.py --steps 20 --warmup 3 "$@" > "$O/bench.json" 2> "$O/bench.err"; ok $? bench
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline "$@" > "$O/prof.log" 2>&1; ok $? rocprof_stats
+if [ "${PM_QUICK:-0}" = "1" ]; then
+  find "$O/prof" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats.csv" \;
+  echo done | tee -a "$O/steps.log"; exit 0
+fi
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-census "$@" > "$O/pmc_fetch.log" 2>&1; ok $? pmc_fetch
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$O/pmc_write" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-census "$@" > "$O/pmc_write.log" 2>&1; ok $? pmc_write
 cd "$R"
