@@ -122,6 +122,7 @@ class Context:
         if rc != 0:
             raise PMError(rc, self.lib.pm_last_error(None).decode())
         self.h = h
+        self.device = device
         self.width = self.height = 0
         self.pinhole = False
 
@@ -234,6 +235,24 @@ class Context:
     def final(self, emitted, rec_begin, rec_count, d_out, stream=None):
         self._chk(self.lib.pm_final(self.h, float(emitted), int(rec_begin), int(rec_count), ctypes.c_void_p(d_out),
                                     stream))
+
+    def final_image(self, emitted):
+        """pm_final over all records into a torch device buffer, returned on the
+        host in the oracle's layout: (H, W, 3) raster for pinhole, else per ray."""
+        import torch
+        n = self.num_records()
+        d = torch.empty((n, 3), dtype=torch.float32, device=f"cuda:{self.device}")
+        torch.cuda.synchronize()
+        self.final(emitted, 0, n, d.data_ptr())
+        self.synchronize()
+        out = d.cpu().numpy()
+        if not self.pinhole:
+            return out
+        img = np.zeros((self.height * self.width, 3), np.float32)
+        pix = self.record_pixels()
+        ok = pix >= 0
+        img[pix[ok]] = out[ok]
+        return img.reshape(self.height, self.width, 3)
 
     # ---- buffers ----------------------------------------------------------------
     def num_records(self):
