@@ -82,6 +82,7 @@ struct Ctx {
     int64_t slots_used = 0;
     /* photon buckets */
     DevBuf d_count, d_cell_start, d_scratch, d_pha, d_phb, d_phc;
+    struct { bool valid = false; int64_t n = 0; GridDesc grid{}; } fused; /* counts made by the last trace */
     GridDesc grid{};
     int map_kind = -1;
     int64_t map_slots = 0;
@@ -91,6 +92,9 @@ struct Ctx {
     /* misc */
     DevBuf d_out, d_counters;
     bool counting = false;
+    /* pm_reset_records is deferred: records read as (flux 0, N 0, r2 = rec_fresh_r2) */
+    bool rec_fresh = false;
+    float rec_fresh_r2 = 0.f;
     int64_t trace_per_block = TRACE_BLOCK; /* env PM_TRACE_PATHS_PER_BLOCK (tuning) */
     std::map<std::string, TimerPool> timers;
 };
@@ -261,6 +265,16 @@ GatherParams gather_params(Ctx *c, const pm_render_params *p) {
     return G;
 }
 
+/* applies a deferred pm_reset_records before a reader that is not a fused full gather */
+int materialize_reset(Ctx *c, hipStream_t s) {
+    if (!c->rec_fresh) return PM_OK;
+    timer_begin(c, "reset", s);
+    HIPCHK(c, launch_reset_records(recs(c), c->rec_fresh_r2, s));
+    timer_end(c, "reset", s);
+    c->rec_fresh = false;
+    return PM_OK;
+}
+
 int check_params(Ctx *c, const pm_render_params *p) {
     if (!p) FAIL(c, PM_ERR_INVALID, "null params");
     if (!c->committed) FAIL(c, PM_ERR_INVALID, "scene not committed (call pm_commit)");
@@ -311,7 +325,7 @@ int pm_create(void **out, const pm_config *cfg) {
         delete c;
         FAIL((Ctx *)nullptr, PM_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
     }
-    e = c->d_counters.ensure(8 * sizeof(unsigned long long)); /* [gather x4][trace x4] */
+    e = c->d_counters.ensure(16 * sizeof(unsigned long long)); /* [gather x4][trace x4][trace profile x8] */
     if (e != hipSuccess) {
         delete c;
         FAIL((Ctx *)nullptr, PM_ERR_HIP, "hipMalloc: %s", hipGetErrorString(e));
@@ -651,6 +665,7 @@ int pm_eye_pass(void *ptr, const pm_render_params *p, void *stream) {
     timer_begin(c, "eye", s);
     HIPCHK(c, launch_eye(E, s));
     timer_end(c, "eye", s);
+    c->rec_fresh = false; /* the eye pass writes every record */
     return PM_OK;
 }
 
@@ -680,6 +695,7 @@ int pm_set_slot_buffer(void *ptr, void *d, int64_t n) {
     GETCTX(ptr);
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->d_slots.release();
+    c->fused.valid = false;
     if (d) {
         if (n <= 0) FAIL(c, PM_ERR_INVALID, "external slot buffer needs n_slots > 0");
         c->d_slots.p = d;
@@ -689,6 +705,29 @@ int pm_set_slot_buffer(void *ptr, void *d, int64_t n) {
     c->slots_used = 0;
     return PM_OK;
 }
+
+/* photon-bucket grid of a render: cell edge >= 2 r_max over the scene box
+ * (PPM radii only shrink, so it holds for every pass of the render) */
+static GridDesc make_grid(const Ctx *c, const pm_render_params *p) {
+    GridDesc g{};
+    const float rq = sqrtf(p->initial_radius2) * 1.0001f + 1e-4f;
+    float cs = 2.0f * rq * 1.001f;
+    float ext[3];
+    for (int a = 0; a < 3; ++a) ext[a] = std::max(c->bbox_hi[a] - c->bbox_lo[a], 1e-3f);
+    int64_t dims[3];
+    while (true) {
+        for (int a = 0; a < 3; ++a) dims[a] = std::max<int64_t>(1, (int64_t)std::ceil(ext[a] / cs) + 1);
+        if (dims[0] * dims[1] * dims[2] <= (int64_t)1 << 26) break;
+        cs *= 1.25f;
+    }
+    g.gx = c->bbox_lo[0]; g.gy = c->bbox_lo[1]; g.gz = c->bbox_lo[2];
+    g.inv_cs = 1.0f / cs;
+    g.dx = (int)dims[0]; g.dy = (int)dims[1]; g.dz = (int)dims[2];
+    g.ncells = (uint32_t)(dims[0] * dims[1] * dims[2]);
+    return g;
+}
+
+static bool same_grid(const GridDesc &a, const GridDesc &b) { return std::memcmp(&a, &b, sizeof(GridDesc)) == 0; }
 
 int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t path_begin, int64_t path_count,
                      int64_t slot_path_base, void *stream) {
@@ -711,11 +750,29 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
     T.pass = pass; T.mpc = (int)mpc; T.max_spec = p->max_specular_depth; T.light_index = p->light_source_index;
     T.eps = p->scene_epsilon; T.seed = p->rng_seed;
     T.counters = c->d_counters.as<unsigned long long>() + 4;
+    T.prof = c->d_counters.as<unsigned long long>() + 8;
     if (c->counting) HIPCHK(c, hipMemsetAsync(T.counters, 0, 32, s));
+    /* A call that fills the slot buffer from slot 0 also runs the counting pass
+     * of the bucket build (keys, ranks, per-cell counts) at deposit time; the
+     * build then skips it (c->fused). Any other slot producer invalidates it. */
+    c->fused.valid = false;
+    const bool fuse = p->gather_structure == PM_GATHER_GRID && path_begin == slot_path_base;
+    if (fuse) {
+        const GridDesc g = make_grid(c, p);
+        HIPCHK(c, c->d_count.ensure(((size_t)g.ncells + 1) * 4));
+        HIPCHK(c, c->d_scratch.ensure(bucket_scratch_words(end_slot, g.ncells) * 4));
+        HIPCHK(c, hipMemsetAsync(c->d_count.p, 0, ((size_t)g.ncells + 1) * 4, s));
+        T.bucket = 1;
+        T.grid = g;
+        T.count = c->d_count.as<uint32_t>();
+        T.key = c->d_scratch.as<uint32_t>();
+        T.rank = c->d_scratch.as<uint32_t>() + end_slot;
+    }
     timer_begin(c, "trace", s);
     /* the kernel writes all path_count * mpc slots: deposits, then zeros */
     HIPCHK(c, launch_trace(T, c->counting, s));
     timer_end(c, "trace", s);
+    if (fuse) { c->fused.valid = true; c->fused.n = end_slot; c->fused.grid = T.grid; }
     c->slots_used = std::max(c->slots_used, end_slot);
     return PM_OK;
 }
@@ -748,29 +805,17 @@ int pm_build_photon_map(void *ptr, const pm_render_params *p, int64_t n_slots, v
     }
     /* photon buckets: cell size >= 2 r_max (PPM radii only shrink) */
     GridDesc &g = c->grid;
-    const float rq = sqrtf(p->initial_radius2) * 1.0001f + 1e-4f;
-    float cs = 2.0f * rq * 1.001f;
-    float ext[3];
-    for (int a = 0; a < 3; ++a) ext[a] = std::max(c->bbox_hi[a] - c->bbox_lo[a], 1e-3f);
-    int64_t dims[3];
-    while (true) {
-        for (int a = 0; a < 3; ++a) dims[a] = std::max<int64_t>(1, (int64_t)std::ceil(ext[a] / cs) + 1);
-        if (dims[0] * dims[1] * dims[2] <= (int64_t)1 << 26) break;
-        cs *= 1.25f;
-    }
-    g.gx = c->bbox_lo[0]; g.gy = c->bbox_lo[1]; g.gz = c->bbox_lo[2];
-    g.inv_cs = 1.0f / cs;
-    g.dx = (int)dims[0]; g.dy = (int)dims[1]; g.dz = (int)dims[2];
-    g.ncells = (uint32_t)(dims[0] * dims[1] * dims[2]);
+    g = make_grid(c, p);
+    const bool counted = c->fused.valid && c->fused.n == n_slots && same_grid(c->fused.grid, g);
     const size_t n = (size_t)n_slots;
     HIPCHK(c, c->d_count.ensure(((size_t)g.ncells + 1) * 4));
     HIPCHK(c, c->d_cell_start.ensure(((size_t)g.ncells + 1) * 4));
-    HIPCHK(c, c->d_scratch.ensure(bucket_scratch_words(n_slots, g.ncells) * 4));
+    if (!counted) HIPCHK(c, c->d_scratch.ensure(bucket_scratch_words(n_slots, g.ncells) * 4));
     HIPCHK(c, c->d_pha.ensure(n * 16)); HIPCHK(c, c->d_phb.ensure(n * 16)); HIPCHK(c, c->d_phc.ensure(n * 4));
     timer_begin(c, "build", s);
     HIPCHK(c, launch_bucket_build(c->d_slots.as<pm_photon>(), n_slots, g, c->d_count.as<uint32_t>(),
                                   c->d_cell_start.as<uint32_t>(), c->d_scratch.as<uint32_t>(), c->d_pha.as<float4>(),
-                                  c->d_phb.as<float4>(), c->d_phc.as<float>(), s));
+                                  c->d_phb.as<float4>(), c->d_phc.as<float>(), counted, s));
     timer_end(c, "build", s);
     c->map_kind = PM_GATHER_GRID;
     return PM_OK;
@@ -788,10 +833,16 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
     G.partial = partial;
     G.rec_begin = rec_begin;
     G.rec_end = rec_begin + rec_count;
+    /* a pending reset is consumed by a fused gather over all records (it starts
+     * from the initial PPM state and writes it); any other gather needs it applied */
+    const bool consume = c->rec_fresh && !partial && rec_begin == 0 && rec_count == c->nrec;
+    if (consume) { G.fresh = 1; G.r2init = c->rec_fresh_r2; }
+    else if ((rc = materialize_reset(c, s))) return rc;
     if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters.p, 0, 32, s));
     timer_begin(c, "gather", s);
     HIPCHK(c, launch_gather(G, p->gather_structure, partial != nullptr, c->counting, s));
     timer_end(c, "gather", s);
+    if (consume) c->rec_fresh = false;
     return PM_OK;
 }
 
@@ -819,6 +870,7 @@ int pm_ppm_update(void *ptr, const pm_render_params *p, const void *d_partial, i
     if (!d_partial || rec_begin < 0 || rec_count < 0 || rec_begin + rec_count > c->nrec)
         FAIL(c, PM_ERR_INVALID, "bad record range");
     hipStream_t s = pick(c, stream);
+    if ((rc = materialize_reset(c, s))) return rc;
     GatherParams G = gather_params(c, p);
     timer_begin(c, "update", s);
     HIPCHK(c, launch_ppm_update(G, (const long long *)d_partial, rec_begin, rec_count, s));
@@ -830,6 +882,8 @@ int pm_get_radius2(void *ptr, int64_t rec_begin, int64_t rec_count, void *d_out,
     GETCTX(ptr);
     if (!d_out || rec_begin < 0 || rec_count < 0 || rec_begin + rec_count > c->nrec)
         FAIL(c, PM_ERR_INVALID, "bad radius2 range");
+    int rc;
+    if ((rc = materialize_reset(c, pick(c, stream)))) return rc;
     HIPCHK(c, launch_radius2_io(recs(c), (float *)d_out, rec_begin, rec_count, 0, pick(c, stream)));
     return PM_OK;
 }
@@ -838,6 +892,8 @@ int pm_set_radius2(void *ptr, const void *d_in, int64_t rec_begin, int64_t rec_c
     GETCTX(ptr);
     if (!d_in || rec_begin < 0 || rec_count < 0 || rec_begin + rec_count > c->nrec)
         FAIL(c, PM_ERR_INVALID, "bad radius2 range");
+    int rc;
+    if ((rc = materialize_reset(c, pick(c, stream)))) return rc;
     HIPCHK(c, launch_radius2_io(recs(c), (float *)d_in, rec_begin, rec_count, 1, pick(c, stream)));
     return PM_OK;
 }
@@ -847,6 +903,8 @@ int pm_final(void *ptr, double emitted, int64_t rec_begin, int64_t rec_count, vo
     if (!d_out || rec_begin < 0 || rec_count < 0 || rec_begin + rec_count > c->nrec)
         FAIL(c, PM_ERR_INVALID, "bad final range");
     hipStream_t s = pick(c, stream);
+    int rc;
+    if ((rc = materialize_reset(c, s))) return rc;
     FinalParams F{};
     F.R = recs(c);
     F.emitted = (float)emitted; /* gContext["emittingPhotons"]->setFloat((float)totalPhotons) */
@@ -952,6 +1010,7 @@ int pm_upload_slots(void *ptr, const pm_photon *in, int64_t n) {
     int rc;
     if (!in || n < 0) FAIL(c, PM_ERR_INVALID, "bad slots");
     if ((rc = pm_reserve_slots(c, n, nullptr))) return rc;
+    c->fused.valid = false;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(c->d_slots.p, in, n * sizeof(pm_photon), hipMemcpyHostToDevice));
     c->slots_used = n;
@@ -961,7 +1020,9 @@ int pm_upload_slots(void *ptr, const pm_photon *in, int64_t n) {
 int pm_download_records(void *ptr, pm_record *out, int64_t n) {
     GETCTX(ptr);
     if (!out || n < 0 || n > c->nrec) FAIL(c, PM_ERR_INVALID, "bad record range");
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int rc;
+    if ((rc = materialize_reset(c, c->stream))) return rc;
+    HIPCHK(c, hipDeviceSynchronize());
     std::vector<float4> pos(n), nrm(n), st(n), dl(n);
     std::vector<float> N(n);
     HIPCHK(c, hipMemcpy(pos.data(), c->d_pos.p, n * 16, hipMemcpyDeviceToHost));
@@ -1000,6 +1061,7 @@ int pm_upload_records(void *ptr, const pm_record *in, int64_t n) {
     HIPCHK(c, hipMemcpy(c->d_state.p, st.data(), n * 16, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_dl.p, dl.data(), n * 16, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_n.p, N.data(), n * 4, hipMemcpyHostToDevice));
+    c->rec_fresh = false; /* every record overwritten */
     return PM_OK;
 }
 
@@ -1031,6 +1093,16 @@ int pm_trace_counters(void *ptr, int64_t out[4]) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(h, c->d_counters.as<unsigned long long>() + 4, 32, hipMemcpyDeviceToHost));
     for (int i = 0; i < 4; ++i) out[i] = (int64_t)h[i];
+    return PM_OK;
+}
+
+int pm_trace_profile(void *ptr, int64_t out[8], int reset) {
+    GETCTX(ptr);
+    unsigned long long h[8];
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemcpy(h, c->d_counters.as<unsigned long long>() + 8, 64, hipMemcpyDeviceToHost));
+    for (int i = 0; i < 8; ++i) out[i] = (int64_t)h[i];
+    if (reset) HIPCHK(c, hipMemset(c->d_counters.as<unsigned long long>() + 8, 0, 64));
     return PM_OK;
 }
 
@@ -1082,10 +1154,11 @@ int pm_reset_records(void *ptr, const pm_render_params *p, void *stream) {
     int rc;
     if ((rc = check_params(c, p))) return rc;
     if (c->nrec <= 0) FAIL(c, PM_ERR_INVALID, "no records (run pm_eye_pass first)");
-    hipStream_t s = pick(c, stream);
-    timer_begin(c, "reset", s);
-    HIPCHK(c, launch_reset_records(recs(c), p->initial_radius2, s));
-    timer_end(c, "reset", s);
+    (void)stream;
+    /* deferred: the next fused full gather starts from the initial state, any
+     * other reader applies it first (materialize_reset) */
+    c->rec_fresh = true;
+    c->rec_fresh_r2 = p->initial_radius2;
     return PM_OK;
 }
 

@@ -7,7 +7,10 @@
  * >= 2 r_max, photons stored cell-contiguously:
  *   1. k_bucket_count  cell key of each valid slot; rank = returning atomicAdd
  *                      on that cell's counter (atomics spread over ~10^5
- *                      cells; there is no single hot word)
+ *                      cells; there is no single hot word). Skipped when the
+ *                      trace kernel already counted its deposits (fused
+ *                      counting, pm_trace.hip: the atomics then overlap the
+ *                      latency-bound trace instead of costing a pass).
  *   2. exclusive scan  of the ncells+1 counters (reduce / top / down kernels,
  *                      16-B vector loads) -> cell_start; cell_start[ncells] =
  *                      number of valid photons
@@ -162,12 +165,14 @@ size_t bucket_scratch_words(int64_t n_slots, uint32_t ncells) {
 }
 
 hipError_t launch_bucket_build(const pm_photon *slots, int64_t n, GridDesc g, uint32_t *count, uint32_t *cell_start,
-                               uint32_t *scratch, float4 *ph_a, float4 *ph_b, float *ph_c, hipStream_t s) {
+                               uint32_t *scratch, float4 *ph_a, float4 *ph_b, float *ph_c, bool counted, hipStream_t s) {
     const int64_t nc = (int64_t)g.ncells + 1; /* last counter stays 0 -> cell_start[ncells] = total */
-    hipError_t e = hipMemsetAsync(count, 0, (size_t)nc * 4, s);
-    if (e != hipSuccess) return e;
     uint32_t *key = scratch, *rank = scratch + n, *sums = scratch + 2 * n;
-    if (n > 0)
+    if (!counted) {
+        hipError_t e = hipMemsetAsync(count, 0, (size_t)nc * 4, s);
+        if (e != hipSuccess) return e;
+    }
+    if (n > 0 && !counted)
         hipLaunchKernelGGL(k_bucket_count, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slots, n, g, count, key,
                            rank);
     const int ntile = (int)((nc + SCAN_TILE - 1) / SCAN_TILE);

@@ -310,40 +310,53 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
     best.ref = 0xffffffffu;
     const v3 inv = safe_inv(ray.d);
     int sp = 0;
-    int cur = 0;
-    /* every node is entered at most once per ray: a bound every lane reaches */
-    for (int guard = 0; guard <= S.n_nodes; ++guard) {
-        cen.node();
-        const float4 *nd = S.nodes + 4 * cur;
-        float4 a = nd[0], b = nd[1], c = nd[2];
-        int4 ch = *reinterpret_cast<const int4 *>(nd + 3);
-        float tl = box_near(a.x, a.y, a.z, a.w, b.x, b.y, ray.o, inv, ray.tmin, best.t);
-        float tr = box_near(b.z, b.w, c.x, c.y, c.z, c.w, ray.o, inv, ray.tmin, best.t);
-        bool hl = tl != __int_as_float(0x7f800000) && ch.z >= 0;
-        bool hr = tr != __int_as_float(0x7f800000) && ch.w >= 0;
-        if (hl && ch.x < 0) {
-            if (leaf_isect<ANY>(S, (uint32_t)~ch.x, (uint32_t)ch.z, ray, best, cen)) return true;
-            hl = false;
+    int cur = 0; /* next node to enter; -1: none left */
+    /* Leaves found while descending are postponed (at most the two children of
+     * one node) and tested in a separate loop, so a wave runs the primitive
+     * code once for all lanes that reached leaves instead of once per node
+     * iteration for a few of them (Aila & Laine's "while-while"). Culling is
+     * unchanged: a postponed leaf's box was hit within the current best t. */
+    uint32_t l0s = 0, l0n = 0, l1s = 0, l1n = 0; /* pending leaves: first ref, count (0 = none) */
+    int guard = 0; /* every node is entered at most once per ray: a bound every lane reaches */
+    while (true) {
+        while (cur >= 0 && l0n == 0 && guard <= S.n_nodes) {
+            ++guard;
+            cen.node();
+            const float4 *nd = S.nodes + 4 * cur;
+            float4 a = nd[0], b = nd[1], c = nd[2];
+            int4 ch = *reinterpret_cast<const int4 *>(nd + 3);
+            float tl = box_near(a.x, a.y, a.z, a.w, b.x, b.y, ray.o, inv, ray.tmin, best.t);
+            float tr = box_near(b.z, b.w, c.x, c.y, c.z, c.w, ray.o, inv, ray.tmin, best.t);
+            bool hl = tl != __int_as_float(0x7f800000) && ch.z >= 0;
+            bool hr = tr != __int_as_float(0x7f800000) && ch.w >= 0;
+            if (hl && ch.x < 0) { l0s = (uint32_t)~ch.x; l0n = (uint32_t)ch.z; hl = false; }
+            if (hr && ch.y < 0) {
+                if (l0n == 0) { l0s = (uint32_t)~ch.y; l0n = (uint32_t)ch.w; }
+                else { l1s = (uint32_t)~ch.y; l1n = (uint32_t)ch.w; }
+                hr = false;
+            }
+            if (hl && hr && sp < S.stack_depth) {
+                int nearc = ch.x, farc = ch.y;
+                if (tr < tl) { nearc = ch.y; farc = ch.x; }
+                stack[sp * stride] = farc;
+                ++sp;
+                cur = nearc;
+            } else if (hl) {
+                cur = ch.x;
+            } else if (hr) {
+                cur = ch.y;
+            } else if (sp > 0) {
+                --sp;
+                cur = stack[sp * stride];
+            } else {
+                cur = -1;
+            }
         }
-        if (hr && ch.y < 0) {
-            if (leaf_isect<ANY>(S, (uint32_t)~ch.y, (uint32_t)ch.w, ray, best, cen)) return true;
-            hr = false;
+        while (l0n != 0) {
+            if (leaf_isect<ANY>(S, l0s, l0n, ray, best, cen)) return true;
+            l0s = l1s; l0n = l1n; l1n = 0;
         }
-        if (hl && hr && sp < S.stack_depth) {
-            int nearc = ch.x, farc = ch.y;
-            if (tr < tl) { nearc = ch.y; farc = ch.x; }
-            stack[sp * stride] = farc;
-            ++sp;
-            cur = nearc;
-        } else if (hl) {
-            cur = ch.x;
-        } else if (hr) {
-            cur = ch.y;
-        } else {
-            if (sp == 0) break;
-            --sp;
-            cur = stack[sp * stride];
-        }
+        if (cur < 0 || guard > S.n_nodes) break;
     }
     return ANY ? false : best.ref != 0xffffffffu;
 }

@@ -56,7 +56,7 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_grid(GatherParams P) {
         if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) {
             if (PARTIAL) write_partial(P.partial + 4 * r, 0, Fx3{0, 0, 0});
         } else {
-            float4 st = P.R.state[r];
+            float4 st = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : P.R.state[r];
             float4 nrm = P.R.nrm[r];
             const float r2 = st.w;
             float4 m = P.materials[__float_as_int(nrm.w)];
@@ -68,28 +68,51 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_grid(GatherParams P) {
             if (r2 > 0.f) {
                 const GridDesc &g = P.grid;
                 const float rq = sqrtf(r2) * 1.0001f + 1e-4f;
+                /* cells overlapping [p - r', p + r']: cell edge >= 2 r_max, so at
+                 * most 2 per axis -> at most 4 (y, z) rows of <= 2 cells in x */
                 uint32_t x0 = cell_axis(p.x - rq, g.gx, g.inv_cs, g.dx), x1 = cell_axis(p.x + rq, g.gx, g.inv_cs, g.dx);
                 uint32_t y0 = cell_axis(p.y - rq, g.gy, g.inv_cs, g.dy), y1 = cell_axis(p.y + rq, g.gy, g.inv_cs, g.dy);
                 uint32_t z0 = cell_axis(p.z - rq, g.gz, g.inv_cs, g.dz), z1 = cell_axis(p.z + rq, g.gz, g.inv_cs, g.dz);
-                for (uint32_t cz = z0; cz <= z1; ++cz) {
-                    for (uint32_t cy = y0; cy <= y1; ++cy) {
-                        uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
-                        uint32_t b = P.cell_start[row + x0], e = P.cell_start[row + x1 + 1];
-                        if (COUNT) { vis += e - b; rows++; }
-                        for (uint32_t j = b; j < e; ++j) {
-                            float4 a = P.ph_a[j];
-                            v3 diff = p - xyz(a);
-                            float dist2 = diff.x * diff.x + diff.y * diff.y + diff.z * diff.z;
-                            if (dist2 < r2) {
-                                M++;
-                                float4 bb = P.ph_b[j];
-                                float wz = P.ph_c[j];
-                                v3 wi = mk(a.w, bb.w, wz);
-                                v3 c = fabsf(dot(ns, wi)) * fv * xyz(bb); /* processPhoton, gathering.cu:17-23 */
-                                Lf.x += to_fx(c.x, sc); Lf.y += to_fx(c.y, sc); Lf.z += to_fx(c.z, sc);
-                            }
-                        }
+                auto photon = [&](const float4 a, uint32_t j) {
+                    v3 diff = p - xyz(a);
+                    float dist2 = diff.x * diff.x + diff.y * diff.y + diff.z * diff.z;
+                    if (dist2 < r2) {
+                        M++;
+                        float4 bb = P.ph_b[j];
+                        float wz = P.ph_c[j];
+                        v3 wi = mk(a.w, bb.w, wz);
+                        v3 c = fabsf(dot(ns, wi)) * fv * xyz(bb); /* processPhoton, gathering.cu:17-23 */
+                        Lf.x += to_fx(c.x, sc); Lf.y += to_fx(c.y, sc); Lf.z += to_fx(c.z, sc);
                     }
+                };
+                auto range = [&](uint32_t j, const uint32_t e) {
+                    for (; j + 4 <= e; j += 4) { /* 4 photon loads in flight */
+                        const float4 a0 = P.ph_a[j], a1 = P.ph_a[j + 1], a2 = P.ph_a[j + 2], a3 = P.ph_a[j + 3];
+                        photon(a0, j); photon(a1, j + 1); photon(a2, j + 2); photon(a3, j + 3);
+                    }
+                    for (; j < e; ++j) photon(P.ph_a[j], j);
+                };
+                if (y1 <= y0 + 1 && z1 <= z0 + 1) {
+                    /* all row bounds first: 8 independent loads in flight */
+                    uint32_t rb[4], re[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t cy = y0 + (k & 1), cz = z0 + (k >> 1);
+                        const bool use = cy <= y1 && cz <= z1;
+                        const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+                        rb[k] = use ? P.cell_start[row + x0] : 0u;
+                        re[k] = use ? P.cell_start[row + x1 + 1] : 0u;
+                        if (COUNT) { vis += re[k] - rb[k]; rows += use; }
+                    }
+                    for (int k = 0; k < 4; ++k) range(rb[k], re[k]);
+                } else { /* radius above the grid's design radius (uploaded records) */
+                    for (uint32_t cz = z0; cz <= z1; ++cz)
+                        for (uint32_t cy = y0; cy <= y1; ++cy) {
+                            const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+                            const uint32_t b = P.cell_start[row + x0], e = P.cell_start[row + x1 + 1];
+                            if (COUNT) { vis += e - b; rows++; }
+                            range(b, e);
+                        }
                 }
             }
             if (COUNT) { hits += (unsigned long long)M; act++; }
@@ -98,9 +121,9 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_grid(GatherParams P) {
             } else {
                 const double inv = P.fx_inv;
                 v3 L = mk((float)((double)Lf.x * inv), (float)((double)Lf.y * inv), (float)((double)Lf.z * inv));
-                float N = P.R.n[r];
+                float N = P.fresh ? 0.f : P.R.n[r];
                 ppm_apply(st, N, M, L, P.ppm_alpha);
-                if (M > 0) { P.R.state[r] = st; P.R.n[r] = N; }
+                if (M > 0 || P.fresh) { P.R.state[r] = st; P.R.n[r] = N; }
             }
         }
     }
@@ -121,7 +144,7 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_kd(GatherParams P) {
         if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) {
             if (PARTIAL) write_partial(P.partial + 4 * r, 0, Fx3{0, 0, 0});
         } else {
-            float4 st = P.R.state[r];
+            float4 st = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : P.R.state[r];
             float4 nrm = P.R.nrm[r];
             const float maxDist2 = st.w;
             float4 m = P.materials[__float_as_int(nrm.w)];
@@ -172,9 +195,9 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_kd(GatherParams P) {
                 const float sc = P.fx_scale;
                 write_partial(P.partial + 4 * r, M, Fx3{to_fx(L.x, sc), to_fx(L.y, sc), to_fx(L.z, sc)});
             } else {
-                float N = P.R.n[r];
+                float N = P.fresh ? 0.f : P.R.n[r];
                 ppm_apply(st, N, M, L, P.ppm_alpha);
-                if (M > 0) { P.R.state[r] = st; P.R.n[r] = N; }
+                if (M > 0 || P.fresh) { P.R.state[r] = st; P.R.n[r] = N; }
             }
         }
     }

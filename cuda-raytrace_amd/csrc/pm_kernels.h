@@ -38,18 +38,6 @@ struct EyeParams {
     uint32_t light_seed;
 };
 
-struct TraceParams {
-    SceneDev S;
-    pm_photon *slots;
-    uint32_t perm[28];
-    int64_t path_begin, path_count, slot_path_base;
-    int64_t per_block; /* paths in each block's pool (>= 1; TRACE_BLOCK = no refills) */
-    int pass, mpc, max_spec, light_index;
-    float eps;
-    uint32_t seed;
-    unsigned long long *counters; /* census [rays, nodes, prim tests, deposits] */
-};
-
 struct GridDesc {
     float gx, gy, gz, inv_cs;
     int dx, dy, dz;
@@ -63,6 +51,24 @@ PMD uint32_t cell_axis(float v, float g0, float inv_cs, int dim) {
     c = c < 0 ? 0 : (c >= dim ? dim - 1 : c);
     return (uint32_t)c;
 }
+
+struct TraceParams {
+    SceneDev S;
+    pm_photon *slots;
+    uint32_t perm[28];
+    int64_t path_begin, path_count, slot_path_base;
+    int64_t per_block; /* paths in each block's pool (>= 1; TRACE_BLOCK = no refills) */
+    int pass, mpc, max_spec, light_index;
+    float eps;
+    uint32_t seed;
+    unsigned long long *counters; /* census [rays, nodes, prim tests, deposits] */
+    unsigned long long *prof;     /* phase cycles (PM_TRACE_PROFILE builds), 8 words */
+    /* fused bucket counting (bucket != 0): per slot cell key (0xffffffff =
+     * invalid) and rank = atomicAdd(count[key]) of the build's counting pass */
+    int bucket;
+    GridDesc grid;
+    uint32_t *count, *key, *rank;
+};
 
 struct GatherParams {
     RecordsDev R;
@@ -83,6 +89,10 @@ struct GatherParams {
     double fx_inv;
     /* partial mode: per record int64 (M, L.x, L.y, L.z) in fixed point */
     long long *partial;
+    /* fresh: records are in a deferred reset (pm_reset_records): read the
+     * initial PPM state (flux 0, N 0, r2init) instead of memory, write it back */
+    int fresh;
+    float r2init;
     unsigned long long *counters; /* [0] visited, [1] in radius */
 };
 
@@ -100,10 +110,11 @@ hipError_t launch_eye(const EyeParams &p, hipStream_t s);
 hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s);
 /* photon-bucket build (pm_bucket.hip): count + rank, scan, fill.
  * count and cell_start have ncells + 1 entries; cell_start[ncells] = valid
- * photons; scratch holds bucket_scratch_words() uint32 */
+ * photons; scratch holds bucket_scratch_words() uint32: key[n], rank[n], ...
+ * counted: key/rank/count were produced by the trace kernel (TraceParams::bucket) */
 size_t bucket_scratch_words(int64_t n_slots, uint32_t ncells);
 hipError_t launch_bucket_build(const pm_photon *slots, int64_t n, GridDesc g, uint32_t *count, uint32_t *cell_start,
-                               uint32_t *scratch, float4 *ph_a, float4 *ph_b, float *ph_c, hipStream_t s);
+                               uint32_t *scratch, float4 *ph_a, float4 *ph_b, float *ph_c, bool counted, hipStream_t s);
 /* gather: structure 0 grid, 1 kd; mode 0 fused PPM, 1 partial */
 hipError_t launch_gather(const GatherParams &p, int structure, int partial, int count, hipStream_t s);
 hipError_t launch_ppm_update(const GatherParams &p, const long long *partial, int64_t rec_begin, int64_t rec_count,

@@ -159,6 +159,31 @@ struct PathState {
     uint32_t stored; /* slots [0, stored) written */
 };
 
+/* Phase profile of k_trace (profiling builds only: make PROF=1 ->
+ * lib/libpmhip_prof.so): per-wave s_memtime cycles accumulated per phase,
+ * summed over waves into TraceParams::prof (pm_trace_profile). */
+struct TProf {
+#ifdef PM_TRACE_PROFILE
+    uint64_t last = 0, start = 0, acc[6] = {0, 0, 0, 0, 0, 0};
+    PMD void begin() { start = last = __builtin_amdgcn_s_memtime(); }
+    PMD void mark(int i) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        acc[i] += t - last;
+        last = t;
+    }
+    PMD void flush(unsigned long long *out) {
+        if (!out || (threadIdx.x & 63) != 0) return;
+        for (int i = 0; i < 6; ++i) atomicAdd(&out[i], (unsigned long long)acc[i]);
+        atomicAdd(&out[6], (unsigned long long)(last - start));
+        atomicAdd(&out[7], 1ull);
+    }
+#else
+    PMD void begin() {}
+    PMD void mark(int) {}
+    PMD void flush(unsigned long long *) {}
+#endif
+};
+
 /* emission: Halton light sample -> first ray (photontracing.cu:88-117) */
 PMD bool emit_path(const TraceParams &P, const SceneDev &S, const uint32_t *perm, uint32_t pid, PathState &st) {
     const uint32_t pm_index = pid * (uint32_t)P.mpc;
@@ -182,10 +207,12 @@ PMD bool emit_path(const TraceParams &P, const SceneDev &S, const uint32_t *perm
 /* one ray of a path: trace, then specular continuation or diffuse deposit +
  * Lambert bounce (photontracing.cu:119-183); false when the path ends */
 template <class C>
-PMD bool path_step(const TraceParams &P, const SceneDev &S, int *stack, PathState &st, C &cen) {
+PMD bool path_step(const TraceParams &P, const SceneDev &S, int *stack, PathState &st, C &cen, TProf &prof) {
     const uint32_t mpc = (uint32_t)P.mpc;
     Hit h;
-    if (!traverse<false>(S, st.ray, h, stack, TRACE_BLOCK, cen)) return false;
+    const bool hit = traverse<false>(S, st.ray, h, stack, TRACE_BLOCK, cen);
+    prof.mark(1);
+    if (!hit) return false;
     Geo g = shade(S, st.ray, h);
     v3 hit_point = st.ray.o + h.t * st.ray.d;
     float4 m = S.materials[g.material];
@@ -200,9 +227,18 @@ PMD bool path_step(const TraceParams &P, const SceneDev &S, int *stack, PathStat
     }
     v3 wo = -st.ray.d;
     if (st.nI >= 1) {
-        pm_photon *slots = P.slots + (size_t)(st.pid - (uint64_t)P.slot_path_base) * mpc;
-        store_photon(slots + (st.nI - 1), hit_point, st.alpha, wo);
+        const size_t slot = (size_t)(st.pid - (uint64_t)P.slot_path_base) * mpc + (st.nI - 1);
+        store_photon(P.slots + slot, hit_point, st.alpha, wo);
         st.stored = st.nI;
+        if (P.bucket) { /* fused counting pass of the bucket build (pm_bucket.hip k_bucket_count) */
+            const GridDesc &g = P.grid;
+            const uint32_t cx = cell_axis(hit_point.x, g.gx, g.inv_cs, g.dx);
+            const uint32_t cy = cell_axis(hit_point.y, g.gy, g.inv_cs, g.dy);
+            const uint32_t cz = cell_axis(hit_point.z, g.gz, g.inv_cs, g.dz);
+            const uint32_t key = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx + cx;
+            P.key[slot] = key;
+            P.rank[slot] = atomicAdd(&P.count[key], 1u);
+        }
     }
     if (st.nI >= mpc) return false;
     const uint32_t pm_index = st.pid * mpc;
@@ -228,6 +264,7 @@ PMD void finish_path(const TraceParams &P, const PathState &st) {
     for (uint32_t k = st.stored; k < mpc; ++k) {
         float2 *q = reinterpret_cast<float2 *>(slots + k);
         q[0] = z; q[1] = z; q[2] = z; q[3] = z; q[4] = z;
+        if (P.bucket) P.key[(size_t)(st.pid - (uint64_t)P.slot_path_base) * mpc + k] = 0xffffffffu;
     }
 }
 
@@ -283,6 +320,8 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceParams P) {
     int64_t next = pool_begin;
     int live = 0;
     PathState st;
+    TProf prof;
+    prof.begin();
     while (true) {
         const int64_t left = pool_end - next;
         const int n_new = (int)((int64_t)(TRACE_BLOCK - live) < left ? (int64_t)(TRACE_BLOCK - live) : left);
@@ -294,19 +333,22 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceParams P) {
             alive = emit_path(P, S, perm, (uint32_t)(P.path_begin + next + (tid - live)), st);
             if (!alive) finish_path(P, st);
         }
+        prof.mark(0);
         if (alive) {
             ++rays;
-            alive = path_step(P, S, stack, st, cen);
+            alive = path_step(P, S, stack, st, cen, prof);
             if (!alive) {
                 if (COUNT) deposits += st.stored;
                 finish_path(P, st);
             }
         }
         next += n_new;
+        prof.mark(2);
         /* compaction: rank = live paths before this thread in the block */
         const unsigned long long bal = __ballot(alive);
         if (lane == 0) wcount[wave] = (uint32_t)__popcll(bal);
         __syncthreads();
+        prof.mark(3);
         int base = 0, total = 0;
 #pragma unroll
         for (int w = 0; w < TRACE_BLOCK / 64; ++w) {
@@ -318,9 +360,11 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceParams P) {
         __syncthreads();
         live = total;
         if (tid < live) state_get(sstate, tid, st);
+        prof.mark(4);
         /* the next writes of wcount / sstate follow the next barrier, which
          * every thread reaches only after these reads */
     }
+    prof.flush(P.prof);
     if (COUNT) {
         uint32_t nodes = 0, prims = 0;
         if constexpr (COUNT != 0) { nodes = cen.nodes; prims = cen.prims; }

@@ -73,6 +73,7 @@ def load_library(path=None):
         "pm_download_kdtree": (c_int, [vp, vp, i64]),
         "pm_gather_counters": (c_int, [vp, ctypes.POINTER(i64)]),
         "pm_trace_counters": (c_int, [vp, ctypes.POINTER(i64)]),
+        "pm_trace_profile": (c_int, [vp, ctypes.POINTER(i64), c_int]),
         "pm_set_counting": (c_int, [vp, c_int]),
         "pm_synchronize": (c_int, [vp]),
         "pm_last_kernel_ms": (c_int, [vp, ctypes.c_char_p, ctypes.POINTER(c_double)]),
@@ -311,6 +312,13 @@ class Context:
         out = (ctypes.c_int64 * 4)()
         self._chk(self.lib.pm_trace_counters(self.h, out))
         return tuple(int(v) for v in out)
+
+    def trace_profile(self, reset=False):
+        """k_trace phase cycles (profiling builds, lib/libpmhip_prof.so): dict of summed cycles."""
+        out = (ctypes.c_int64 * 8)()
+        self._chk(self.lib.pm_trace_profile(self.h, out, int(bool(reset))))
+        keys = ("emit", "traverse", "shade", "compact_barrier", "exchange", "unused", "lifetime", "waves")
+        return dict(zip(keys, (int(v) for v in out)))
 
     def synchronize(self):
         self._chk(self.lib.pm_synchronize(self.h))

@@ -229,6 +229,13 @@ int pm_gather_counters(void *ctx, int64_t out[4]);
  * [1] BVH nodes entered, [2] primitive intersection tests, [3] photons
  * deposited (the traffic census behind the trace roofline) */
 int pm_trace_counters(void *ctx, int64_t out[4]);
+/* Phase profile of the trace kernel, summed over waves and launches since the
+ * last reset: shader-clock cycles in [0] emission, [1] BVH traversal,
+ * [2] shading + bounce + deposit, [3] compaction barrier, [4] state exchange,
+ * [5] unused, [6] wave lifetime, [7] waves. All zero unless the library was
+ * built with PROF=1 (lib/libpmhip_prof.so); a measurement hook, not used by
+ * the render path. */
+int pm_trace_profile(void *ctx, int64_t out[8], int reset);
 /* enable/disable census counters in the trace and gather kernels (off by
  * default: costs an atomic per wave) */
 int pm_set_counting(void *ctx, int enabled);

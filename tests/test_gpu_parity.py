@@ -89,6 +89,28 @@ def test_trace_census(cornell):
     assert nodes >= rays and prims >= deposits
 
 
+@pytest.mark.parametrize("structure", [PM_GATHER_GRID, PM_GATHER_KDTREE])
+def test_deferred_reset(cornell, structure):
+    """pm_reset_records is deferred: a fused full gather consumes it (same
+    records as a gather right after the eye pass); any other reader sees the
+    reset applied first."""
+    ctx, _ = cornell
+    p = RenderParams.defaults(paths_per_pass=16384, initial_radius2=25.0, gather_structure=structure)
+    ctx.eye_pass(p)
+    eye = ctx.download_records()
+    ctx.trace_photons(p, 0, 0, 16384)
+    ctx.build_photon_map(p, 16384 * 4)
+    ctx.gather(p)
+    first = ctx.download_records()
+    assert (first["photon_count"] > 0).sum() > 100
+    for _ in range(2):
+        ctx.reset_records(p)
+        ctx.gather(p)
+        assert_bitexact(ctx.download_records(), first, "gather after deferred reset")
+    ctx.reset_records(p)
+    assert_bitexact(ctx.download_records(), eye, "reset records read back")
+
+
 def _gather_inputs(orc, paths=16384, radius2=25.0):
     p = RenderParams.defaults(paths_per_pass=paths, initial_radius2=radius2)
     recs = orc.eye_pass(p)
