@@ -95,7 +95,9 @@ struct Ctx {
     /* pm_reset_records is deferred: records read as (flux 0, N 0, r2 = rec_fresh_r2) */
     bool rec_fresh = false;
     float rec_fresh_r2 = 0.f;
-    int64_t trace_per_block = TRACE_BLOCK; /* env PM_TRACE_PATHS_PER_BLOCK (tuning) */
+    int64_t trace_per_block = 0; /* 0: per-lane paths (default); >0: block-compacting pool (env PM_TRACE_PATHS_PER_BLOCK) */
+    int64_t trace_wave_paths = 64; /* per-lane kernel: paths per wave (env PM_TRACE_WAVE_PATHS) */
+    int trace_refill_min = 32;     /* per-lane kernel: idle lanes that trigger a refill (env PM_TRACE_REFILL_MIN) */
     std::map<std::string, TimerPool> timers;
 };
 
@@ -318,7 +320,9 @@ int pm_create(void **out, const pm_config *cfg) {
     if (dev < 0 || dev >= ndev) FAIL((Ctx *)nullptr, PM_ERR_INVALID, "device %d out of range (%d devices)", dev, ndev);
     Ctx *c = new Ctx();
     c->device = dev;
-    if (const char *e = getenv("PM_TRACE_PATHS_PER_BLOCK")) c->trace_per_block = std::max(1LL, atoll(e));
+    if (const char *e = getenv("PM_TRACE_PATHS_PER_BLOCK")) c->trace_per_block = std::max(0LL, atoll(e));
+    if (const char *e = getenv("PM_TRACE_WAVE_PATHS")) c->trace_wave_paths = std::max(64LL, atoll(e));
+    if (const char *e = getenv("PM_TRACE_REFILL_MIN")) c->trace_refill_min = std::max(1, std::min(64, atoi(e)));
     (void)hipSetDevice(dev);
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -747,6 +751,8 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
     halton_perm((uint32_t)pass, T.perm);
     T.path_begin = path_begin; T.path_count = path_count; T.slot_path_base = slot_path_base;
     T.per_block = c->trace_per_block;
+    T.wave_paths = c->trace_wave_paths;
+    T.refill_min = c->trace_refill_min;
     T.pass = pass; T.mpc = (int)mpc; T.max_spec = p->max_specular_depth; T.light_index = p->light_source_index;
     T.eps = p->scene_epsilon; T.seed = p->rng_seed;
     T.counters = c->d_counters.as<unsigned long long>() + 4;

@@ -104,13 +104,18 @@ PMD void concentric_sample_disk(float u1, float u2, float *dx, float *dy) {
     float sx = 2 * u1 - 1;
     float sy = 2 * u2 - 1;
     if (sx == 0.0f && sy == 0.0f) { *dx = 0.0f; *dy = 0.0f; return; }
+    /* the reference's four branches each divide; here the branch only selects
+     * (r, numerator, offset) and one IEEE division follows. Bit-identical:
+     * c - a/r == c + (-a)/r, and 0 + q == q for the q > 0 of that case. */
+    float num, base;
     if (sx >= -sy) {
-        if (sx > sy) { r = sx; theta = (sy > 0.0f) ? sy / r : 8.0f + sy / r; }
-        else { r = sy; theta = 2.0f - sx / r; }
+        if (sx > sy) { r = sx; num = sy; base = (sy > 0.0f) ? 0.0f : 8.0f; }
+        else { r = sy; num = -sx; base = 2.0f; }
     } else {
-        if (sx <= sy) { r = -sx; theta = 4.0f - sy / r; }
-        else { r = -sy; theta = 6.0f + sx / r; }
+        if (sx <= sy) { r = -sx; num = -sy; base = 4.0f; }
+        else { r = -sy; num = sx; base = 6.0f; }
     }
+    theta = base + num / r;
     theta = (float)((double)theta * (M_PI / 4.f));
     float st, ct;
     pmdm_sincosf(theta, &st, &ct);
@@ -139,6 +144,37 @@ PMD float permuted_radical_inverse(uint32_t n, uint32_t base, const uint32_t *p)
         invBi *= invBase;
     }
     return val;
+}
+
+/* The four dimensions (bases 2, 3, 5, 7; table offsets 0, 2, 5, 10) of
+ * photontracing.cu:33-43 as four interleaved chains of one loop, so their
+ * independent digit steps overlap instead of running as four serial loops.
+ * Each chain is exactly permuted_radical_inverse; base 2 has the most digits
+ * (every chain's n stays <= base 2's), so it bounds the loop. */
+PMD void permuted_halton4(uint32_t n, const uint32_t *p, float out[4]) {
+    const uint32_t base[4] = {2u, 3u, 5u, 7u}, off[4] = {0u, 2u, 5u, 10u};
+    float val[4], invBase[4], invBi[4];
+    uint32_t m[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        val[k] = 0.f;
+        invBase[k] = 1.f / base[k];
+        invBi[k] = invBase[k];
+        m[k] = n;
+    }
+    while ((m[0] | m[1] | m[2] | m[3]) != 0u) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (m[k] > 0) {
+                const uint32_t d_i = p[off[k] + m[k] % base[k]];
+                val[k] += d_i * invBi[k];
+                m[k] = (uint32_t)((float)m[k] * invBase[k]); /* reference quirk: n *= invBase */
+                invBi[k] *= invBase[k];
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) out[k] = val[k];
 }
 
 /* ------------------------------------------------------------ intersect */
@@ -216,11 +252,15 @@ PMD bool isect_sphere(const float4 *s, const Ray &ray, float *thit) {
 
 /* ---------------------------------------------------------- traversal */
 /* Slab test of one child box; returns tnear (inf = miss). */
-PMD float box_near(float lx, float ly, float lz, float hx, float hy, float hz, v3 o, v3 inv, float tmin,
+/* t = (plane - o) / d as one FMA, plane * inv - o * inv (oinv precomputed per
+ * ray). The slab test only culls: its error is about one ulp of the
+ * coordinates, and every primitive box is padded by 1e-4 of its coordinate
+ * magnitude at commit (thousands of ulps), so no box holding a hit is culled. */
+PMD float box_near(float lx, float ly, float lz, float hx, float hy, float hz, v3 oinv, v3 inv, float tmin,
                    float tmax) {
-    float t0x = (lx - o.x) * inv.x, t1x = (hx - o.x) * inv.x;
-    float t0y = (ly - o.y) * inv.y, t1y = (hy - o.y) * inv.y;
-    float t0z = (lz - o.z) * inv.z, t1z = (hz - o.z) * inv.z;
+    float t0x = __builtin_fmaf(lx, inv.x, -oinv.x), t1x = __builtin_fmaf(hx, inv.x, -oinv.x);
+    float t0y = __builtin_fmaf(ly, inv.y, -oinv.y), t1y = __builtin_fmaf(hy, inv.y, -oinv.y);
+    float t0z = __builtin_fmaf(lz, inv.z, -oinv.z), t1z = __builtin_fmaf(hz, inv.z, -oinv.z);
     float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
     float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), tmax));
     return tn <= tf ? tn : __int_as_float(0x7f800000);
@@ -309,6 +349,7 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
     best.gid = 0xffffffffu;
     best.ref = 0xffffffffu;
     const v3 inv = safe_inv(ray.d);
+    const v3 oinv = mk(ray.o.x * inv.x, ray.o.y * inv.y, ray.o.z * inv.z);
     int sp = 0;
     int cur = 0; /* next node to enter; -1: none left */
     /* Leaves found while descending are postponed (at most the two children of
@@ -325,8 +366,8 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
             const float4 *nd = S.nodes + 4 * cur;
             float4 a = nd[0], b = nd[1], c = nd[2];
             int4 ch = *reinterpret_cast<const int4 *>(nd + 3);
-            float tl = box_near(a.x, a.y, a.z, a.w, b.x, b.y, ray.o, inv, ray.tmin, best.t);
-            float tr = box_near(b.z, b.w, c.x, c.y, c.z, c.w, ray.o, inv, ray.tmin, best.t);
+            float tl = box_near(a.x, a.y, a.z, a.w, b.x, b.y, oinv, inv, ray.tmin, best.t);
+            float tr = box_near(b.z, b.w, c.x, c.y, c.z, c.w, oinv, inv, ray.tmin, best.t);
             bool hl = tl != __int_as_float(0x7f800000) && ch.z >= 0;
             bool hr = tr != __int_as_float(0x7f800000) && ch.w >= 0;
             if (hl && ch.x < 0) { l0s = (uint32_t)~ch.x; l0n = (uint32_t)ch.z; hl = false; }

@@ -57,7 +57,9 @@ struct TraceParams {
     pm_photon *slots;
     uint32_t perm[28];
     int64_t path_begin, path_count, slot_path_base;
-    int64_t per_block; /* paths in each block's pool (>= 1; TRACE_BLOCK = no refills) */
+    int64_t per_block;  /* > 0: block-compacting kernel, paths per block pool; 0: per-lane kernel */
+    int64_t wave_paths; /* per-lane kernel: paths per wave pool (>= 64; 64 = no refills) */
+    int refill_min;     /* per-lane kernel: refill when at least this many lanes are idle */
     int pass, mpc, max_spec, light_index;
     float eps;
     uint32_t seed;

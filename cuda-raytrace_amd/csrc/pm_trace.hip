@@ -188,12 +188,7 @@ struct TProf {
 PMD bool emit_path(const TraceParams &P, const SceneDev &S, const uint32_t *perm, uint32_t pid, PathState &st) {
     const uint32_t pm_index = pid * (uint32_t)P.mpc;
     float smp[4];
-    {
-        const uint32_t b[4] = {2, 3, 5, 7};
-        const uint32_t off[4] = {0, 2, 5, 10};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) smp[k] = permuted_radical_inverse(pm_index, b[k], perm + off[k]);
-    }
+    permuted_halton4(pm_index, perm, smp);
     const LightDev Lt = S.lights[P.light_index];
     v3 N1; float pdf;
     v3 Le = sample_le(Lt, smp[0], smp[1], smp[2], smp[3], P.eps, &st.ray, &N1, &pdf);
@@ -372,9 +367,78 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceParams P) {
     }
 }
 
+/* Per-lane variant (per_block == 0): no block barriers. Each wave owns
+ * wave_paths consecutive paths; every lane runs one path at a time, and when
+ * at least refill_min lanes (or all) have finished, the wave hands them the
+ * next paths of its pool (ballot + popcount ranks). With wave_paths == 64
+ * every lane runs exactly one path and a wave lives as long as its longest. */
+template <int COUNT, bool LDS>
+__global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
+    extern __shared__ __attribute__((aligned(16))) int stk[];
+    __shared__ uint32_t perm[28];
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (tid < 28) perm[tid] = P.perm[tid];
+    const SceneDev S = scene_view<LDS>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * TRACE_BLOCK), tid,
+                                       TRACE_BLOCK);
+    __syncthreads();
+    int *stack = stk + tid;
+    typename std::conditional<COUNT != 0, Census, NoCensus>::type cen;
+    TProf prof;
+    uint32_t rays = 0, deposits = 0;
+    const int64_t wave_id = ((int64_t)blockIdx.x * TRACE_BLOCK + tid) >> 6;
+    const int64_t wbegin = wave_id * P.wave_paths;
+    const int64_t wend = wbegin + P.wave_paths < P.path_count ? wbegin + P.wave_paths : P.path_count;
+    int64_t cursor = wbegin; /* wave-uniform: next unassigned path of the pool */
+    PathState st;
+    bool alive = false;
+    while (true) {
+        const unsigned long long idle = __ballot(!alive);
+        const int nidle = __popcll(idle);
+        if (cursor < wend && (nidle >= P.refill_min || nidle == 64)) {
+            const int64_t mine = cursor + __popcll(idle & ((1ull << lane) - 1ull));
+            if (!alive && mine < wend) {
+                alive = emit_path(P, S, perm, (uint32_t)(P.path_begin + mine), st);
+                if (!alive) finish_path(P, st);
+            }
+            cursor = cursor + nidle < wend ? cursor + nidle : wend;
+        }
+        if (!__ballot(alive)) {
+            if (cursor >= wend) break;
+            continue;
+        }
+        if (alive) {
+            ++rays;
+            alive = path_step(P, S, stack, st, cen, prof);
+            if (!alive) {
+                if (COUNT) deposits += st.stored;
+                finish_path(P, st);
+            }
+        }
+    }
+    if (COUNT) {
+        uint32_t nodes = 0, prims = 0;
+        if constexpr (COUNT != 0) { nodes = cen.nodes; prims = cen.prims; }
+        count4(P.counters, rays, nodes, prims, deposits);
+    }
+}
+
 hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s) {
     if (p.path_count <= 0) return hipSuccess;
-    if (p.per_block <= 0) return hipErrorInvalidValue;
+    if (p.per_block == 0) {
+        if (p.wave_paths < 64 || p.refill_min < 1) return hipErrorInvalidValue;
+        const int64_t waves = (p.path_count + p.wave_paths - 1) / p.wave_paths;
+        const unsigned grid = (unsigned)((waves + TRACE_BLOCK / 64 - 1) / (TRACE_BLOCK / 64));
+        const size_t lds = (size_t)p.S.stack_depth * TRACE_BLOCK * 4 + p.S.lds_bytes;
+        if (p.S.lds_bytes) {
+            if (count) hipLaunchKernelGGL((k_trace_lane<1, true>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
+            else hipLaunchKernelGGL((k_trace_lane<0, true>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
+        } else {
+            if (count) hipLaunchKernelGGL((k_trace_lane<1, false>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
+            else hipLaunchKernelGGL((k_trace_lane<0, false>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
+        }
+        return hipGetLastError();
+    }
+    if (p.per_block < 0) return hipErrorInvalidValue;
     unsigned grid = (unsigned)((p.path_count + p.per_block - 1) / p.per_block);
     const size_t lds = (size_t)p.S.stack_depth * TRACE_BLOCK * 4 + p.S.lds_bytes;
     if (p.S.lds_bytes) {
