@@ -631,6 +631,14 @@ int pm_commit(void *ptr) {
     S.spheres = (const float4 *)(base + o_spheres); S.materials = (const float4 *)(base + o_mats);
     S.lights = (const LightDev *)(base + o_lights);
     S.n_lights = (int)c->lights.size(); S.n_nodes = (int)nodes4.size() / 4;
+    S.n_refs = (int)bvh.refs.size();
+    S.n_tris = (int)tri_info.size(); S.n_disks = (int)nd; S.n_spheres = (int)ns;
+    {
+        /* tiny LDS scenes skip the BVH (MODE_BRUTE); env PM_TRACE_BRUTE_MAX overrides the limit (0 = never) */
+        const char *e = getenv("PM_TRACE_BRUTE_MAX");
+        const int brute_max = e ? atoi(e) : BRUTE_MAX_PRIMS;
+        S.brute = (S.lds_bytes > 0 && S.n_refs <= brute_max) ? 1 : 0;
+    }
     /* a push happens only when descending a level, so depth + 1 entries suffice;
      * sizing the LDS stack by the actual tree keeps occupancy VGPR-bound */
     S.stack_depth = std::min(BVH_STACK, std::max(2, c->bvh_depth + 2));

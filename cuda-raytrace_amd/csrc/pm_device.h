@@ -75,6 +75,9 @@ struct SceneDev {
     int n_lights;
     int n_nodes;
     int stack_depth; /* LDS stack entries per lane (>= BVH depth, <= BVH_STACK_DEPTH) */
+    int n_refs;      /* primitives (leaf refs) */
+    int n_tris, n_disks, n_spheres;
+    int brute;       /* 1: test every primitive wave-uniformly instead of the BVH (tiny LDS scenes) */
     /* all arrays above are 16-B aligned sections of one blob in HBM */
     const char *blob;
     uint32_t blob_bytes;
@@ -84,6 +87,12 @@ struct SceneDev {
 /* Scenes up to this size are copied into each block's LDS and traversed from
  * there (Cornell C2: ~4 KB); larger ones are traversed from HBM/L2. */
 constexpr uint32_t LDS_SCENE_MAX = 16384;
+/* LDS scenes with at most this many primitives skip the BVH: every lane
+ * tests every primitive (MODE_BRUTE) */
+constexpr int BRUTE_MAX_PRIMS = 64;
+
+/* how the kernels see the scene (template argument of the traversal kernels) */
+enum SceneMode : int { MODE_GLOBAL = 0, MODE_LDS = 1, MODE_BRUTE = 2 };
 
 struct Ray { v3 o, d; float tmin, tmax; };
 
@@ -306,6 +315,41 @@ PMD SceneDev scene_view(const SceneDev &S, uint4 *lds, int tid, int nthreads) {
     return V;
 }
 
+/* closest hit so far: smaller t wins, equal t -> lowest global primitive id
+ * (callers pass only t <= best.t), so the result is independent of the order
+ * primitives are tested in (BVH or brute force) */
+PMD void consider(Hit &best, float t, float b, float g, uint32_t ref, uint32_t gid) {
+    if (t < best.t || gid < best.gid) { best.t = t; best.beta = b; best.gamma = g; best.ref = ref; best.gid = gid; }
+}
+
+/* MODE_BRUTE: every primitive, wave-uniform loop (same primitive in every
+ * lane: broadcast LDS reads, no divergence, no stack) */
+template <bool ANY, class C>
+PMD bool brute_isect(const SceneDev &S, const Ray &ray, Hit &best, C &cen) {
+    for (int k = 0; k < S.n_tris; ++k) {
+        cen.prim();
+        float t, b, g;
+        const bool ok = isect_tri(S.tri_geo + 3 * k, ray, &t, &b, &g);
+        if (ANY) { if (ok) return true; continue; }
+        if (ok && t <= best.t) consider(best, t, b, g, (PRIM_TRI << 30) | (uint32_t)k, S.tri_id[k]);
+    }
+    for (int k = 0; k < S.n_disks; ++k) {
+        cen.prim();
+        float t;
+        const bool ok = isect_disk(S.disks + 5 * k, ray, &t);
+        if (ANY) { if (ok) return true; continue; }
+        if (ok && t <= best.t) consider(best, t, 0.f, 0.f, (PRIM_DISK << 30) | (uint32_t)k, (uint32_t)fbits(S.disks[5 * k + 4].w));
+    }
+    for (int k = 0; k < S.n_spheres; ++k) {
+        cen.prim();
+        float t;
+        const bool ok = isect_sphere(S.spheres + 4 * k, ray, &t);
+        if (ANY) { if (ok) return true; continue; }
+        if (ok && t <= best.t) consider(best, t, 0.f, 0.f, (PRIM_SPHERE << 30) | (uint32_t)k, (uint32_t)fbits(S.spheres[4 * k + 3].w));
+    }
+    return false;
+}
+
 /* Tests the primitives of one leaf; for ANY=true returns at the first hit. */
 template <bool ANY, class C>
 PMD bool leaf_isect(const SceneDev &S, uint32_t start, uint32_t count, const Ray &ray, Hit &best, C &cen) {
@@ -343,7 +387,7 @@ PMD bool leaf_isect(const SceneDev &S, uint32_t start, uint32_t count, const Ray
  * Closest hit (ANY=false) or occlusion (ANY=true). Node = 4 float4:
  * (l.lo, l.hi.x) (l.hi.yz, r.lo.xy) (r.lo.z, r.hi) (left, right, lcount, rcount);
  * child >= 0 internal node, child < 0 leaf with refs start ~child. */
-template <bool ANY, class C>
+template <bool ANY, int MODE, class C>
 PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int stride, C &cen) {
     best.t = ray.tmax;
     best.gid = 0xffffffffu;
@@ -357,6 +401,11 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
      * code once for all lanes that reached leaves instead of once per node
      * iteration for a few of them (Aila & Laine's "while-while"). Culling is
      * unchanged: a postponed leaf's box was hit within the current best t. */
+    if constexpr (MODE == MODE_BRUTE) {
+        cen.node();
+        if (brute_isect<ANY>(S, ray, best, cen)) return true;
+        return ANY ? false : best.ref != 0xffffffffu;
+    }
     uint32_t l0s = 0, l0n = 0, l1s = 0, l1n = 0; /* pending leaves: first ref, count (0 = none) */
     int guard = 0; /* every node is entered at most once per ray: a bound every lane reaches */
     while (true) {
@@ -401,10 +450,10 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
     }
     return ANY ? false : best.ref != 0xffffffffu;
 }
-template <bool ANY>
+template <bool ANY, int MODE>
 PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int stride) {
     NoCensus none;
-    return traverse<ANY>(S, ray, best, stack, stride, none);
+    return traverse<ANY, MODE>(S, ray, best, stack, stride, none);
 }
 
 /* ------------------------------------------------------------- shading */

@@ -107,6 +107,9 @@ struct FinalParams {
     int W;
 };
 
+/* traversal mode of a scene: LDS-resident blob (brute force when tiny) or HBM */
+inline int scene_mode(const SceneDev &S) { return S.lds_bytes ? (S.brute ? MODE_BRUTE : MODE_LDS) : MODE_GLOBAL; }
+
 hipError_t launch_eye(const EyeParams &p, hipStream_t s);
 /* writes every slot of its paths (deposits, then zeros); count: census */
 hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s);

@@ -20,13 +20,13 @@ namespace pm {
 /* ====================================================================== */
 /* eye pass                                                               */
 /* ====================================================================== */
-template <bool LDS>
+template <int MODE>
 __global__ __launch_bounds__(EYE_BLOCK) void k_eye(EyeParams P) {
     extern __shared__ __attribute__((aligned(16))) int stk[]; /* [stack_depth x EYE_BLOCK][scene blob (LDS)] */
     int *stack = stk + threadIdx.x;
-    const SceneDev S = scene_view<LDS>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * EYE_BLOCK),
-                                       threadIdx.x, EYE_BLOCK);
-    if (LDS) __syncthreads();
+    const SceneDev S = scene_view<MODE != MODE_GLOBAL>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * EYE_BLOCK),
+                                                       threadIdx.x, EYE_BLOCK);
+    if (MODE != MODE_GLOBAL) __syncthreads();
     const int64_t r = (int64_t)blockIdx.x * EYE_BLOCK + threadIdx.x;
     if (r >= P.R.count) return;
 
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(EYE_BLOCK) void k_eye(EyeParams P) {
     Geo g;
     uint32_t flags = 0;
     while (true) {
-        if (!traverse<false>(S, ray, h, stack, EYE_BLOCK)) { flags = PM_REC_MISS; break; }
+        if (!traverse<false, MODE>(S, ray, h, stack, EYE_BLOCK)) { flags = PM_REC_MISS; break; }
         g = shade(S, ray, h);
         const v3 point = ray.o + ray.d * h.t;
         int mtype = fbits(S.materials[g.material].w);
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(EYE_BLOCK) void k_eye(EyeParams P) {
                 Ray sr;
                 sr.o = point; sr.d = uwi; sr.tmin = 0.001f; sr.tmax = 1.0f - 0.001f;
                 Hit sh;
-                float atten = traverse<true>(S, sr, sh, stack, EYE_BLOCK) ? 0.0f : 1.0f;
+                float atten = traverse<true, MODE>(S, sr, sh, stack, EYE_BLOCK) ? 0.0f : 1.0f;
                 v3 wi = normalize(uwi);
                 L = L + (atten * fabsf(dot(ns, wi))) * fv * li / (pdf * nS);
             }
@@ -129,8 +129,11 @@ hipError_t launch_eye(const EyeParams &p, hipStream_t s) {
     if (p.R.count <= 0) return hipSuccess;
     unsigned grid = (unsigned)((p.R.count + EYE_BLOCK - 1) / EYE_BLOCK);
     const size_t lds = (size_t)p.S.stack_depth * EYE_BLOCK * 4 + p.S.lds_bytes;
-    if (p.S.lds_bytes) hipLaunchKernelGGL(k_eye<true>, dim3(grid), dim3(EYE_BLOCK), lds, s, p);
-    else hipLaunchKernelGGL(k_eye<false>, dim3(grid), dim3(EYE_BLOCK), lds, s, p);
+    switch (scene_mode(p.S)) {
+    case MODE_BRUTE: hipLaunchKernelGGL(k_eye<MODE_BRUTE>, dim3(grid), dim3(EYE_BLOCK), lds, s, p); break;
+    case MODE_LDS: hipLaunchKernelGGL(k_eye<MODE_LDS>, dim3(grid), dim3(EYE_BLOCK), lds, s, p); break;
+    default: hipLaunchKernelGGL(k_eye<MODE_GLOBAL>, dim3(grid), dim3(EYE_BLOCK), lds, s, p); break;
+    }
     return hipGetLastError();
 }
 
@@ -159,7 +162,7 @@ struct PathState {
     uint32_t stored; /* slots [0, stored) written */
 };
 
-/* Phase profile of k_trace (profiling builds only: make PROF=1 ->
+/* Phase profile of k_trace (profiling builds only: `make prof` ->
  * lib/libpmhip_prof.so): per-wave s_memtime cycles accumulated per phase,
  * summed over waves into TraceParams::prof (pm_trace_profile). */
 struct TProf {
@@ -201,11 +204,11 @@ PMD bool emit_path(const TraceParams &P, const SceneDev &S, const uint32_t *perm
 
 /* one ray of a path: trace, then specular continuation or diffuse deposit +
  * Lambert bounce (photontracing.cu:119-183); false when the path ends */
-template <class C>
+template <int MODE, class C>
 PMD bool path_step(const TraceParams &P, const SceneDev &S, int *stack, PathState &st, C &cen, TProf &prof) {
     const uint32_t mpc = (uint32_t)P.mpc;
     Hit h;
-    const bool hit = traverse<false>(S, st.ray, h, stack, TRACE_BLOCK, cen);
+    const bool hit = traverse<false, MODE>(S, st.ray, h, stack, TRACE_BLOCK, cen);
     prof.mark(1);
     if (!hit) return false;
     Geo g = shade(S, st.ray, h);
@@ -295,7 +298,7 @@ PMD void state_get(uint32_t (*lds)[TRACE_BLOCK], int slot, PathState &st) {
  * Results are identical to one-thread-per-path (path math unchanged).
  * COUNT: census [rays traced, BVH nodes entered, primitive tests, photons
  * deposited], one atomic per wave (counting launches only, never timed). */
-template <int COUNT, bool LDS>
+template <int COUNT, int MODE>
 __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceParams P) {
     extern __shared__ __attribute__((aligned(16))) int stk[]; /* [stack_depth x TRACE_BLOCK][scene blob (LDS)] */
     __shared__ uint32_t perm[28];
@@ -303,8 +306,8 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceParams P) {
     __shared__ uint32_t wcount[TRACE_BLOCK / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < 28) perm[tid] = P.perm[tid];
-    const SceneDev S = scene_view<LDS>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * TRACE_BLOCK), tid,
-                                       TRACE_BLOCK);
+    const SceneDev S = scene_view<MODE != MODE_GLOBAL>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * TRACE_BLOCK),
+                                                       tid, TRACE_BLOCK);
     __syncthreads();
     int *stack = stk + tid;
     typename std::conditional<COUNT != 0, Census, NoCensus>::type cen;
@@ -331,7 +334,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceParams P) {
         prof.mark(0);
         if (alive) {
             ++rays;
-            alive = path_step(P, S, stack, st, cen, prof);
+            alive = path_step<MODE>(P, S, stack, st, cen, prof);
             if (!alive) {
                 if (COUNT) deposits += st.stored;
                 finish_path(P, st);
@@ -372,14 +375,14 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceParams P) {
  * at least refill_min lanes (or all) have finished, the wave hands them the
  * next paths of its pool (ballot + popcount ranks). With wave_paths == 64
  * every lane runs exactly one path and a wave lives as long as its longest. */
-template <int COUNT, bool LDS>
+template <int COUNT, int MODE>
 __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
     extern __shared__ __attribute__((aligned(16))) int stk[];
     __shared__ uint32_t perm[28];
     const int tid = threadIdx.x, lane = tid & 63;
     if (tid < 28) perm[tid] = P.perm[tid];
-    const SceneDev S = scene_view<LDS>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * TRACE_BLOCK), tid,
-                                       TRACE_BLOCK);
+    const SceneDev S = scene_view<MODE != MODE_GLOBAL>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * TRACE_BLOCK),
+                                                       tid, TRACE_BLOCK);
     __syncthreads();
     int *stack = stk + tid;
     typename std::conditional<COUNT != 0, Census, NoCensus>::type cen;
@@ -408,7 +411,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
         }
         if (alive) {
             ++rays;
-            alive = path_step(P, S, stack, st, cen, prof);
+            alive = path_step<MODE>(P, S, stack, st, cen, prof);
             if (!alive) {
                 if (COUNT) deposits += st.stored;
                 finish_path(P, st);
@@ -422,32 +425,35 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
     }
 }
 
+#define PM_LAUNCH_MODES(KERNEL, GRID, BLOCK, LDS, STREAM, PARAMS, COUNT)                                        \
+    switch (scene_mode((PARAMS).S)) {                                                                            \
+    case MODE_BRUTE:                                                                                             \
+        if (COUNT) hipLaunchKernelGGL((KERNEL<1, MODE_BRUTE>), GRID, BLOCK, LDS, STREAM, PARAMS);                \
+        else hipLaunchKernelGGL((KERNEL<0, MODE_BRUTE>), GRID, BLOCK, LDS, STREAM, PARAMS);                      \
+        break;                                                                                                   \
+    case MODE_LDS:                                                                                               \
+        if (COUNT) hipLaunchKernelGGL((KERNEL<1, MODE_LDS>), GRID, BLOCK, LDS, STREAM, PARAMS);                  \
+        else hipLaunchKernelGGL((KERNEL<0, MODE_LDS>), GRID, BLOCK, LDS, STREAM, PARAMS);                        \
+        break;                                                                                                   \
+    default:                                                                                                     \
+        if (COUNT) hipLaunchKernelGGL((KERNEL<1, MODE_GLOBAL>), GRID, BLOCK, LDS, STREAM, PARAMS);               \
+        else hipLaunchKernelGGL((KERNEL<0, MODE_GLOBAL>), GRID, BLOCK, LDS, STREAM, PARAMS);                     \
+        break;                                                                                                   \
+    }
+
 hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s) {
     if (p.path_count <= 0) return hipSuccess;
+    const size_t lds = (size_t)p.S.stack_depth * TRACE_BLOCK * 4 + p.S.lds_bytes;
     if (p.per_block == 0) {
         if (p.wave_paths < 64 || p.refill_min < 1) return hipErrorInvalidValue;
         const int64_t waves = (p.path_count + p.wave_paths - 1) / p.wave_paths;
         const unsigned grid = (unsigned)((waves + TRACE_BLOCK / 64 - 1) / (TRACE_BLOCK / 64));
-        const size_t lds = (size_t)p.S.stack_depth * TRACE_BLOCK * 4 + p.S.lds_bytes;
-        if (p.S.lds_bytes) {
-            if (count) hipLaunchKernelGGL((k_trace_lane<1, true>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
-            else hipLaunchKernelGGL((k_trace_lane<0, true>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
-        } else {
-            if (count) hipLaunchKernelGGL((k_trace_lane<1, false>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
-            else hipLaunchKernelGGL((k_trace_lane<0, false>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
-        }
+        PM_LAUNCH_MODES(k_trace_lane, dim3(grid), dim3(TRACE_BLOCK), lds, s, p, count);
         return hipGetLastError();
     }
     if (p.per_block < 0) return hipErrorInvalidValue;
-    unsigned grid = (unsigned)((p.path_count + p.per_block - 1) / p.per_block);
-    const size_t lds = (size_t)p.S.stack_depth * TRACE_BLOCK * 4 + p.S.lds_bytes;
-    if (p.S.lds_bytes) {
-        if (count) hipLaunchKernelGGL((k_trace<1, true>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
-        else hipLaunchKernelGGL((k_trace<0, true>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
-    } else {
-        if (count) hipLaunchKernelGGL((k_trace<1, false>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
-        else hipLaunchKernelGGL((k_trace<0, false>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
-    }
+    const unsigned grid = (unsigned)((p.path_count + p.per_block - 1) / p.per_block);
+    PM_LAUNCH_MODES(k_trace, dim3(grid), dim3(TRACE_BLOCK), lds, s, p, count);
     return hipGetLastError();
 }
 
