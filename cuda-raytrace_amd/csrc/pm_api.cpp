@@ -633,6 +633,7 @@ int pm_commit(void *ptr) {
     S.n_lights = (int)c->lights.size(); S.n_nodes = (int)nodes4.size() / 4;
     S.n_refs = (int)bvh.refs.size();
     S.n_tris = (int)tri_info.size(); S.n_disks = (int)nd; S.n_spheres = (int)ns;
+    S.tri_geo_g = S.tri_geo; S.tri_id_g = S.tri_id;
     {
         /* tiny LDS scenes skip the BVH (MODE_BRUTE); env PM_TRACE_BRUTE_MAX overrides the limit (0 = never) */
         const char *e = getenv("PM_TRACE_BRUTE_MAX");

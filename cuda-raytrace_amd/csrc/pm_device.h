@@ -78,6 +78,10 @@ struct SceneDev {
     int n_refs;      /* primitives (leaf refs) */
     int n_tris, n_disks, n_spheres;
     int brute;       /* 1: test every primitive wave-uniformly instead of the BVH (tiny LDS scenes) */
+    /* HBM copies of tri_geo / tri_id (never rebased to LDS): MODE_BRUTE reads
+     * them with wave-uniform indices through the scalar cache into SGPRs */
+    const float4 *tri_geo_g;
+    const uint32_t *tri_id_g;
     /* all arrays above are 16-B aligned sections of one blob in HBM */
     const char *blob;
     uint32_t blob_bytes;
@@ -189,8 +193,8 @@ PMD void permuted_halton4(uint32_t n, const uint32_t *p, float out[4]) {
 /* ------------------------------------------------------------ intersect */
 /* OptiX 3 intersect_triangle (cudatrianglemesh.cu:24) on precomputed
  * e0 = p1-p0, e1 = p0-p2, n = e1 x e0 (identical float values). */
-PMD bool isect_tri(const float4 *g, const Ray &ray, float *t, float *beta, float *gamma) {
-    float4 a = g[0], b = g[1], c = g[2];
+PMD bool isect_tri_v(const float4 a, const float4 b, const float4 c, const Ray &ray, float *t, float *beta,
+                     float *gamma) {
     v3 p0 = mk(a.x, a.y, a.z), e0 = mk(a.w, b.x, b.y), e1 = mk(b.z, b.w, c.x), n = mk(c.y, c.z, c.w);
     const v3 e2 = (1.0f / dot(n, ray.d)) * (p0 - ray.o);
     const v3 i = cross(ray.d, e2);
@@ -198,6 +202,9 @@ PMD bool isect_tri(const float4 *g, const Ray &ray, float *t, float *beta, float
     *gamma = dot(i, e0);
     *t = dot(n, e2);
     return (*t < ray.tmax) & (*t > ray.tmin) & (*beta >= 0.0f) & (*gamma >= 0.0f) & (*beta + *gamma <= 1);
+}
+PMD bool isect_tri(const float4 *g, const Ray &ray, float *t, float *beta, float *gamma) {
+    return isect_tri_v(g[0], g[1], g[2], ray, t, beta, gamma);
 }
 
 /* cudadisk.cu:18-50 */
@@ -324,14 +331,23 @@ PMD void consider(Hit &best, float t, float b, float g, uint32_t ref, uint32_t g
 
 /* MODE_BRUTE: every primitive, wave-uniform loop (same primitive in every
  * lane: broadcast LDS reads, no divergence, no stack) */
+typedef const float __attribute__((address_space(4))) *const_f32_ptr;
+typedef const uint32_t __attribute__((address_space(4))) *const_u32_ptr;
+
 template <bool ANY, class C>
 PMD bool brute_isect(const SceneDev &S, const Ray &ray, Hit &best, C &cen) {
+    const const_f32_ptr tg = (const_f32_ptr)S.tri_geo_g; /* constant address space: s_load */
+    const const_u32_ptr tid = (const_u32_ptr)S.tri_id_g;
+#pragma unroll 2
     for (int k = 0; k < S.n_tris; ++k) {
         cen.prim();
         float t, b, g;
-        const bool ok = isect_tri(S.tri_geo + 3 * k, ray, &t, &b, &g);
+        const const_f32_ptr q = tg + 12 * k;
+        const float4 a = make_float4(q[0], q[1], q[2], q[3]), bb = make_float4(q[4], q[5], q[6], q[7]),
+                     cc = make_float4(q[8], q[9], q[10], q[11]);
+        const bool ok = isect_tri_v(a, bb, cc, ray, &t, &b, &g);
         if (ANY) { if (ok) return true; continue; }
-        if (ok && t <= best.t) consider(best, t, b, g, (PRIM_TRI << 30) | (uint32_t)k, S.tri_id[k]);
+        if (ok && t <= best.t) consider(best, t, b, g, (PRIM_TRI << 30) | (uint32_t)k, tid[k]);
     }
     for (int k = 0; k < S.n_disks; ++k) {
         cen.prim();
