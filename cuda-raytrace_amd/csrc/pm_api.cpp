@@ -98,6 +98,7 @@ struct Ctx {
     int64_t trace_per_block = 0; /* 0: per-lane paths (default); >0: block-compacting pool (env PM_TRACE_PATHS_PER_BLOCK) */
     int64_t trace_wave_paths = 64; /* per-lane kernel: paths per wave (env PM_TRACE_WAVE_PATHS) */
     int trace_refill_min = 32;     /* per-lane kernel: idle lanes that trigger a refill (env PM_TRACE_REFILL_MIN) */
+    bool fuse_count = true;        /* bucket counting inside the trace kernel (env PM_FUSE_COUNT=0 disables) */
     std::map<std::string, TimerPool> timers;
 };
 
@@ -323,6 +324,7 @@ int pm_create(void **out, const pm_config *cfg) {
     if (const char *e = getenv("PM_TRACE_PATHS_PER_BLOCK")) c->trace_per_block = std::max(0LL, atoll(e));
     if (const char *e = getenv("PM_TRACE_WAVE_PATHS")) c->trace_wave_paths = std::max(64LL, atoll(e));
     if (const char *e = getenv("PM_TRACE_REFILL_MIN")) c->trace_refill_min = std::max(1, std::min(64, atoi(e)));
+    if (const char *e = getenv("PM_FUSE_COUNT")) c->fuse_count = atoi(e) != 0;
     (void)hipSetDevice(dev);
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -771,7 +773,7 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
      * of the bucket build (keys, ranks, per-cell counts) at deposit time; the
      * build then skips it (c->fused). Any other slot producer invalidates it. */
     c->fused.valid = false;
-    const bool fuse = p->gather_structure == PM_GATHER_GRID && path_begin == slot_path_base;
+    const bool fuse = c->fuse_count && p->gather_structure == PM_GATHER_GRID && path_begin == slot_path_base;
     if (fuse) {
         const GridDesc g = make_grid(c, p);
         HIPCHK(c, c->d_count.ensure(((size_t)g.ncells + 1) * 4));

@@ -334,20 +334,54 @@ PMD void consider(Hit &best, float t, float b, float g, uint32_t ref, uint32_t g
 typedef const float __attribute__((address_space(4))) *const_f32_ptr;
 typedef const uint32_t __attribute__((address_space(4))) *const_u32_ptr;
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+PMD f2 bc2(float x) { return f2{x, x}; }
+
+/* isect_tri_v for two triangles at once (packed v_pk_mul/add_f32): the same
+ * per-component IEEE operations in the same order, so each lane of the pair is
+ * bit-identical to the scalar test. */
+PMD void isect_tri_pair(const_f32_ptr qa, const_f32_ptr qb, const Ray &ray, f2 &t, f2 &beta, f2 &gamma) {
+    const f2 p0x = {qa[0], qb[0]}, p0y = {qa[1], qb[1]}, p0z = {qa[2], qb[2]};
+    const f2 e0x = {qa[3], qb[3]}, e0y = {qa[4], qb[4]}, e0z = {qa[5], qb[5]};
+    const f2 e1x = {qa[6], qb[6]}, e1y = {qa[7], qb[7]}, e1z = {qa[8], qb[8]};
+    const f2 nx = {qa[9], qb[9]}, ny = {qa[10], qb[10]}, nz = {qa[11], qb[11]};
+    const f2 dx = bc2(ray.d.x), dy = bc2(ray.d.y), dz = bc2(ray.d.z);
+    const f2 den = (nx * dx + ny * dy) + nz * dz; /* dot(n, d) */
+    f2 inv;
+    inv.x = 1.0f / den.x;
+    inv.y = 1.0f / den.y;
+    const f2 e2x = inv * (p0x - bc2(ray.o.x)), e2y = inv * (p0y - bc2(ray.o.y)), e2z = inv * (p0z - bc2(ray.o.z));
+    const f2 ix = dy * e2z - dz * e2y, iy = dz * e2x - dx * e2z, iz = dx * e2y - dy * e2x; /* cross(d, e2) */
+    beta = (ix * e1x + iy * e1y) + iz * e1z;
+    gamma = (ix * e0x + iy * e0y) + iz * e0z;
+    t = (nx * e2x + ny * e2y) + nz * e2z;
+}
+
 template <bool ANY, class C>
 PMD bool brute_isect(const SceneDev &S, const Ray &ray, Hit &best, C &cen) {
     const const_f32_ptr tg = (const_f32_ptr)S.tri_geo_g; /* constant address space: s_load */
     const const_u32_ptr tid = (const_u32_ptr)S.tri_id_g;
+    int k = 0;
 #pragma unroll 2
-    for (int k = 0; k < S.n_tris; ++k) {
+    for (; k + 1 < S.n_tris; k += 2) {
+        cen.prim(); cen.prim();
+        f2 t, b, g;
+        isect_tri_pair(tg + 12 * k, tg + 12 * (k + 1), ray, t, b, g);
+        const bool ok0 = (t.x < ray.tmax) & (t.x > ray.tmin) & (b.x >= 0.0f) & (g.x >= 0.0f) & (b.x + g.x <= 1);
+        const bool ok1 = (t.y < ray.tmax) & (t.y > ray.tmin) & (b.y >= 0.0f) & (g.y >= 0.0f) & (b.y + g.y <= 1);
+        if (ANY) { if (ok0 | ok1) return true; continue; }
+        if (ok0 && t.x <= best.t) consider(best, t.x, b.x, g.x, (PRIM_TRI << 30) | (uint32_t)k, tid[k]);
+        if (ok1 && t.y <= best.t) consider(best, t.y, b.y, g.y, (PRIM_TRI << 30) | (uint32_t)(k + 1), tid[k + 1]);
+    }
+    if (k < S.n_tris) {
         cen.prim();
         float t, b, g;
         const const_f32_ptr q = tg + 12 * k;
         const float4 a = make_float4(q[0], q[1], q[2], q[3]), bb = make_float4(q[4], q[5], q[6], q[7]),
                      cc = make_float4(q[8], q[9], q[10], q[11]);
         const bool ok = isect_tri_v(a, bb, cc, ray, &t, &b, &g);
-        if (ANY) { if (ok) return true; continue; }
-        if (ok && t <= best.t) consider(best, t, b, g, (PRIM_TRI << 30) | (uint32_t)k, tid[k]);
+        if (ANY && ok) return true;
+        if (!ANY && ok && t <= best.t) consider(best, t, b, g, (PRIM_TRI << 30) | (uint32_t)k, tid[k]);
     }
     for (int k = 0; k < S.n_disks; ++k) {
         cen.prim();

@@ -394,6 +394,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
     int64_t cursor = wbegin; /* wave-uniform: next unassigned path of the pool */
     PathState st;
     bool alive = false;
+    prof.begin();
     while (true) {
         const unsigned long long idle = __ballot(!alive);
         const int nidle = __popcll(idle);
@@ -405,6 +406,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
             }
             cursor = cursor + nidle < wend ? cursor + nidle : wend;
         }
+        prof.mark(0);
         if (!__ballot(alive)) {
             if (cursor >= wend) break;
             continue;
@@ -417,7 +419,9 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
                 finish_path(P, st);
             }
         }
+        prof.mark(2);
     }
+    prof.flush(P.prof);
     if (COUNT) {
         uint32_t nodes = 0, prims = 0;
         if constexpr (COUNT != 0) { nodes = cen.nodes; prims = cen.prims; }
