@@ -92,6 +92,10 @@ struct Ctx {
     /* misc */
     DevBuf d_out, d_counters;
     bool counting = false;
+    /* record view (pm_set_record_view): active records compacted in record order */
+    bool view_active = false;
+    int64_t n_view = 0;
+    DevBuf d_vflags, d_vrank, d_vlist, d_vsums;
     /* pm_reset_records is deferred: records read as (flux 0, N 0, r2 = rec_fresh_r2) */
     bool rec_fresh = false;
     float rec_fresh_r2 = 0.f;
@@ -256,6 +260,7 @@ GatherParams gather_params(Ctx *c, const pm_render_params *p) {
     G.ph_a = c->d_pha.as<float4>(); G.ph_b = c->d_phb.as<float4>(); G.ph_c = c->d_phc.as<float>();
     G.kd_nodes = c->d_kd.as<pm_photon>(); G.kd_count = c->kd_count;
     G.counters = c->d_counters.as<unsigned long long>();
+    if (c->view_active) { G.view_rank = c->d_vrank.as<uint32_t>(); G.view_list = c->d_vlist.as<uint32_t>(); }
     /* fixed-point scale 2^S: a single contribution is bounded by
      * alpha_max * Kd_max / pi with alpha_max = emission * Kd_max^mpc (Lambert
      * weight ~Kd, specular weight 1); x4 headroom; 2^40 per contribution
@@ -267,6 +272,26 @@ GatherParams gather_params(Ctx *c, const pm_render_params *p) {
     G.fx_inv = std::ldexp(1.0, -S);
     return G;
 }
+
+/* (re)builds the active-record view from the current records; synchronizes to read its size */
+int build_view(Ctx *c, hipStream_t s) {
+    const int64_t n = c->nrec;
+    HIPCHK(c, c->d_vflags.ensure((size_t)(n + 1) * 4));
+    HIPCHK(c, c->d_vrank.ensure((size_t)(n + 1) * 4));
+    HIPCHK(c, c->d_vlist.ensure((size_t)std::max<int64_t>(n, 1) * 4));
+    HIPCHK(c, c->d_vsums.ensure(scan_scratch_words(n + 1) * 4));
+    HIPCHK(c, launch_record_view(recs(c), c->d_vflags.as<uint32_t>(), c->d_vrank.as<uint32_t>(),
+                                 c->d_vlist.as<uint32_t>(), c->d_vsums.as<uint32_t>(), s));
+    uint32_t total = 0;
+    HIPCHK(c, hipMemcpyAsync(&total, c->d_vrank.as<uint32_t>() + n, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->n_view = total;
+    return PM_OK;
+}
+
+/* number of records the range-based record calls address */
+int64_t view_size(const Ctx *c) { return c->view_active ? c->n_view : c->nrec; }
+const uint32_t *view_list(Ctx *c) { return c->view_active ? c->d_vlist.as<uint32_t>() : nullptr; }
 
 /* applies a deferred pm_reset_records before a reader that is not a fused full gather */
 int materialize_reset(Ctx *c, hipStream_t s) {
@@ -351,7 +376,7 @@ void pm_destroy(void *ptr) {
             (void)hipEventDestroy(t.b);
         }
     DevBuf *bufs[] = {&c->d_scene, &c->d_rays, &c->d_rand2d, &c->d_pos, &c->d_nrm, &c->d_state, &c->d_n,
-                      &c->d_dl, &c->d_slots, &c->d_count, &c->d_scratch,
+                      &c->d_dl, &c->d_slots, &c->d_count, &c->d_scratch, &c->d_vflags, &c->d_vrank, &c->d_vlist, &c->d_vsums,
                       &c->d_cell_start, &c->d_pha, &c->d_phb, &c->d_phc,
                       &c->d_kd, &c->d_out, &c->d_counters};
     for (DevBuf *b : bufs) b->release();
@@ -681,6 +706,7 @@ int pm_eye_pass(void *ptr, const pm_render_params *p, void *stream) {
     HIPCHK(c, launch_eye(E, s));
     timer_end(c, "eye", s);
     c->rec_fresh = false; /* the eye pass writes every record */
+    if (c->view_active && (rc = build_view(c, s))) return rc;
     return PM_OK;
 }
 
@@ -884,7 +910,7 @@ int pm_ppm_update(void *ptr, const pm_render_params *p, const void *d_partial, i
     GETCTX(ptr);
     int rc;
     if ((rc = check_params(c, p))) return rc;
-    if (!d_partial || rec_begin < 0 || rec_count < 0 || rec_begin + rec_count > c->nrec)
+    if (!d_partial || rec_begin < 0 || rec_count < 0 || rec_begin + rec_count > view_size(c))
         FAIL(c, PM_ERR_INVALID, "bad record range");
     hipStream_t s = pick(c, stream);
     if ((rc = materialize_reset(c, s))) return rc;
@@ -897,21 +923,21 @@ int pm_ppm_update(void *ptr, const pm_render_params *p, const void *d_partial, i
 
 int pm_get_radius2(void *ptr, int64_t rec_begin, int64_t rec_count, void *d_out, void *stream) {
     GETCTX(ptr);
-    if (!d_out || rec_begin < 0 || rec_count < 0 || rec_begin + rec_count > c->nrec)
+    if (!d_out || rec_begin < 0 || rec_count < 0 || rec_begin + rec_count > view_size(c))
         FAIL(c, PM_ERR_INVALID, "bad radius2 range");
     int rc;
     if ((rc = materialize_reset(c, pick(c, stream)))) return rc;
-    HIPCHK(c, launch_radius2_io(recs(c), (float *)d_out, rec_begin, rec_count, 0, pick(c, stream)));
+    HIPCHK(c, launch_radius2_io(recs(c), (float *)d_out, rec_begin, rec_count, 0, view_list(c), pick(c, stream)));
     return PM_OK;
 }
 
 int pm_set_radius2(void *ptr, const void *d_in, int64_t rec_begin, int64_t rec_count, void *stream) {
     GETCTX(ptr);
-    if (!d_in || rec_begin < 0 || rec_count < 0 || rec_begin + rec_count > c->nrec)
+    if (!d_in || rec_begin < 0 || rec_count < 0 || rec_begin + rec_count > view_size(c))
         FAIL(c, PM_ERR_INVALID, "bad radius2 range");
     int rc;
     if ((rc = materialize_reset(c, pick(c, stream)))) return rc;
-    HIPCHK(c, launch_radius2_io(recs(c), (float *)d_in, rec_begin, rec_count, 1, pick(c, stream)));
+    HIPCHK(c, launch_radius2_io(recs(c), (float *)d_in, rec_begin, rec_count, 1, view_list(c), pick(c, stream)));
     return PM_OK;
 }
 
@@ -1079,6 +1105,7 @@ int pm_upload_records(void *ptr, const pm_record *in, int64_t n) {
     HIPCHK(c, hipMemcpy(c->d_dl.p, dl.data(), n * 16, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_n.p, N.data(), n * 4, hipMemcpyHostToDevice));
     c->rec_fresh = false; /* every record overwritten */
+    if (c->view_active && (rc = build_view(c, c->stream))) return rc;
     return PM_OK;
 }
 
@@ -1120,6 +1147,46 @@ int pm_trace_profile(void *ptr, int64_t out[8], int reset) {
     HIPCHK(c, hipMemcpy(h, c->d_counters.as<unsigned long long>() + 8, 64, hipMemcpyDeviceToHost));
     for (int i = 0; i < 8; ++i) out[i] = (int64_t)h[i];
     if (reset) HIPCHK(c, hipMemset(c->d_counters.as<unsigned long long>() + 8, 0, 64));
+    return PM_OK;
+}
+
+int pm_final_view(void *ptr, double emitted, int64_t v_begin, int64_t v_count, void *d_out, void *stream) {
+    GETCTX(ptr);
+    if (!c->view_active) FAIL(c, PM_ERR_INVALID, "no active-record view (pm_set_record_view)");
+    if (!d_out || v_begin < 0 || v_count < 0 || v_begin + v_count > c->n_view) FAIL(c, PM_ERR_INVALID, "bad view range");
+    hipStream_t s = pick(c, stream);
+    int rc;
+    if ((rc = materialize_reset(c, s))) return rc;
+    FinalParams F{};
+    F.R = recs(c);
+    F.emitted = (float)emitted;
+    F.rec_begin = v_begin; F.rec_count = v_count; F.out = (float *)d_out; F.raster = 0; F.W = c->W;
+    F.view = c->d_vlist.as<uint32_t>();
+    timer_begin(c, "final", s);
+    HIPCHK(c, launch_final(F, s));
+    timer_end(c, "final", s);
+    return PM_OK;
+}
+
+int pm_record_view_list(void *ptr, void *d_out, void *stream) {
+    GETCTX(ptr);
+    if (!c->view_active) FAIL(c, PM_ERR_INVALID, "no active-record view (pm_set_record_view)");
+    if (!d_out) FAIL(c, PM_ERR_INVALID, "null output");
+    if (c->n_view > 0)
+        HIPCHK(c, hipMemcpyAsync(d_out, c->d_vlist.p, (size_t)c->n_view * 4, hipMemcpyDeviceToDevice, pick(c, stream)));
+    return PM_OK;
+}
+
+int pm_set_record_view(void *ptr, int active_only, int64_t *n_view) {
+    GETCTX(ptr);
+    if (active_only) {
+        if (c->nrec <= 0) FAIL(c, PM_ERR_INVALID, "no records (run pm_eye_pass first)");
+        int rc;
+        HIPCHK(c, hipDeviceSynchronize());
+        if ((rc = build_view(c, c->stream))) return rc;
+    }
+    c->view_active = active_only != 0;
+    if (n_view) *n_view = view_size(c);
     return PM_OK;
 }
 

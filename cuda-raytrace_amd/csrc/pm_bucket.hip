@@ -159,6 +159,17 @@ __global__ __launch_bounds__(256) void k_bucket_fill(const pm_photon *slots, int
     ph_c[dst] = e.y;
 }
 
+size_t scan_scratch_words(int64_t n) { return (size_t)((n + SCAN_TILE - 1) / SCAN_TILE) + 16; }
+
+hipError_t launch_exclusive_scan(const uint32_t *in, int64_t n, uint32_t *out, uint32_t *sums, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int ntile = (int)((n + SCAN_TILE - 1) / SCAN_TILE);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(ntile), dim3(SCAN_BLOCK), 0, s, in, n, sums);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_BLOCK), 0, s, sums, ntile);
+    hipLaunchKernelGGL(k_scan_down, dim3(ntile), dim3(SCAN_BLOCK), 0, s, in, n, sums, out);
+    return hipGetLastError();
+}
+
 size_t bucket_scratch_words(int64_t n_slots, uint32_t ncells) {
     const int64_t ntile = ((int64_t)ncells + 1 + SCAN_TILE - 1) / SCAN_TILE;
     return (size_t)(2 * n_slots + ntile + 16);

@@ -36,6 +36,13 @@ PMD void ppm_apply(float4 &st, float &N, int M, v3 L, float alpha) {
  * arrival order in pm_bucket.hip) and the number of GPUs that hold the
  * photons therefore never change a bit of the result. */
 struct Fx3 { long long x, y, z; };
+/* where record r's partial goes: its rank in the record view (active records
+ * only, -1 = not in the view) or r itself (all-records view) */
+PMD long long *partial_slot(const GatherParams &P, int64_t r) {
+    if (!P.view_rank) return P.partial + 4 * r;
+    const uint32_t k = P.view_rank[r];
+    return k == 0xffffffffu ? nullptr : P.partial + 4 * (int64_t)k;
+}
 PMD long long to_fx(float c, float scale) { return (long long)rintf(c * scale); }
 PMD void write_partial(long long *p, int M, Fx3 L) {
     longlong2 *q = reinterpret_cast<longlong2 *>(p);
@@ -54,7 +61,7 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_grid(GatherParams P) {
         float4 pos = P.R.pos[r];
         uint32_t flags = (uint32_t)__float_as_int(pos.w);
         if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) {
-            if (PARTIAL) write_partial(P.partial + 4 * r, 0, Fx3{0, 0, 0});
+            if (PARTIAL) { if (long long *q = partial_slot(P, r)) write_partial(q, 0, Fx3{0, 0, 0}); }
         } else {
             float4 st = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : P.R.state[r];
             float4 nrm = P.R.nrm[r];
@@ -117,7 +124,7 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_grid(GatherParams P) {
             }
             if (COUNT) { hits += (unsigned long long)M; act++; }
             if (PARTIAL) {
-                write_partial(P.partial + 4 * r, M, Lf);
+                write_partial(partial_slot(P, r), M, Lf);
             } else {
                 const double inv = P.fx_inv;
                 v3 L = mk((float)((double)Lf.x * inv), (float)((double)Lf.y * inv), (float)((double)Lf.z * inv));
@@ -142,7 +149,7 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_kd(GatherParams P) {
         float4 pos = P.R.pos[r];
         uint32_t flags = (uint32_t)__float_as_int(pos.w);
         if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) {
-            if (PARTIAL) write_partial(P.partial + 4 * r, 0, Fx3{0, 0, 0});
+            if (PARTIAL) { if (long long *q = partial_slot(P, r)) write_partial(q, 0, Fx3{0, 0, 0}); }
         } else {
             float4 st = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : P.R.state[r];
             float4 nrm = P.R.nrm[r];
@@ -193,7 +200,7 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_kd(GatherParams P) {
             if (COUNT) { hits += (unsigned long long)M; act++; }
             if (PARTIAL) {
                 const float sc = P.fx_scale;
-                write_partial(P.partial + 4 * r, M, Fx3{to_fx(L.x, sc), to_fx(L.y, sc), to_fx(L.z, sc)});
+                write_partial(partial_slot(P, r), M, Fx3{to_fx(L.x, sc), to_fx(L.y, sc), to_fx(L.z, sc)});
             } else {
                 float N = P.fresh ? 0.f : P.R.n[r];
                 ppm_apply(st, N, M, L, P.ppm_alpha);
@@ -233,28 +240,28 @@ hipError_t launch_gather(const GatherParams &p, int structure, int partial, int 
  * owner's PPM update every rank needs the new radii for the next pass's
  * range queries (pmrender/dist.py, "reduce" exchange) */
 __global__ __launch_bounds__(256) void k_radius2_io(RecordsDev R, float *buf, int64_t rec_begin, int64_t rec_count,
-                                                    int to_records) {
+                                                    int to_records, const uint32_t *view) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= rec_count) return;
-    const int64_t r = rec_begin + i;
+    const int64_t r = view ? (int64_t)view[rec_begin + i] : rec_begin + i;
     if (to_records) R.state[r].w = buf[i];
     else buf[i] = R.state[r].w;
 }
 
 hipError_t launch_radius2_io(const RecordsDev &R, float *buf, int64_t rec_begin, int64_t rec_count, int to_records,
-                             hipStream_t s) {
+                             const uint32_t *view, hipStream_t s) {
     if (rec_count <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_radius2_io, dim3((unsigned)((rec_count + 255) / 256)), dim3(256), 0, s, R, buf, rec_begin,
-                       rec_count, to_records);
+                       rec_count, to_records, view);
     return hipGetLastError();
 }
 
 /* PPM update from summed partials (M, L in fixed point), record chunk */
 __global__ __launch_bounds__(256) void k_ppm_update(RecordsDev R, const long long *partial, int64_t rec_begin,
-                                                    int64_t rec_count, float alpha, double inv) {
+                                                    int64_t rec_count, float alpha, double inv, const uint32_t *view) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= rec_count) return;
-    const int64_t r = rec_begin + i;
+    const int64_t r = view ? (int64_t)view[rec_begin + i] : rec_begin + i;
     uint32_t flags = (uint32_t)__float_as_int(R.pos[r].w);
     if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) return;
     const longlong2 *q = reinterpret_cast<const longlong2 *>(partial + 4 * i);
@@ -273,7 +280,36 @@ hipError_t launch_ppm_update(const GatherParams &p, const long long *partial, in
                              hipStream_t s) {
     if (rec_count <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_ppm_update, dim3((unsigned)((rec_count + 255) / 256)), dim3(256), 0, s, p.R, partial,
-                       rec_begin, rec_count, p.ppm_alpha, p.fx_inv);
+                       rec_begin, rec_count, p.ppm_alpha, p.fx_inv, p.view_list);
+    return hipGetLastError();
+}
+
+/* ====================================================================== */
+/* record view (active records, compacted in record order)               */
+/* ====================================================================== */
+__global__ __launch_bounds__(256) void k_view_flags(RecordsDev R, uint32_t *flags) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r > R.count) return;
+    if (r == R.count) { flags[r] = 0u; return; } /* scanned tail -> total */
+    const uint32_t f = (uint32_t)__float_as_int(R.pos[r].w);
+    flags[r] = (f & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) ? 0u : 1u;
+}
+
+__global__ __launch_bounds__(256) void k_view_list(RecordsDev R, const uint32_t *flags, uint32_t *rank,
+                                                   uint32_t *list) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= R.count) return;
+    if (flags[r]) list[rank[r]] = (uint32_t)r;
+    else rank[r] = 0xffffffffu;
+}
+
+hipError_t launch_record_view(const RecordsDev &R, uint32_t *flags, uint32_t *rank, uint32_t *list, uint32_t *sums,
+                              hipStream_t s) {
+    const int64_t n = R.count;
+    hipLaunchKernelGGL(k_view_flags, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, s, R, flags);
+    hipError_t e = launch_exclusive_scan(flags, n + 1, rank, sums, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_view_list, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, R, flags, rank, list);
     return hipGetLastError();
 }
 
@@ -283,7 +319,7 @@ hipError_t launch_ppm_update(const GatherParams &p, const long long *partial, in
 __global__ __launch_bounds__(256) void k_final(FinalParams P) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= P.rec_count) return;
-    const int64_t r = P.rec_begin + i;
+    const int64_t r = P.view ? (int64_t)P.view[P.rec_begin + i] : P.rec_begin + i;
     int64_t o = i;
     if (P.raster) {
         int px, py;

@@ -95,6 +95,10 @@ struct GatherParams {
      * initial PPM state (flux 0, N 0, r2init) instead of memory, write it back */
     int fresh;
     float r2init;
+    /* record view: view_rank[r] = position of record r in the view (partials),
+     * view_list[i] = record of view position i (update); null = all records */
+    const uint32_t *view_rank;
+    const uint32_t *view_list;
     unsigned long long *counters; /* [0] visited, [1] in radius */
 };
 
@@ -105,6 +109,7 @@ struct FinalParams {
     float *out;     /* float3 */
     int raster;     /* 1: out indexed by pixel (pinhole), 0: by record - rec_begin */
     int W;
+    const uint32_t *view; /* non-null: [rec_begin, rec_begin + rec_count) index the active-record view */
 };
 
 /* traversal mode of a scene: LDS-resident blob (brute force when tiny) or HBM */
@@ -126,7 +131,13 @@ hipError_t launch_ppm_update(const GatherParams &p, const long long *partial, in
                              hipStream_t s);
 hipError_t launch_final(const FinalParams &p, hipStream_t s);
 hipError_t launch_radius2_io(const RecordsDev &R, float *buf, int64_t rec_begin, int64_t rec_count, int to_records,
-                             hipStream_t s);
+                             const uint32_t *view, hipStream_t s);
+/* exclusive scan of n uint32 (pm_bucket.hip); in/out 16-B aligned; sums: scan_scratch_words(n) */
+size_t scan_scratch_words(int64_t n);
+hipError_t launch_exclusive_scan(const uint32_t *in, int64_t n, uint32_t *out, uint32_t *sums, hipStream_t s);
+/* active-record view: flags/rank n+1 words, list n words; rank[n] = active count */
+hipError_t launch_record_view(const RecordsDev &R, uint32_t *flags, uint32_t *rank, uint32_t *list, uint32_t *sums,
+                              hipStream_t s);
 hipError_t launch_reset_records(const RecordsDev &R, float r2init, hipStream_t s);
 
 } // namespace pm

@@ -6,16 +6,21 @@ Work split:
     in a 1-GPU run (owner-writes, photontracing.cu:93,144);
   * gather records: every rank holds the full eye-pass record set (the eye
     pass is deterministic and cheap, so it is replicated instead of
-    exchanged); PPM state is owned per contiguous record chunk.
+    exchanged); PPM state is owned per contiguous chunk of the ACTIVE
+    records (pm_set_record_view: MISS / EXCEPTION / padding records never
+    take part in the exchange — 47% of the records at C2).
 
 Two exchange strategies:
   * "reduce" (default): each rank builds a map of ITS photons and gathers all
     records against it; the PPM estimator's sums (M, L) are linear in the
-    photon set, so a reduce-scatter of one int64x4 per record (M and the
-    flux in the gather's exact fixed point) gives every owner the global
+    photon set, so a reduce-scatter of one int64x4 per active record (M and
+    the flux in the gather's exact fixed point) gives every owner the global
     (M, L) of its chunk, bit-identical to a 1-GPU gather; the owner then
-    applies the PPM update. Bytes on xGMI per pass: 32 B x records (66 MB at
-    1080p), independent of the photon count.
+    applies the PPM update and the new radii are all-gathered. Bytes on xGMI
+    per pass: 32 B + 4 B per active record (39 MB at 1080p), independent of
+    the photon count. The reduce-scatter is issued asynchronously and only
+    waited for after the NEXT pass's trace and bucket build (which do not
+    read records), so it overlaps them; flush() completes the last one.
   * "allgather": the reference-style exchange: all-gather the
     40-B photon slots into a replicated map, gather locally owned chunks.
     Bytes per pass: 40 B x slots x (N-1)/N per rank.
@@ -61,6 +66,9 @@ class HipEngine:
     def reset_records(self, p):
         self.ctx.reset_records(p, self._s())
 
+    def set_record_view(self, active_only=True):
+        return self.ctx.set_record_view(active_only)
+
     def trace_photons(self, p, pass_index, path_begin, path_count, slot_path_base):
         self.ctx.trace_photons(p, pass_index, path_begin, path_count, slot_path_base, self._s())
 
@@ -88,6 +96,12 @@ class HipEngine:
     def final(self, emitted, rec_begin, rec_count, out):
         self.ctx.final(emitted, rec_begin, rec_count, out.data_ptr(), self._s())
 
+    def final_view(self, emitted, v_begin, v_count, out):
+        self.ctx.final_view(emitted, v_begin, v_count, out.data_ptr(), self._s())
+
+    def record_view_list(self, out):
+        self.ctx.record_view_list(out.data_ptr(), self._s())
+
 
 class PassRunner:
     def __init__(self, engine, params, rank=0, world=1, exchange="reduce"):
@@ -99,16 +113,21 @@ class PassRunner:
         self.slots_per_rank = self.paths * int(params.max_photon_count)
         n = engine.num_records()
         self.n_records = n
-        self.rec_begin, self.rec_count, self.rec_per = _chunk(n, world, rank)
+        self.rec_begin, self.rec_count, self.rec_per = _chunk(n, world, rank)   # final image split
         self.padded = self.rec_per * world
         self.partial = None
         self.chunk = None
         self.slot_buf = None
+        self._pending = None
         if world > 1 and exchange == "reduce":
-            # per record (M, L.rgb) as int64 fixed point: the sum over ranks is exact
-            self.partial = engine.alloc((self.padded, 4), torch.int64)
-            self.chunk = engine.alloc((self.rec_per, 4), torch.int64)
-            self.r2_all = engine.alloc((self.padded,), torch.float32)
+            # exchange over the active records only, owned in contiguous chunks of the view
+            self.n_view = engine.set_record_view(True)
+            self.v_begin, self.v_count, self.v_per = _chunk(self.n_view, world, rank)
+            # per active record (M, L.rgb) as int64 fixed point: the sum over ranks is exact;
+            # rows past n_view stay zero
+            self.partial = engine.alloc((self.v_per * world, 4), torch.int64)
+            self.chunk = engine.alloc((self.v_per, 4), torch.int64)
+            self.r2_all = engine.alloc((self.v_per * world,), torch.float32)
         if world > 1 and exchange == "allgather":
             self.slot_buf = engine.alloc((world * self.slots_per_rank * PHOTON_DTYPE.itemsize,), torch.uint8)
             engine.use_slot_buffer(self.slot_buf)
@@ -117,50 +136,99 @@ class PassRunner:
     def emitted_per_pass(self):
         return self.paths * self.world
 
-    def _reduce_scatter(self):
-        if dist.get_backend() == "gloo":     # gloo has no reduce_scatter: all-reduce + slice
-            dist.all_reduce(self.partial)
-            self.chunk.copy_(self.partial[self.rank * self.rec_per:(self.rank + 1) * self.rec_per])
+    # gloo (CPU tests, or several ranks sharing one GPU) has no reduce_scatter
+    # and works on host tensors: device tensors are staged through host memory
+    @staticmethod
+    def _gloo():
+        return dist.get_backend() == "gloo"
+
+    def _all_gather(self, out, mine):
+        if self._gloo() and out.is_cuda:
+            host = out.cpu()
+            dist.all_gather_into_tensor(host, mine.cpu())
+            out.copy_(host)
         else:
-            dist.reduce_scatter_tensor(self.chunk, self.partial)
+            dist.all_gather_into_tensor(out, mine)
+
+    def _start_exchange(self):
+        if self._gloo():
+            self._pending = ("gloo", None)   # done synchronously in _finish_exchange
+        else:
+            self._pending = ("rs", dist.reduce_scatter_tensor(self.chunk, self.partial, async_op=True))
+
+    def _finish_exchange(self):
+        """Complete the previous pass: summed (M, L) -> owner PPM update -> radii to every rank."""
+        if self._pending is None:
+            return
+        kind, work = self._pending
+        self._pending = None
+        if kind == "gloo":                   # all-reduce + slice
+            host = self.partial.cpu()
+            dist.all_reduce(host)
+            self.chunk.copy_(host[self.rank * self.v_per:(self.rank + 1) * self.v_per])
+        else:
+            work.wait()                      # the compute stream waits for the collective
+        e, p = self.e, self.p
+        e.ppm_update(p, self.chunk, self.v_begin, self.v_count)
+        mine = self.r2_all[self.rank * self.v_per:(self.rank + 1) * self.v_per]
+        e.get_radius2(self.v_begin, self.v_count, mine)
+        self._all_gather(self.r2_all, mine)
+        e.set_radius2(self.r2_all, 0, self.n_view)
+
+    def flush(self):
+        """Finish the exchange still in flight (call before reading records or timing)."""
+        self._finish_exchange()
 
     def step(self, pass_index, reset=False):
         """One PPM pass: trace this rank's paths, build, gather (+ exchange)."""
         e, p = self.e, self.p
-        if reset:
-            e.reset_records(p)
         if self.world == 1:
+            if reset:
+                e.reset_records(p)
             e.trace_photons(p, pass_index, 0, self.paths, 0)
             e.build_photon_map(p, self.slots_per_rank)
             e.gather(p)
             return
         if self.exchange == "reduce":
+            # trace + build do not read records: they overlap the previous exchange
             e.trace_photons(p, pass_index, self.path_begin, self.paths, self.path_begin)
             e.build_photon_map(p, self.slots_per_rank)
+            self._finish_exchange()
+            if reset:
+                e.reset_records(p)
             e.gather_partial(p, self.partial)
-            self._reduce_scatter()
-            e.ppm_update(p, self.chunk, self.rec_begin, self.rec_count)
-            # publish the owners' new radii: every rank queries the next pass with them
-            mine = self.r2_all[self.rank * self.rec_per:(self.rank + 1) * self.rec_per]
-            e.get_radius2(self.rec_begin, self.rec_count, mine)
-            dist.all_gather_into_tensor(self.r2_all, mine)
-            e.set_radius2(self.r2_all, 0, self.n_records)
+            self._start_exchange()
         else:
+            if reset:
+                e.reset_records(p)
             e.trace_photons(p, pass_index, self.path_begin, self.paths, 0)
             mine = self.slot_buf[self.rank * self.slots_per_rank * PHOTON_DTYPE.itemsize:
                                  (self.rank + 1) * self.slots_per_rank * PHOTON_DTYPE.itemsize]
-            dist.all_gather_into_tensor(self.slot_buf, mine)
+            self._all_gather(self.slot_buf, mine)
             e.build_photon_map(p, self.world * self.slots_per_rank)
             e.gather_range(p, self.rec_begin, self.rec_count)   # replicated map, owned records
 
     def final_gather(self, emitted, out_full):
         """Final radiance of all records (record order) on every rank."""
+        self.flush()
         if self.world == 1:
             self.e.final(emitted, 0, self.n_records, out_full)
+            return out_full
+        if self.exchange == "reduce":
+            # owners hold the PPM state of their view chunk; records outside the
+            # active view (MISS / EXCEPTION / padding) are black
+            mine = self.e.alloc((self.v_per, 3), torch.float32)
+            self.e.final_view(emitted, self.v_begin, self.v_count, mine)
+            gathered = self.e.alloc((self.v_per * self.world, 3), torch.float32)
+            self._all_gather(gathered, mine)
+            view = self.e.alloc((self.n_view,), torch.int32)
+            self.e.record_view_list(view)
+            out_full.zero_()
+            out_full[view.long()] = gathered[: self.n_view]
             return out_full
         mine = self.e.alloc((self.rec_per, 3), torch.float32)
         self.e.final(emitted, self.rec_begin, self.rec_count, mine)
         gathered = self.e.alloc((self.padded, 3), torch.float32)
-        dist.all_gather_into_tensor(gathered, mine)
+        self._all_gather(gathered, mine)
         out_full.copy_(gathered[: self.n_records])
         return out_full

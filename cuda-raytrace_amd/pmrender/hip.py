@@ -75,6 +75,9 @@ def load_library(path=None):
         "pm_trace_counters": (c_int, [vp, ctypes.POINTER(i64)]),
         "pm_trace_profile": (c_int, [vp, ctypes.POINTER(i64), c_int]),
         "pm_set_counting": (c_int, [vp, c_int]),
+        "pm_set_record_view": (c_int, [vp, c_int, ctypes.POINTER(i64)]),
+        "pm_final_view": (c_int, [vp, c_double, i64, i64, vp, vp]),
+        "pm_record_view_list": (c_int, [vp, vp, vp]),
         "pm_synchronize": (c_int, [vp]),
         "pm_last_kernel_ms": (c_int, [vp, ctypes.c_char_p, ctypes.POINTER(c_double)]),
         "pm_halton_permutation": (c_int, [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
@@ -295,6 +298,19 @@ class Context:
         if n > 0:
             self._chk(self.lib.pm_download_kdtree(self.h, out.ctypes.data, n))
         return out
+
+    def set_record_view(self, active_only=True):
+        """Index record-range calls by active records only (compacted); returns the view size."""
+        n = ctypes.c_int64()
+        self._chk(self.lib.pm_set_record_view(self.h, int(bool(active_only)), ctypes.byref(n)))
+        return int(n.value)
+
+    def final_view(self, emitted, v_begin, v_count, d_out, stream=None):
+        self._chk(self.lib.pm_final_view(self.h, float(emitted), int(v_begin), int(v_count), ctypes.c_void_p(d_out),
+                                         stream))
+
+    def record_view_list(self, d_out, stream=None):
+        self._chk(self.lib.pm_record_view_list(self.h, ctypes.c_void_p(d_out), stream))
 
     def set_counting(self, enabled=True):
         self._chk(self.lib.pm_set_counting(self.h, int(bool(enabled))))

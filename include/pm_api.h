@@ -189,9 +189,22 @@ int pm_gather(void *ctx, const pm_render_params *params, void *stream);
 int pm_gather_range(void *ctx, const pm_render_params *params, int64_t rec_begin, int64_t rec_count,
                     void *stream);
 /* Range query only: writes per record four int64 (M, L.r, L.g, L.b) to
- * d_partial (device pointer, 32 B x n_records); L is in the gather's exact
- * fixed point, so partials of photon shards sum to the 1-GPU result. */
+ * d_partial (device pointer, 32 B x records of the view, see
+ * pm_set_record_view); L is in the gather's exact fixed point, so partials of
+ * photon shards sum to the 1-GPU result. */
 int pm_gather_partial(void *ctx, const pm_render_params *params, void *d_partial, void *stream);
+/* Record view of pm_gather_partial, pm_ppm_update, pm_get_radius2 and
+ * pm_set_radius2 (their rec_begin / rec_count and buffers index the view):
+ * active_only = 0 -> all records (default); 1 -> only active records (not
+ * MISS / EXCEPTION / INVALID), compacted in record order — what a multi-GPU
+ * exchange has to move (53% of the records at C2). The view is rebuilt by
+ * every pm_eye_pass / pm_upload_records. *n_view = records in the view. */
+int pm_set_record_view(void *ctx, int active_only, int64_t *n_view);
+/* With the active view set: final radiance of view records [v_begin,
+ * v_begin + v_count) into d_out (float3 each, view order) and the view's
+ * record indices (uint32 x n_view) — records outside the view are black. */
+int pm_final_view(void *ctx, double emitted, int64_t v_begin, int64_t v_count, void *d_out, void *stream);
+int pm_record_view_list(void *ctx, void *d_out, void *stream);
 /* PPM update of records [rec_begin, rec_begin+rec_count) from summed partials
  * (d_partial points at the partial of rec_begin). */
 int pm_ppm_update(void *ctx, const pm_render_params *params, const void *d_partial,

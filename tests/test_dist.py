@@ -30,6 +30,7 @@ class OracleEngine:
         self.slots = None
         self.slot_buf = None
         self.nodes = None
+        self.view = None      # active-record view (indices), like pm_set_record_view
 
     def num_records(self):
         return len(self.recs)
@@ -42,6 +43,13 @@ class OracleEngine:
 
     def reset_records(self, p):
         self.recs = self.init.copy()
+
+    def set_record_view(self, active_only=True):
+        self.view = np.nonzero((self.recs["flags"] & 7) == 0)[0] if active_only else None
+        return len(self.view) if active_only else len(self.recs)
+
+    def _rec(self, i):
+        return int(self.view[i]) if self.view is not None else int(i)
 
     def trace_photons(self, p, pass_index, path_begin, path_count, slot_path_base):
         s = self.orc.trace_photons(p, pass_index, path_begin, path_count)
@@ -68,6 +76,8 @@ class OracleEngine:
 
     def gather_partial(self, p, out):
         part = self.orc.gather_partial(self.nodes, self.recs)
+        if self.view is not None:
+            part = part[self.view]
         n = len(part)
         out[:n, 0] = torch.from_numpy(part[:, 0].astype(np.int64))
         out[:n, 1:] = torch.from_numpy(np.rint(part[:, 1:].astype(np.float64) * self.FX).astype(np.int64))
@@ -77,7 +87,8 @@ class OracleEngine:
         lib = self.oracle.load()
         P = partial.numpy()
         for i in range(n):
-            r = self.recs[b + i]
+            ri = self._rec(b + i)
+            r = self.recs[ri]
             if r["flags"] & 7:
                 continue
             r2 = np.float32([r["radius2"]])
@@ -87,18 +98,27 @@ class OracleEngine:
             fp = ctypes.POINTER(ctypes.c_float)
             lib.orc_ppm_update(r2.ctypes.data_as(fp), N.ctypes.data_as(fp), flux.ctypes.data_as(fp), int(P[i, 0]),
                                L.ctypes.data_as(fp), float(p.ppm_alpha))
-            self.recs[b + i]["radius2"], self.recs[b + i]["photon_count"] = r2[0], N[0]
-            self.recs[b + i]["flux"] = flux
+            self.recs[ri]["radius2"], self.recs[ri]["photon_count"] = r2[0], N[0]
+            self.recs[ri]["flux"] = flux
 
     def get_radius2(self, b, n, out):
-        out[:n] = torch.from_numpy(self.recs["radius2"][b:b + n].copy())
+        idx = self.view[b:b + n] if self.view is not None else np.arange(b, b + n)
+        out[:n] = torch.from_numpy(self.recs["radius2"][idx].copy())
 
     def set_radius2(self, src, b, n):
-        self.recs["radius2"][b:b + n] = src[:n].numpy()
+        idx = self.view[b:b + n] if self.view is not None else np.arange(b, b + n)
+        self.recs["radius2"][idx] = src[:n].numpy()
 
     def final(self, emitted, b, n, out):
         img = self.orc.final(self.recs, emitted)
         out.copy_(torch.from_numpy(img[b:b + n]))
+
+    def final_view(self, emitted, b, n, out):
+        img = self.orc.final(self.recs, emitted)
+        out[:n] = torch.from_numpy(img[self.view[b:b + n]])
+
+    def record_view_list(self, out):
+        out.copy_(torch.from_numpy(self.view.astype(np.int32)))
 
 
 def _scene():
@@ -120,9 +140,15 @@ def _worker(rank, world, port, exchange, outdir):
     runner = PassRunner(eng, p, rank, world, exchange)
     for pass_index in range(2):
         runner.step(pass_index)
+    runner.flush()
     out = torch.zeros((runner.n_records, 3), dtype=torch.float32)
     runner.final_gather(float(runner.emitted_per_pass * 2), out)
-    np.save(os.path.join(outdir, f"recs{rank}.npy"), eng.recs[runner.rec_begin:runner.rec_begin + runner.rec_count])
+    if exchange == "reduce":   # PPM state is owned per chunk of the active-record view
+        owned = eng.view[runner.v_begin:runner.v_begin + runner.v_count]
+    else:                      # per contiguous record chunk
+        owned = np.arange(runner.rec_begin, runner.rec_begin + runner.rec_count)
+    np.save(os.path.join(outdir, f"idx{rank}.npy"), owned)
+    np.save(os.path.join(outdir, f"recs{rank}.npy"), eng.recs[owned])
     np.save(os.path.join(outdir, f"img{rank}.npy"), out.numpy())
     dist.barrier()
     dist.destroy_process_group()
@@ -152,8 +178,11 @@ def test_two_rank_pass_matches_single_process(exchange, tmp_path):
     mp.start_processes(_worker, args=(world, _free_port(), exchange, str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
     ref_recs, ref_img = _single_process_reference(world)
+    idx = np.concatenate([np.load(tmp_path / f"idx{r}.npy") for r in range(world)])
     recs = np.concatenate([np.load(tmp_path / f"recs{r}.npy") for r in range(world)]).view(RECORD_DTYPE)
-    assert len(recs) == len(ref_recs)
+    expect = np.nonzero((ref_recs["flags"] & 7) == 0)[0] if exchange == "reduce" else np.arange(len(ref_recs))
+    assert np.array_equal(np.sort(idx), expect)        # every record owned exactly once
+    ref_recs = ref_recs[idx]
     assert np.array_equal(recs["photon_count"], ref_recs["photon_count"])
     assert np.array_equal(recs["radius2"].view(np.uint32), ref_recs["radius2"].view(np.uint32))
     img = np.load(tmp_path / "img0.npy")

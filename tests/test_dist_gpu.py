@@ -1,0 +1,78 @@
+"""The multi-GPU pass runner (pmrender/dist.py) with the real HIP engine:
+two ranks share the one GPU of the test box and talk over gloo (RCCL needs
+one GPU per rank; the driver's 8-GPU bench uses it). Exercises the
+active-record view, the pipelined exchange, pm_final_view and the slot
+all-gather on the device, against one context over the same global paths —
+both exchanges are bit-exact (exact fixed-point sums, canonical buckets)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+PATHS, PASSES, W, H = 8192, 3, 64, 48
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, exchange, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "cuda-raytrace_amd")]
+    import torch  # noqa: F811  (before libpmhip: one HIP runtime)
+    from pmrender import hip, scenes
+    from pmrender.abi import RenderParams
+    from pmrender.dist import HipEngine, PassRunner
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctx = scenes.cornell_box(W, H).load_into(hip.Context(0))
+    p = RenderParams.defaults(paths_per_pass=PATHS, initial_radius2=25.0)
+    with torch.cuda.stream(torch.cuda.Stream()):
+        eng = HipEngine(ctx)
+        ctx.eye_pass(p, eng._s())
+        runner = PassRunner(eng, p, rank, world, exchange)
+        for k in range(PASSES):
+            runner.step(k)
+        out = torch.zeros((runner.n_records, 3), dtype=torch.float32, device="cuda")
+        runner.final_gather(float(runner.emitted_per_pass * PASSES), out)
+        torch.cuda.synchronize()
+    np.save(os.path.join(outdir, f"img{rank}.npy"), out.cpu().numpy())
+    ctx.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("exchange", ["reduce", "allgather"])
+def test_two_ranks_one_gpu_match_single_context(exchange, tmp_path, hip_mod):
+    from pmrender import scenes
+    from pmrender.abi import RenderParams
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), exchange, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    ref = scenes.cornell_box(W, H).load_into(hip_mod.Context(0))
+    p = RenderParams.defaults(paths_per_pass=world * PATHS, initial_radius2=25.0)
+    ref.eye_pass(p)
+    for k in range(PASSES):
+        ref.trace_photons(p, k, 0, world * PATHS)
+        ref.build_photon_map(p)
+        ref.gather(p)
+    n = ref.num_records()
+    img = torch.zeros((n, 3), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    ref.final(float(world * PATHS * PASSES), 0, n, img.data_ptr())
+    ref.synchronize()
+    want = img.cpu().numpy()
+    ref.close()
+    for r in range(world):
+        got = np.load(tmp_path / f"img{r}.npy")
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"rank {r} image differs"

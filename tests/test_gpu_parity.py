@@ -225,6 +225,73 @@ def test_sharded_reduce_exchange_bitexact(oracle_mod, hip_mod):
     assert_bitexact(got, ref.download_records(), "2-shard reduce exchange vs 1 context")
 
 
+def test_sharded_reduce_exchange_active_view(oracle_mod, hip_mod):
+    """Same emulated exchange over the active-record view (what PassRunner
+    moves across GPUs), ownership in view chunks, final radiance gathered per
+    view chunk and scattered through the view list: bit-identical records and
+    image to one context over all paths."""
+    torch = pytest.importorskip("torch")
+    sc = scenes.cornell_box(64, 48)
+    paths = 8192
+    p = RenderParams.defaults(paths_per_pass=paths)
+    pr = RenderParams.defaults(paths_per_pass=2 * paths)
+    ref = sc.load_into(hip_mod.Context(0))
+    ref.eye_pass(pr)
+    shards = [sc.load_into(hip_mod.Context(0)) for _ in range(2)]
+    for c in shards:
+        c.eye_pass(p)
+    nv = [c.set_record_view(True) for c in shards][0]
+    recs0 = ref.download_records()
+    active = np.nonzero((recs0["flags"] & 7) == 0)[0]
+    assert nv == len(active) and 0 < nv < len(recs0)
+    vl = torch.zeros(nv, dtype=torch.int32, device="cuda")
+    shards[0].record_view_list(vl.data_ptr())
+    shards[0].synchronize()
+    assert np.array_equal(vl.cpu().numpy(), active)
+    half = nv // 2
+    for pass_index in range(3):
+        ref.trace_photons(pr, pass_index, 0, 2 * paths)
+        ref.build_photon_map(pr)
+        ref.gather(pr)
+        parts = []
+        for rank, c in enumerate(shards):
+            c.trace_photons(p, pass_index, rank * paths, paths, rank * paths)
+            c.build_photon_map(p, paths * 4)
+            t = torch.zeros((nv, 4), dtype=torch.int64, device="cuda")
+            torch.cuda.synchronize()
+            c.gather_partial(p, t.data_ptr())
+            c.synchronize()
+            parts.append(t)
+        total = parts[0] + parts[1]
+        torch.cuda.synchronize()
+        r2 = torch.zeros(nv, dtype=torch.float32, device="cuda")
+        for rank, c in enumerate(shards):
+            b, cnt = (0, half) if rank == 0 else (half, nv - half)
+            c.ppm_update(p, total[b:].data_ptr(), b, cnt)
+            c.get_radius2(b, cnt, r2[b:].data_ptr())
+            c.synchronize()
+        for c in shards:
+            c.set_radius2(r2.data_ptr(), 0, nv)
+            c.synchronize()
+    want = ref.download_records()
+    got0, got1 = shards[0].download_records(), shards[1].download_records()
+    assert_bitexact(got0[active[:half]], want[active[:half]], "owned view chunk 0")
+    assert_bitexact(got1[active[half:]], want[active[half:]], "owned view chunk 1")
+    emitted = float(2 * paths * 3)
+    img = torch.zeros((nv, 3), dtype=torch.float32, device="cuda")
+    for rank, c in enumerate(shards):
+        b, cnt = (0, half) if rank == 0 else (half, nv - half)
+        c.final_view(emitted, b, cnt, img[b:].data_ptr())
+        c.synchronize()
+    full = torch.zeros((len(want), 3), dtype=torch.float32, device="cuda")
+    ref.final(emitted, 0, len(want), full.data_ptr())
+    ref.synchronize()
+    full = full.cpu().numpy()
+    assert np.array_equal(img.cpu().numpy().view(np.uint32), full[active].view(np.uint32))
+    inactive = np.setdiff1d(np.arange(len(want)), active)
+    assert not full[inactive].any()          # records outside the view are black
+
+
 @pytest.mark.parametrize("structure", [PM_GATHER_KDTREE, PM_GATHER_GRID])
 def test_render_parity_cornell(cornell, structure):
     ctx, orc = cornell
