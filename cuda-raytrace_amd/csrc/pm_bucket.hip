@@ -11,8 +11,9 @@
  *                      trace kernel already counted its deposits (fused
  *                      counting, pm_trace.hip: the atomics then overlap the
  *                      latency-bound trace instead of costing a pass).
- *   2. exclusive scan  of the ncells+1 counters (reduce / top / down kernels,
- *                      16-B vector loads) -> cell_start; cell_start[ncells] =
+ *   2. exclusive scan  of the ncells+1 counters (tile sums, then per tile:
+ *                      prefix of the earlier tile sums + local scan; 16-B
+ *                      vector loads) -> cell_start; cell_start[ncells] =
  *                      number of valid photons
  *   3. k_bucket_fill   slot -> cell_start[key] + rank, written straight into
  *                      the SoA arrays the gather streams (ph_a, ph_b, ph_c)
@@ -93,20 +94,6 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_reduce(const uint32_t *in, 
     if (threadIdx.x == 0) sums[blockIdx.x] = tot;
 }
 
-/* exclusive scan of the tile sums, one block, any count */
-__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_top(uint32_t *sums, int nt) {
-    __shared__ uint32_t lds[4];
-    uint32_t carry = 0;
-    for (int b = 0; b < nt; b += SCAN_BLOCK) {
-        const int i = b + threadIdx.x;
-        const uint32_t v = i < nt ? sums[i] : 0u;
-        uint32_t excl;
-        const uint32_t tot = block_excl_scan(v, &excl, lds);
-        if (i < nt) sums[i] = carry + excl;
-        carry += tot;
-    }
-}
-
 __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_down(const uint32_t *in, int64_t n, const uint32_t *sums,
                                                           uint32_t *out) {
     __shared__ uint32_t lds[4];
@@ -129,7 +116,14 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_down(const uint32_t *in, in
     for (int k = 0; k < SCAN_ITEMS; ++k) s += v[k];
     uint32_t excl;
     block_excl_scan(s, &excl, lds);
-    uint32_t run = sums[blockIdx.x] + excl;
+    /* this tile's offset: the sum of all earlier tile sums (a few hundred
+     * values, read by every block) — no separate scan of the sums, and no
+     * block ever waits on another */
+    uint32_t prev = 0;
+    for (int t = threadIdx.x; t < (int)blockIdx.x; t += SCAN_BLOCK) prev += sums[t];
+    uint32_t prev_excl;
+    prev = block_excl_scan(prev, &prev_excl, lds);
+    uint32_t run = prev + excl;
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; ++k) { uint32_t t = v[k]; v[k] = run; run += t; }
     if (full) {
@@ -165,7 +159,6 @@ hipError_t launch_exclusive_scan(const uint32_t *in, int64_t n, uint32_t *out, u
     if (n <= 0) return hipSuccess;
     const int ntile = (int)((n + SCAN_TILE - 1) / SCAN_TILE);
     hipLaunchKernelGGL(k_scan_reduce, dim3(ntile), dim3(SCAN_BLOCK), 0, s, in, n, sums);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_BLOCK), 0, s, sums, ntile);
     hipLaunchKernelGGL(k_scan_down, dim3(ntile), dim3(SCAN_BLOCK), 0, s, in, n, sums, out);
     return hipGetLastError();
 }
@@ -188,7 +181,6 @@ hipError_t launch_bucket_build(const pm_photon *slots, int64_t n, GridDesc g, ui
                            rank);
     const int ntile = (int)((nc + SCAN_TILE - 1) / SCAN_TILE);
     hipLaunchKernelGGL(k_scan_reduce, dim3(ntile), dim3(SCAN_BLOCK), 0, s, count, nc, sums);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_BLOCK), 0, s, sums, ntile);
     hipLaunchKernelGGL(k_scan_down, dim3(ntile), dim3(SCAN_BLOCK), 0, s, count, nc, sums, cell_start);
     if (n > 0)
         hipLaunchKernelGGL(k_bucket_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slots, n, key, rank,

@@ -54,7 +54,7 @@ PMD void write_partial(long long *p, int M, Fx3 L) {
  * d^2 < r^2 is inside the visited cells because the cell range is taken
  * over [p - r', p + r'] with r' slightly larger than sqrt(r^2). */
 template <int PARTIAL, int COUNT>
-__global__ __launch_bounds__(GATHER_BLOCK) void k_gather_grid(GatherParams P) {
+__global__ __launch_bounds__(GATHER_BLOCK, 8) void k_gather_grid(GatherParams P) { /* 8 waves/SIMD: latency bound */
     const int64_t r = P.rec_begin + (int64_t)blockIdx.x * GATHER_BLOCK + threadIdx.x;
     unsigned long long vis = 0, hits = 0, rows = 0, act = 0;
     if (r < P.rec_end) {
