@@ -135,6 +135,9 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         ctx.timing_reset()
+        # events only on the roofline kernel's stage inside the timed region:
+        # every timed stage boundary costs a few us of idle GPU
+        ctx.set_stage_timing("gather")
         t0 = time.perf_counter()
         for _ in range(args.steps):
             runner.step(0, reset=True)
@@ -146,13 +149,20 @@ def main():
             t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
+        gather_launches, gather_ms_total = ctx.timing_total("gather")
+        gather_ms = gather_ms_total / max(gather_launches, 1)
+        # per-stage split: a few more passes after the timed region, every stage timed
+        ctx.set_stage_timing("all")
+        ctx.timing_reset()
+        for _ in range(min(args.steps, 10)):
+            runner.step(0, reset=True)
+        runner.flush()
+        torch.cuda.synchronize()
         stages = {}
         for name in ("reset", "trace", "build", "gather", "update"):
             n, ms = ctx.timing_total(name)
             if n:
                 stages[name] = round(ms / n, 5)
-        gather_launches, gather_ms_total = ctx.timing_total("gather")
-        gather_ms = gather_ms_total / max(gather_launches, 1)
 
         census = canonical = tcensus = None
         if not args.no_census:
@@ -266,7 +276,7 @@ def main():
         "mgather_samples_per_s": round(g_points * args.steps / elapsed / 1e6, 3),
         "kernel_rates": {
             "trace_mphotons_per_s": round(args.paths / (stages["trace"] * 1e-3) / 1e6, 2) if "trace" in stages else None,
-            "gather_msamples_per_s": round(g_points / (gather_ms * 1e-3) / 1e6, 2),
+            "gather_msamples_per_s": round(g_points / (gather_ms * 1e-3) / 1e6, 2) if gather_ms > 0 else None,
         },
         "stages_ms": stages,
         "setup_s": round(setup_s, 3),

@@ -103,6 +103,16 @@ struct Ctx {
     int64_t trace_wave_paths = 64; /* per-lane kernel: paths per wave (env PM_TRACE_WAVE_PATHS) */
     int trace_refill_min = 32;     /* per-lane kernel: idle lanes that trigger a refill (env PM_TRACE_REFILL_MIN) */
     bool fuse_count = true;        /* bucket counting inside the trace kernel (env PM_FUSE_COUNT=0 disables) */
+    /* leading words of d_count known to be zero (the bucket scan clears the
+     * counters it reads); valid while d_count.p == count_zero_ptr */
+    size_t count_zero_words = 0;
+    void *count_zero_ptr = nullptr;
+    /* stages that get event pairs: "all", "" (none) or a comma list
+     * (pm_set_stage_timing; env PM_STAGE_TIMERS=0 starts with none) */
+    std::string timed_stages = "all";
+    bool stage_active = false;
+    StageEvents stage;             /* the stage being timed (g_stage points here) */
+    bool stage_marker = false;
     std::map<std::string, TimerPool> timers;
 };
 
@@ -112,6 +122,7 @@ struct Ctx {
         snprintf(_b, sizeof(_b), __VA_ARGS__);                                 \
         if (c) (c)->err = _b;                                                  \
         g_last_error = _b;                                                     \
+        pm::g_stage = nullptr; /* an error inside a timed stage ends it */    \
         return code;                                                           \
     } while (0)
 
@@ -128,22 +139,57 @@ struct Ctx {
 
 hipStream_t pick(Ctx *c, void *s) { return s ? (hipStream_t)s : c->stream; }
 
-/* Every stage launch records a fresh event pair from a per-stage pool, on the
- * stream the kernels run on; nothing synchronizes until a reader asks. */
-int timer_begin(Ctx *c, const char *name, hipStream_t s) {
+} // namespace
+thread_local pm::StageEvents *pm::g_stage = nullptr;
+namespace {
+
+/* Every stage launch takes a fresh event pair from a per-stage pool. Kernel
+ * stages bind the pair to their own dispatches (pm_launch, pm_kernels.h):
+ * no marker packets, so timing leaves no idle gap between kernels. A stage
+ * of host work / copies (marker = true) records the pair as markers.
+ * Nothing synchronizes until a reader asks. */
+bool stage_timed(const Ctx *c, const char *name) {
+    const std::string &t = c->timed_stages;
+    if (t == "all") return true;
+    const size_t n = strlen(name);
+    for (size_t i = 0; i < t.size();) {
+        size_t j = t.find(',', i);
+        if (j == std::string::npos) j = t.size();
+        if (j - i == n && t.compare(i, n, name) == 0) return true;
+        i = j + 1;
+    }
+    return false;
+}
+int timer_begin(Ctx *c, const char *name, hipStream_t s, bool marker = false) {
+    c->stage_active = stage_timed(c, name);
+    if (!c->stage_active) return 0;
     TimerPool &tp = c->timers[name];
     if (tp.used == tp.ev.size()) {
         Timer t;
-        (void)hipEventCreate(&t.a);
-        (void)hipEventCreate(&t.b);
+        /* timing-only events: no system-scope fence (cache write-back +
+         * invalidate) when recorded */
+        (void)hipEventCreateWithFlags(&t.a, hipEventDisableSystemFence);
+        (void)hipEventCreateWithFlags(&t.b, hipEventDisableSystemFence);
         tp.ev.push_back(t);
     }
-    (void)hipEventRecord(tp.ev[tp.used].a, s);
+    const Timer &t = tp.ev[tp.used];
+    c->stage = StageEvents{t.a, t.b, 0};
+    c->stage_marker = marker;
+    if (marker) {
+        (void)hipEventRecord(t.a, s);
+        c->stage.launched = 1; /* start taken: kernels only move the stop */
+    }
+    g_stage = &c->stage;
     return 0;
 }
 void timer_end(Ctx *c, const char *name, hipStream_t s) {
+    if (!c->stage_active) return;
+    c->stage_active = false;
+    g_stage = nullptr;
     TimerPool &tp = c->timers[name];
-    (void)hipEventRecord(tp.ev[tp.used].b, s);
+    const Timer &t = tp.ev[tp.used];
+    if (c->stage.launched == 0) (void)hipEventRecord(t.a, s); /* nothing launched: an empty interval */
+    if (c->stage_marker || c->stage.launched == 0) (void)hipEventRecord(t.b, s);
     tp.used++;
 }
 double pair_ms(const Timer &t) {
@@ -350,6 +396,7 @@ int pm_create(void **out, const pm_config *cfg) {
     if (const char *e = getenv("PM_TRACE_WAVE_PATHS")) c->trace_wave_paths = std::max(64LL, atoll(e));
     if (const char *e = getenv("PM_TRACE_REFILL_MIN")) c->trace_refill_min = std::max(1, std::min(64, atoi(e)));
     if (const char *e = getenv("PM_FUSE_COUNT")) c->fuse_count = atoi(e) != 0;
+    if (const char *e = getenv("PM_STAGE_TIMERS")) if (atoi(e) == 0) c->timed_stages.clear();
     (void)hipSetDevice(dev);
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -770,6 +817,15 @@ static GridDesc make_grid(const Ctx *c, const pm_render_params *p) {
 
 static bool same_grid(const GridDesc &a, const GridDesc &b) { return std::memcmp(&a, &b, sizeof(GridDesc)) == 0; }
 
+/* make the first `words` bucket counters zero (a memset only when the last
+ * bucket scan did not already leave them cleared) */
+static hipError_t count_zeroed(Ctx *c, size_t words, hipStream_t s) {
+    if (c->count_zero_ptr == c->d_count.p && c->count_zero_words >= words) return hipSuccess;
+    hipError_t e = hipMemsetAsync(c->d_count.p, 0, words * 4, s);
+    if (e == hipSuccess) { c->count_zero_words = words; c->count_zero_ptr = c->d_count.p; }
+    return e;
+}
+
 int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t path_begin, int64_t path_count,
                      int64_t slot_path_base, void *stream) {
     GETCTX(ptr);
@@ -804,7 +860,7 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
         const GridDesc g = make_grid(c, p);
         HIPCHK(c, c->d_count.ensure(((size_t)g.ncells + 1) * 4));
         HIPCHK(c, c->d_scratch.ensure(bucket_scratch_words(end_slot, g.ncells) * 4));
-        HIPCHK(c, hipMemsetAsync(c->d_count.p, 0, ((size_t)g.ncells + 1) * 4, s));
+        HIPCHK(c, count_zeroed(c, (size_t)g.ncells + 1, s));
         T.bucket = 1;
         T.grid = g;
         T.count = c->d_count.as<uint32_t>();
@@ -815,7 +871,7 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
     /* the kernel writes all path_count * mpc slots: deposits, then zeros */
     HIPCHK(c, launch_trace(T, c->counting, s));
     timer_end(c, "trace", s);
-    if (fuse) { c->fused.valid = true; c->fused.n = end_slot; c->fused.grid = T.grid; }
+    if (fuse) { c->fused.valid = true; c->fused.n = end_slot; c->fused.grid = T.grid; c->count_zero_words = 0; }
     c->slots_used = std::max(c->slots_used, end_slot);
     return PM_OK;
 }
@@ -830,7 +886,7 @@ int pm_build_photon_map(void *ptr, const pm_render_params *p, int64_t n_slots, v
     c->map_slots = n_slots;
     if (p->gather_structure == PM_GATHER_KDTREE) {
         /* reference path (CreatePhotonMap): DtoH, CPU pbrt KdTree, HtoD */
-        timer_begin(c, "build", s);
+        timer_begin(c, "build", s, true);
         std::vector<pm_photon> h((size_t)n_slots), nodes;
         HIPCHK(c, hipMemcpyAsync(h.data(), c->d_slots.p, n_slots * sizeof(pm_photon), hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
@@ -853,12 +909,18 @@ int pm_build_photon_map(void *ptr, const pm_render_params *p, int64_t n_slots, v
     const size_t n = (size_t)n_slots;
     HIPCHK(c, c->d_count.ensure(((size_t)g.ncells + 1) * 4));
     HIPCHK(c, c->d_cell_start.ensure(((size_t)g.ncells + 1) * 4));
-    if (!counted) HIPCHK(c, c->d_scratch.ensure(bucket_scratch_words(n_slots, g.ncells) * 4));
+    if (!counted) {
+        HIPCHK(c, c->d_scratch.ensure(bucket_scratch_words(n_slots, g.ncells) * 4));
+        HIPCHK(c, count_zeroed(c, (size_t)g.ncells + 1, s));
+    }
     HIPCHK(c, c->d_pha.ensure(n * 16)); HIPCHK(c, c->d_phb.ensure(n * 16)); HIPCHK(c, c->d_phc.ensure(n * 4));
     timer_begin(c, "build", s);
     HIPCHK(c, launch_bucket_build(c->d_slots.as<pm_photon>(), n_slots, g, c->d_count.as<uint32_t>(),
                                   c->d_cell_start.as<uint32_t>(), c->d_scratch.as<uint32_t>(), c->d_pha.as<float4>(),
                                   c->d_phb.as<float4>(), c->d_phc.as<float>(), counted, s));
+    /* the scan left the counters zeroed */
+    c->count_zero_words = (size_t)g.ncells + 1;
+    c->count_zero_ptr = c->d_count.p;
     timer_end(c, "build", s);
     c->map_kind = PM_GATHER_GRID;
     return PM_OK;
@@ -1193,6 +1255,13 @@ int pm_set_record_view(void *ptr, int active_only, int64_t *n_view) {
 int pm_set_counting(void *ptr, int enabled) {
     GETCTX(ptr);
     c->counting = enabled != 0;
+    return PM_OK;
+}
+
+int pm_set_stage_timing(void *ptr, const char *stages) {
+    GETCTX(ptr);
+    if (c->stage_active) FAIL(c, PM_ERR_INVALID, "stage timing changed inside a stage");
+    c->timed_stages = stages ? stages : "";
     return PM_OK;
 }
 

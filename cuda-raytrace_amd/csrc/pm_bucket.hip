@@ -14,7 +14,8 @@
  *   2. exclusive scan  of the ncells+1 counters (tile sums, then per tile:
  *                      prefix of the earlier tile sums + local scan; 16-B
  *                      vector loads) -> cell_start; cell_start[ncells] =
- *                      number of valid photons
+ *                      number of valid photons. The counters are zeroed as
+ *                      they are read, so the next pass needs no memset.
  *   3. k_bucket_fill   slot -> cell_start[key] + rank, written straight into
  *                      the SoA arrays the gather streams (ph_a, ph_b, ph_c)
  * The order inside a bucket depends on atomic arrival order. Results do not:
@@ -94,8 +95,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_reduce(const uint32_t *in, 
     if (threadIdx.x == 0) sums[blockIdx.x] = tot;
 }
 
+/* clear != nullptr: the tile of `in` is zeroed after it is read (the bucket
+ * counters then start the next pass at zero without a memset launch) */
 __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_down(const uint32_t *in, int64_t n, const uint32_t *sums,
-                                                          uint32_t *out) {
+                                                          uint32_t *out, uint32_t *clear) {
     __shared__ uint32_t lds[4];
     const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
     uint32_t v[SCAN_ITEMS];
@@ -110,6 +113,15 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_down(const uint32_t *in, in
     } else {
 #pragma unroll
         for (int k = 0; k < SCAN_ITEMS; ++k) v[k] = (base + k < n) ? in[base + k] : 0u;
+    }
+    if (clear) {
+        if (full) {
+            uint4 *p = reinterpret_cast<uint4 *>(clear + base);
+#pragma unroll
+            for (int k = 0; k < SCAN_ITEMS / 4; ++k) p[k] = make_uint4(0u, 0u, 0u, 0u);
+        } else {
+            for (int64_t k = base; k < n; ++k) clear[k] = 0u;
+        }
     }
     uint32_t s = 0;
 #pragma unroll
@@ -152,14 +164,19 @@ __global__ __launch_bounds__(256) void k_bucket_fill(const pm_photon *slots, int
     ph_b[dst] = make_float4(c.x, c.y, d.x, e.x);
     ph_c[dst] = e.y;
 }
+/* Measured (PMC WRITE_SIZE): ~55 MB written per launch for ~20 MB of photon
+ * data — the scattered 16-B stores cost whole-line write-backs. Giving each
+ * XCD its own contiguous destination window (blocks b, b+8 share an XCD;
+ * eight equal-photon key ranges from the scan) left the write bytes at
+ * ~58 MB and read every key 8x: 41 us vs 29 us, so not used. */
 
 size_t scan_scratch_words(int64_t n) { return (size_t)((n + SCAN_TILE - 1) / SCAN_TILE) + 16; }
 
 hipError_t launch_exclusive_scan(const uint32_t *in, int64_t n, uint32_t *out, uint32_t *sums, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const int ntile = (int)((n + SCAN_TILE - 1) / SCAN_TILE);
-    hipLaunchKernelGGL(k_scan_reduce, dim3(ntile), dim3(SCAN_BLOCK), 0, s, in, n, sums);
-    hipLaunchKernelGGL(k_scan_down, dim3(ntile), dim3(SCAN_BLOCK), 0, s, in, n, sums, out);
+    pm_launch(k_scan_reduce, dim3(ntile), dim3(SCAN_BLOCK), 0, s, in, n, sums);
+    pm_launch(k_scan_down, dim3(ntile), dim3(SCAN_BLOCK), 0, s, in, n, sums, out, nullptr);
     return hipGetLastError();
 }
 
@@ -172,18 +189,15 @@ hipError_t launch_bucket_build(const pm_photon *slots, int64_t n, GridDesc g, ui
                                uint32_t *scratch, float4 *ph_a, float4 *ph_b, float *ph_c, bool counted, hipStream_t s) {
     const int64_t nc = (int64_t)g.ncells + 1; /* last counter stays 0 -> cell_start[ncells] = total */
     uint32_t *key = scratch, *rank = scratch + n, *sums = scratch + 2 * n;
-    if (!counted) {
-        hipError_t e = hipMemsetAsync(count, 0, (size_t)nc * 4, s);
-        if (e != hipSuccess) return e;
-    }
     if (n > 0 && !counted)
-        hipLaunchKernelGGL(k_bucket_count, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slots, n, g, count, key,
+        pm_launch(k_bucket_count, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slots, n, g, count, key,
                            rank);
     const int ntile = (int)((nc + SCAN_TILE - 1) / SCAN_TILE);
-    hipLaunchKernelGGL(k_scan_reduce, dim3(ntile), dim3(SCAN_BLOCK), 0, s, count, nc, sums);
-    hipLaunchKernelGGL(k_scan_down, dim3(ntile), dim3(SCAN_BLOCK), 0, s, count, nc, sums, cell_start);
+    pm_launch(k_scan_reduce, dim3(ntile), dim3(SCAN_BLOCK), 0, s, count, nc, sums);
+    /* the counters are zeroed as they are scanned: ready for the next pass */
+    pm_launch(k_scan_down, dim3(ntile), dim3(SCAN_BLOCK), 0, s, count, nc, sums, cell_start, count);
     if (n > 0)
-        hipLaunchKernelGGL(k_bucket_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slots, n, key, rank,
+        pm_launch(k_bucket_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slots, n, key, rank,
                            cell_start, ph_a, ph_b, ph_c);
     return hipGetLastError();
 }

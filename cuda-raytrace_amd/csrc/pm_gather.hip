@@ -215,9 +215,9 @@ template <int STRUCT, int PARTIAL, int COUNT>
 static void launch_g(const GatherParams &p, hipStream_t s) {
     unsigned grid = (unsigned)((p.rec_end - p.rec_begin + GATHER_BLOCK - 1) / GATHER_BLOCK);
     if (STRUCT == PM_GATHER_GRID)
-        hipLaunchKernelGGL((k_gather_grid<PARTIAL, COUNT>), dim3(grid), dim3(GATHER_BLOCK), 0, s, p);
+        pm_launch((k_gather_grid<PARTIAL, COUNT>), dim3(grid), dim3(GATHER_BLOCK), 0, s, p);
     else
-        hipLaunchKernelGGL((k_gather_kd<PARTIAL, COUNT>), dim3(grid), dim3(GATHER_BLOCK), 0, s, p);
+        pm_launch((k_gather_kd<PARTIAL, COUNT>), dim3(grid), dim3(GATHER_BLOCK), 0, s, p);
 }
 
 hipError_t launch_gather(const GatherParams &p, int structure, int partial, int count, hipStream_t s) {
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256) void k_radius2_io(RecordsDev R, float *buf, in
 hipError_t launch_radius2_io(const RecordsDev &R, float *buf, int64_t rec_begin, int64_t rec_count, int to_records,
                              const uint32_t *view, hipStream_t s) {
     if (rec_count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_radius2_io, dim3((unsigned)((rec_count + 255) / 256)), dim3(256), 0, s, R, buf, rec_begin,
+    pm_launch(k_radius2_io, dim3((unsigned)((rec_count + 255) / 256)), dim3(256), 0, s, R, buf, rec_begin,
                        rec_count, to_records, view);
     return hipGetLastError();
 }
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(256) void k_ppm_update(RecordsDev R, const long lon
 hipError_t launch_ppm_update(const GatherParams &p, const long long *partial, int64_t rec_begin, int64_t rec_count,
                              hipStream_t s) {
     if (rec_count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_ppm_update, dim3((unsigned)((rec_count + 255) / 256)), dim3(256), 0, s, p.R, partial,
+    pm_launch(k_ppm_update, dim3((unsigned)((rec_count + 255) / 256)), dim3(256), 0, s, p.R, partial,
                        rec_begin, rec_count, p.ppm_alpha, p.fx_inv, p.view_list);
     return hipGetLastError();
 }
@@ -306,10 +306,10 @@ __global__ __launch_bounds__(256) void k_view_list(RecordsDev R, const uint32_t 
 hipError_t launch_record_view(const RecordsDev &R, uint32_t *flags, uint32_t *rank, uint32_t *list, uint32_t *sums,
                               hipStream_t s) {
     const int64_t n = R.count;
-    hipLaunchKernelGGL(k_view_flags, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, s, R, flags);
+    pm_launch(k_view_flags, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, s, R, flags);
     hipError_t e = launch_exclusive_scan(flags, n + 1, rank, sums, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_view_list, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, R, flags, rank, list);
+    pm_launch(k_view_list, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, R, flags, rank, list);
     return hipGetLastError();
 }
 
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(256) void k_final(FinalParams P) {
 
 hipError_t launch_final(const FinalParams &p, hipStream_t s) {
     if (p.rec_count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_final, dim3((unsigned)((p.rec_count + 255) / 256)), dim3(256), 0, s, p);
+    pm_launch(k_final, dim3((unsigned)((p.rec_count + 255) / 256)), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
@@ -365,7 +365,7 @@ __global__ __launch_bounds__(256) void k_reset_records(RecordsDev R, float r2ini
 
 hipError_t launch_reset_records(const RecordsDev &R, float r2init, hipStream_t s) {
     if (R.count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_reset_records, dim3((unsigned)((R.count + 255) / 256)), dim3(256), 0, s, R, r2init);
+    pm_launch(k_reset_records, dim3((unsigned)((R.count + 255) / 256)), dim3(256), 0, s, R, r2init);
     return hipGetLastError();
 }
 

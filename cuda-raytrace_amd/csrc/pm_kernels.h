@@ -3,12 +3,33 @@
  * the host orchestration (pm_api.cpp) and the HIP kernels (pm_trace.hip, pm_bucket.hip, pm_gather.hip).
  */
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "pm_device.h"
 
 namespace pm {
+
+/* Stage timing without marker packets: the API (pm_api.cpp timer_begin /
+ * timer_end) points g_stage at an event pair around one stage, and every
+ * launch in the stage goes through pm_launch, which binds the start event to
+ * the stage's first dispatch and the stop event to each dispatch (the last
+ * one wins) — the timestamps come from the kernel dispatches themselves, so
+ * timing adds no idle gap between kernels. */
+struct StageEvents { hipEvent_t start = nullptr, stop = nullptr; int launched = 0; };
+extern thread_local StageEvents *g_stage;
+
+template <typename F, typename... Args>
+inline void pm_launch(F kernel, dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, Args... args) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (StageEvents *st = g_stage) {
+        a = st->launched ? nullptr : st->start;
+        b = st->stop;
+        st->launched++;
+    }
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, a, b, 0u, args...);
+}
 
 constexpr int EYE_BLOCK = 128;     /* traversal kernels: LDS stack column per lane */
 constexpr int TRACE_BLOCK = 256;    /* k_trace: 4 waves compact paths together */
@@ -121,7 +142,8 @@ hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s);
 /* photon-bucket build (pm_bucket.hip): count + rank, scan, fill.
  * count and cell_start have ncells + 1 entries; cell_start[ncells] = valid
  * photons; scratch holds bucket_scratch_words() uint32: key[n], rank[n], ...
- * counted: key/rank/count were produced by the trace kernel (TraceParams::bucket) */
+ * counted: key/rank/count were produced by the trace kernel (TraceParams::bucket);
+ * otherwise count must arrive zeroed. count leaves zeroed (cleared by the scan). */
 size_t bucket_scratch_words(int64_t n_slots, uint32_t ncells);
 hipError_t launch_bucket_build(const pm_photon *slots, int64_t n, GridDesc g, uint32_t *count, uint32_t *cell_start,
                                uint32_t *scratch, float4 *ph_a, float4 *ph_b, float *ph_c, bool counted, hipStream_t s);

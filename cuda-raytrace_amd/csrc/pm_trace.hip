@@ -130,9 +130,9 @@ hipError_t launch_eye(const EyeParams &p, hipStream_t s) {
     unsigned grid = (unsigned)((p.R.count + EYE_BLOCK - 1) / EYE_BLOCK);
     const size_t lds = (size_t)p.S.stack_depth * EYE_BLOCK * 4 + p.S.lds_bytes;
     switch (scene_mode(p.S)) {
-    case MODE_BRUTE: hipLaunchKernelGGL(k_eye<MODE_BRUTE>, dim3(grid), dim3(EYE_BLOCK), lds, s, p); break;
-    case MODE_LDS: hipLaunchKernelGGL(k_eye<MODE_LDS>, dim3(grid), dim3(EYE_BLOCK), lds, s, p); break;
-    default: hipLaunchKernelGGL(k_eye<MODE_GLOBAL>, dim3(grid), dim3(EYE_BLOCK), lds, s, p); break;
+    case MODE_BRUTE: pm_launch(k_eye<MODE_BRUTE>, dim3(grid), dim3(EYE_BLOCK), lds, s, p); break;
+    case MODE_LDS: pm_launch(k_eye<MODE_LDS>, dim3(grid), dim3(EYE_BLOCK), lds, s, p); break;
+    default: pm_launch(k_eye<MODE_GLOBAL>, dim3(grid), dim3(EYE_BLOCK), lds, s, p); break;
     }
     return hipGetLastError();
 }
@@ -432,16 +432,16 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
 #define PM_LAUNCH_MODES(KERNEL, GRID, BLOCK, LDS, STREAM, PARAMS, COUNT)                                        \
     switch (scene_mode((PARAMS).S)) {                                                                            \
     case MODE_BRUTE:                                                                                             \
-        if (COUNT) hipLaunchKernelGGL((KERNEL<1, MODE_BRUTE>), GRID, BLOCK, LDS, STREAM, PARAMS);                \
-        else hipLaunchKernelGGL((KERNEL<0, MODE_BRUTE>), GRID, BLOCK, LDS, STREAM, PARAMS);                      \
+        if (COUNT) pm_launch((KERNEL<1, MODE_BRUTE>), GRID, BLOCK, LDS, STREAM, PARAMS);                \
+        else pm_launch((KERNEL<0, MODE_BRUTE>), GRID, BLOCK, LDS, STREAM, PARAMS);                      \
         break;                                                                                                   \
     case MODE_LDS:                                                                                               \
-        if (COUNT) hipLaunchKernelGGL((KERNEL<1, MODE_LDS>), GRID, BLOCK, LDS, STREAM, PARAMS);                  \
-        else hipLaunchKernelGGL((KERNEL<0, MODE_LDS>), GRID, BLOCK, LDS, STREAM, PARAMS);                        \
+        if (COUNT) pm_launch((KERNEL<1, MODE_LDS>), GRID, BLOCK, LDS, STREAM, PARAMS);                  \
+        else pm_launch((KERNEL<0, MODE_LDS>), GRID, BLOCK, LDS, STREAM, PARAMS);                        \
         break;                                                                                                   \
     default:                                                                                                     \
-        if (COUNT) hipLaunchKernelGGL((KERNEL<1, MODE_GLOBAL>), GRID, BLOCK, LDS, STREAM, PARAMS);               \
-        else hipLaunchKernelGGL((KERNEL<0, MODE_GLOBAL>), GRID, BLOCK, LDS, STREAM, PARAMS);                     \
+        if (COUNT) pm_launch((KERNEL<1, MODE_GLOBAL>), GRID, BLOCK, LDS, STREAM, PARAMS);               \
+        else pm_launch((KERNEL<0, MODE_GLOBAL>), GRID, BLOCK, LDS, STREAM, PARAMS);                     \
         break;                                                                                                   \
     }
 

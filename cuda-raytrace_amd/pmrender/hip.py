@@ -75,6 +75,7 @@ def load_library(path=None):
         "pm_trace_counters": (c_int, [vp, ctypes.POINTER(i64)]),
         "pm_trace_profile": (c_int, [vp, ctypes.POINTER(i64), c_int]),
         "pm_set_counting": (c_int, [vp, c_int]),
+        "pm_set_stage_timing": (c_int, [vp, ctypes.c_char_p]),
         "pm_set_record_view": (c_int, [vp, c_int, ctypes.POINTER(i64)]),
         "pm_final_view": (c_int, [vp, c_double, i64, i64, vp, vp]),
         "pm_record_view_list": (c_int, [vp, vp, vp]),
@@ -311,6 +312,10 @@ class Context:
 
     def record_view_list(self, d_out, stream=None):
         self._chk(self.lib.pm_record_view_list(self.h, ctypes.c_void_p(d_out), stream))
+
+    def set_stage_timing(self, stages="all"):
+        """Stages that record HIP events: "all", "" (none) or e.g. "gather"."""
+        self._chk(self.lib.pm_set_stage_timing(self.h, (stages or "").encode()))
 
     def set_counting(self, enabled=True):
         self._chk(self.lib.pm_set_counting(self.h, int(bool(enabled))))

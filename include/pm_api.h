@@ -258,6 +258,10 @@ int pm_synchronize(void *ctx);
  * "reset". last = most recent launch; total = sum over launches since
  * pm_timing_reset (synchronizes on the last event only when read). */
 int pm_last_kernel_ms(void *ctx, const char *name, double *ms);
+/* Which stages record events: "all" (default), "" / NULL (none) or a comma
+ * list ("gather"). Each timed stage boundary costs a few us of GPU idle
+ * time, so a throughput run times only the stage it reports on. */
+int pm_set_stage_timing(void *ctx, const char *stages);
 int pm_timing_reset(void *ctx);
 int pm_timing_total(void *ctx, const char *name, int64_t *count, double *total_ms);
 /* Restores every active record to the eye pass's initial PPM state
