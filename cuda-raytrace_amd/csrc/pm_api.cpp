@@ -637,22 +637,38 @@ int pm_commit(void *ptr) {
     c->bvh_depth = bvh.depth;
     if (bvh.depth >= BVH_STACK) FAIL(c, PM_ERR_INVALID, "BVH too deep (%d)", bvh.depth);
 
-    /* triangles in leaf order; per-triangle precomputed (p0, e0, e1, n) for the
-     * intersector and the normalized shading frame for hits */
+    /* tiny LDS scenes skip the BVH (MODE_BRUTE); env PM_TRACE_BRUTE_MAX
+     * overrides the limit (0 = never). Their triangles are stored in global-id
+     * order (brute_isect's tie-break relies on it), others in leaf order. */
+    const char *brute_env = getenv("PM_TRACE_BRUTE_MAX");
+    const int brute_max = brute_env ? atoi(brute_env) : BRUTE_MAX_PRIMS;
+    const bool id_order = (int64_t)bvh.refs.size() <= brute_max;
+    std::vector<uint32_t> tri_order; /* triangle ids in storage order */
+    tri_order.reserve(nt);
+    if (id_order) {
+        for (int64_t t = 0; t < nt; ++t) tri_order.push_back((uint32_t)t);
+    } else {
+        for (uint32_t ref : bvh.refs)
+            if ((ref >> 30) == PRIM_TRI) tri_order.push_back(ref & 0x3fffffffu);
+    }
+    std::vector<uint32_t> slot_of(nt);
+    for (size_t k = 0; k < tri_order.size(); ++k) slot_of[tri_order[k]] = (uint32_t)k;
+    for (uint32_t &ref : bvh.refs)
+        if ((ref >> 30) == PRIM_TRI) ref = (PRIM_TRI << 30) | slot_of[ref & 0x3fffffffu];
+
+    /* per-triangle precomputed (p0, e0, e1, n) for the intersector and the
+     * normalized shading frame for hits */
     std::vector<float4> tri_geo, tri_shade;
     std::vector<int4> tri_info;
     std::vector<uint32_t> tri_id;
     tri_geo.reserve(3 * nt); tri_shade.reserve(2 * nt); tri_info.reserve(nt); tri_id.reserve(nt);
-    for (uint32_t &ref : bvh.refs) {
-        if ((ref >> 30) != PRIM_TRI) continue;
-        uint32_t t = ref & 0x3fffffffu;
+    for (uint32_t t : tri_order) {
         const HTri &tr = c->tris[t];
         const HMesh &m = c->meshes[tr.mesh];
         const float *p0 = V + 3 * tr.v[0], *p1 = V + 3 * tr.v[1], *p2 = V + 3 * tr.v[2];
         float e0[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
         float e1[3] = {p0[0] - p2[0], p0[1] - p2[1], p0[2] - p2[2]};
         float n[3] = {e1[1] * e0[2] - e1[2] * e0[1], e1[2] * e0[0] - e1[0] * e0[2], e1[0] * e0[1] - e1[1] * e0[0]};
-        uint32_t k = (uint32_t)tri_info.size();
         tri_geo.push_back(f4(p0[0], p0[1], p0[2], e0[0]));
         tri_geo.push_back(f4(e0[1], e0[2], e1[0], e1[1]));
         tri_geo.push_back(f4(e1[2], n[0], n[1], n[2]));
@@ -662,7 +678,6 @@ int pm_commit(void *ptr) {
         tri_shade.push_back(f4(dpdu[0], dpdu[1], dpdu[2], bits_f((uint32_t)m.light)));
         tri_info.push_back(make_int4(tr.v[0], tr.v[1], tr.v[2], tr.mesh));
         tri_id.push_back(t);
-        ref = (PRIM_TRI << 30) | k;
     }
     std::vector<float4> norms(c->N.size() / 3);
     for (size_t i = 0; i < norms.size(); ++i) norms[i] = f4(c->N[3 * i], c->N[3 * i + 1], c->N[3 * i + 2], 0.f);
@@ -708,12 +723,7 @@ int pm_commit(void *ptr) {
     S.n_refs = (int)bvh.refs.size();
     S.n_tris = (int)tri_info.size(); S.n_disks = (int)nd; S.n_spheres = (int)ns;
     S.tri_geo_g = S.tri_geo; S.tri_id_g = S.tri_id;
-    {
-        /* tiny LDS scenes skip the BVH (MODE_BRUTE); env PM_TRACE_BRUTE_MAX overrides the limit (0 = never) */
-        const char *e = getenv("PM_TRACE_BRUTE_MAX");
-        const int brute_max = e ? atoi(e) : BRUTE_MAX_PRIMS;
-        S.brute = (S.lds_bytes > 0 && S.n_refs <= brute_max) ? 1 : 0;
-    }
+    S.brute = (S.lds_bytes > 0 && id_order) ? 1 : 0;
     /* a push happens only when descending a level, so depth + 1 entries suffice;
      * sizing the LDS stack by the actual tree keeps occupancy VGPR-bound */
     S.stack_depth = std::min(BVH_STACK, std::max(2, c->bvh_depth + 2));

@@ -31,10 +31,21 @@ PMD v3 operator*(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
 PMD v3 operator*(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
 PMD v3 operator*(float s, v3 a) { return mk(s * a.x, s * a.y, s * a.z); }
 /* OptiX float3 / float multiplies by the reciprocal */
-PMD v3 operator/(v3 a, float s) { float inv = 1.0f / s; return a * inv; }
+/* IEEE correctly rounded 1/x in 3 instructions instead of the ~10 of the
+ * scaled division sequence: one FMA Newton step on v_rcp_f32. Checked bit for
+ * bit against 1.0f / x for every float with 2^-125 <= |x| < 2^125
+ * (tools/rcp_exhaustive.hip: 0 mismatches on gfx950); other inputs (zero,
+ * denormal, huge, inf, nan) take the full division. */
+PMD float rcp_exact(float x) {
+    const float r0 = __builtin_amdgcn_rcpf(x);
+    float r = __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
+    if (__builtin_expect(((__float_as_uint(x) >> 23) & 0xffu) - 2u > 249u, 0)) r = 1.0f / x;
+    return r;
+}
+PMD v3 operator/(v3 a, float s) { float inv = rcp_exact(s); return a * inv; }
 PMD float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 PMD v3 cross(v3 a, v3 b) { return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
-PMD v3 normalize(v3 v) { float inv = 1.0f / sqrtf(dot(v, v)); return v * inv; }
+PMD v3 normalize(v3 v) { float inv = rcp_exact(sqrtf(dot(v, v))); return v * inv; }
 PMD float absdot(v3 a, v3 b) { return fabsf(dot(a, b)); }
 PMD bool is_black(v3 s) { return s.x == 0.0f && s.y == 0.0f && s.z == 0.0f; }
 PMD v3 xyz(float4 a) { return mk(a.x, a.y, a.z); }
@@ -196,7 +207,7 @@ PMD void permuted_halton4(uint32_t n, const uint32_t *p, float out[4]) {
 PMD bool isect_tri_v(const float4 a, const float4 b, const float4 c, const Ray &ray, float *t, float *beta,
                      float *gamma) {
     v3 p0 = mk(a.x, a.y, a.z), e0 = mk(a.w, b.x, b.y), e1 = mk(b.z, b.w, c.x), n = mk(c.y, c.z, c.w);
-    const v3 e2 = (1.0f / dot(n, ray.d)) * (p0 - ray.o);
+    const v3 e2 = rcp_exact(dot(n, ray.d)) * (p0 - ray.o);
     const v3 i = cross(ray.d, e2);
     *beta = dot(i, e1);
     *gamma = dot(i, e0);
@@ -340,16 +351,24 @@ PMD f2 bc2(float x) { return f2{x, x}; }
 /* isect_tri_v for two triangles at once (packed v_pk_mul/add_f32): the same
  * per-component IEEE operations in the same order, so each lane of the pair is
  * bit-identical to the scalar test. */
-PMD void isect_tri_pair(const_f32_ptr qa, const_f32_ptr qb, const Ray &ray, f2 &t, f2 &beta, f2 &gamma) {
-    const f2 p0x = {qa[0], qb[0]}, p0y = {qa[1], qb[1]}, p0z = {qa[2], qb[2]};
-    const f2 e0x = {qa[3], qb[3]}, e0y = {qa[4], qb[4]}, e0z = {qa[5], qb[5]};
-    const f2 e1x = {qa[6], qb[6]}, e1y = {qa[7], qb[7]}, e1z = {qa[8], qb[8]};
-    const f2 nx = {qa[9], qb[9]}, ny = {qa[10], qb[10]}, nz = {qa[11], qb[11]};
+/* two triangles' (p0, e0, e1, n) as packed pairs, wave-uniform */
+struct TriPair { f2 p0x, p0y, p0z, e0x, e0y, e0z, e1x, e1y, e1z, nx, ny, nz; };
+PMD TriPair load_pair(const_f32_ptr qa, const_f32_ptr qb) {
+    TriPair q;
+    q.p0x = f2{qa[0], qb[0]}; q.p0y = f2{qa[1], qb[1]}; q.p0z = f2{qa[2], qb[2]};
+    q.e0x = f2{qa[3], qb[3]}; q.e0y = f2{qa[4], qb[4]}; q.e0z = f2{qa[5], qb[5]};
+    q.e1x = f2{qa[6], qb[6]}; q.e1y = f2{qa[7], qb[7]}; q.e1z = f2{qa[8], qb[8]};
+    q.nx = f2{qa[9], qb[9]}; q.ny = f2{qa[10], qb[10]}; q.nz = f2{qa[11], qb[11]};
+    return q;
+}
+PMD void isect_tri_pair(const TriPair &q, const Ray &ray, f2 &t, f2 &beta, f2 &gamma) {
+    const f2 p0x = q.p0x, p0y = q.p0y, p0z = q.p0z, e0x = q.e0x, e0y = q.e0y, e0z = q.e0z;
+    const f2 e1x = q.e1x, e1y = q.e1y, e1z = q.e1z, nx = q.nx, ny = q.ny, nz = q.nz;
     const f2 dx = bc2(ray.d.x), dy = bc2(ray.d.y), dz = bc2(ray.d.z);
     const f2 den = (nx * dx + ny * dy) + nz * dz; /* dot(n, d) */
     f2 inv;
-    inv.x = 1.0f / den.x;
-    inv.y = 1.0f / den.y;
+    inv.x = rcp_exact(den.x);
+    inv.y = rcp_exact(den.y);
     const f2 e2x = inv * (p0x - bc2(ray.o.x)), e2y = inv * (p0y - bc2(ray.o.y)), e2z = inv * (p0z - bc2(ray.o.z));
     const f2 ix = dy * e2z - dz * e2y, iy = dz * e2x - dx * e2z, iz = dx * e2y - dy * e2x; /* cross(d, e2) */
     beta = (ix * e1x + iy * e1y) + iz * e1z;
@@ -357,21 +376,30 @@ PMD void isect_tri_pair(const_f32_ptr qa, const_f32_ptr qb, const Ray &ray, f2 &
     t = (nx * e2x + ny * e2y) + nz * e2z;
 }
 
+/* Brute-force scenes store their triangles in global-id order (pm_api.cpp
+ * build_scene), and triangles, disks, spheres are tested in that order, which
+ * is ascending global id: a strict t < best.t keeps the first of equal-t hits
+ * = the lowest id, the same hit consider() picks in any order — no id loads
+ * in the loop. best.gid is left unset (nothing after the query reads it). */
+PMD void take(Hit &best, float t, float b, float g, uint32_t ref) {
+    best.t = t; best.beta = b; best.gamma = g; best.ref = ref;
+}
 template <bool ANY, class C>
 PMD bool brute_isect(const SceneDev &S, const Ray &ray, Hit &best, C &cen) {
     const const_f32_ptr tg = (const_f32_ptr)S.tri_geo_g; /* constant address space: s_load */
-    const const_u32_ptr tid = (const_u32_ptr)S.tri_id_g;
     int k = 0;
+    /* (software-pipelining the next pair's scalar loads measured slower:
+     * C2 trace 91 vs 86 us — more live SGPRs, no unroll) */
 #pragma unroll 2
     for (; k + 1 < S.n_tris; k += 2) {
         cen.prim(); cen.prim();
         f2 t, b, g;
-        isect_tri_pair(tg + 12 * k, tg + 12 * (k + 1), ray, t, b, g);
+        isect_tri_pair(load_pair(tg + 12 * k, tg + 12 * (k + 1)), ray, t, b, g);
         const bool ok0 = (t.x < ray.tmax) & (t.x > ray.tmin) & (b.x >= 0.0f) & (g.x >= 0.0f) & (b.x + g.x <= 1);
         const bool ok1 = (t.y < ray.tmax) & (t.y > ray.tmin) & (b.y >= 0.0f) & (g.y >= 0.0f) & (b.y + g.y <= 1);
         if (ANY) { if (ok0 | ok1) return true; continue; }
-        if (ok0 && t.x <= best.t) consider(best, t.x, b.x, g.x, (PRIM_TRI << 30) | (uint32_t)k, tid[k]);
-        if (ok1 && t.y <= best.t) consider(best, t.y, b.y, g.y, (PRIM_TRI << 30) | (uint32_t)(k + 1), tid[k + 1]);
+        if (ok0 && t.x < best.t) take(best, t.x, b.x, g.x, (PRIM_TRI << 30) | (uint32_t)k);
+        if (ok1 && t.y < best.t) take(best, t.y, b.y, g.y, (PRIM_TRI << 30) | (uint32_t)(k + 1));
     }
     if (k < S.n_tris) {
         cen.prim();
@@ -381,21 +409,21 @@ PMD bool brute_isect(const SceneDev &S, const Ray &ray, Hit &best, C &cen) {
                      cc = make_float4(q[8], q[9], q[10], q[11]);
         const bool ok = isect_tri_v(a, bb, cc, ray, &t, &b, &g);
         if (ANY && ok) return true;
-        if (!ANY && ok && t <= best.t) consider(best, t, b, g, (PRIM_TRI << 30) | (uint32_t)k, tid[k]);
+        if (!ANY && ok && t < best.t) take(best, t, b, g, (PRIM_TRI << 30) | (uint32_t)k);
     }
     for (int k = 0; k < S.n_disks; ++k) {
         cen.prim();
         float t;
         const bool ok = isect_disk(S.disks + 5 * k, ray, &t);
         if (ANY) { if (ok) return true; continue; }
-        if (ok && t <= best.t) consider(best, t, 0.f, 0.f, (PRIM_DISK << 30) | (uint32_t)k, (uint32_t)fbits(S.disks[5 * k + 4].w));
+        if (ok && t < best.t) take(best, t, 0.f, 0.f, (PRIM_DISK << 30) | (uint32_t)k);
     }
     for (int k = 0; k < S.n_spheres; ++k) {
         cen.prim();
         float t;
         const bool ok = isect_sphere(S.spheres + 4 * k, ray, &t);
         if (ANY) { if (ok) return true; continue; }
-        if (ok && t <= best.t) consider(best, t, 0.f, 0.f, (PRIM_SPHERE << 30) | (uint32_t)k, (uint32_t)fbits(S.spheres[4 * k + 3].w));
+        if (ok && t < best.t) take(best, t, 0.f, 0.f, (PRIM_SPHERE << 30) | (uint32_t)k);
     }
     return false;
 }
@@ -603,7 +631,7 @@ PMD v3 sample_l_shading(const LightDev &L, v3 point, float u1, float u2, v3 *uwi
     int type = fbits(L.o_type.w);
     if (type == PM_LIGHT_POINT) {
         *uwi = xyz(L.o_type) - point;
-        float invlength2 = 1.0f / dot(*uwi, *uwi);
+        float invlength2 = rcp_exact(dot(*uwi, *uwi));
         *pdf = 1.f;
         return xyz(L.le) * invlength2;
     }

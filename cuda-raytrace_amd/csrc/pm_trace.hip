@@ -160,7 +160,16 @@ struct PathState {
     uint32_t nI;     /* photons-in-path counter (reference nI) */
     uint32_t spec;   /* specular bounces so far */
     uint32_t stored; /* slots [0, stored) written */
+    /* fused counting: the bucket rank of the last deposit is stored one deposit
+     * later (or when the path ends), so the wave never waits for the returning
+     * atomic right after issuing it */
+    uint32_t pslot;  /* slot of the pending rank, PSLOT_NONE if none */
+    uint32_t prank;
 };
+constexpr uint32_t PSLOT_NONE = 0xffffffffu;
+PMD void flush_rank(const TraceParams &P, PathState &st) {
+    if (st.pslot != PSLOT_NONE) { P.rank[st.pslot] = st.prank; st.pslot = PSLOT_NONE; }
+}
 
 /* Phase profile of k_trace (profiling builds only: `make prof` ->
  * lib/libpmhip_prof.so): per-wave s_memtime cycles accumulated per phase,
@@ -195,7 +204,7 @@ PMD bool emit_path(const TraceParams &P, const SceneDev &S, const uint32_t *perm
     const LightDev Lt = S.lights[P.light_index];
     v3 N1; float pdf;
     v3 Le = sample_le(Lt, smp[0], smp[1], smp[2], smp[3], P.eps, &st.ray, &N1, &pdf);
-    st.pid = pid; st.nI = 0; st.spec = 0; st.stored = 0;
+    st.pid = pid; st.nI = 0; st.spec = 0; st.stored = 0; st.pslot = PSLOT_NONE;
     if (pdf == 0.0f || is_black(Le)) return false;
     st.ray.tmax = RT_DEFAULT_MAX;
     st.alpha = (absdot(N1, st.ray.d) * Le) / pdf;
@@ -215,6 +224,7 @@ PMD bool path_step(const TraceParams &P, const SceneDev &S, int *stack, PathStat
     v3 hit_point = st.ray.o + h.t * st.ray.d;
     float4 m = S.materials[g.material];
     int mtype = fbits(m.w);
+    prof.mark(3);
     if (is_specular(mtype)) {
         v3 wi;
         if (!material_specular(mtype, g, -st.ray.d, &wi)) return false;
@@ -235,9 +245,12 @@ PMD bool path_step(const TraceParams &P, const SceneDev &S, int *stack, PathStat
             const uint32_t cz = cell_axis(hit_point.z, g.gz, g.inv_cs, g.dz);
             const uint32_t key = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx + cx;
             P.key[slot] = key;
-            P.rank[slot] = atomicAdd(&P.count[key], 1u);
+            const uint32_t rank = atomicAdd(&P.count[key], 1u);
+            flush_rank(P, st);
+            st.prank = rank; st.pslot = (uint32_t)slot;
         }
     }
+    prof.mark(4);
     if (st.nI >= mpc) return false;
     const uint32_t pm_index = st.pid * mpc;
     uint32_t o4[4];
@@ -250,12 +263,14 @@ PMD bool path_step(const TraceParams &P, const SceneDev &S, int *stack, PathStat
     st.alpha = anew;
     st.nI++;
     st.ray.o = hit_point; st.ray.d = wiw; st.ray.tmin = P.eps; st.ray.tmax = RT_DEFAULT_MAX;
+    prof.mark(5);
     return true;
 }
 
 /* a finished path's unused slots are invalid = zero (the reference leaves
  * them stale, DESIGN.md divergences); written here instead of a memset pass */
-PMD void finish_path(const TraceParams &P, const PathState &st) {
+PMD void finish_path(const TraceParams &P, PathState &st) {
+    flush_rank(P, st);
     const uint32_t mpc = (uint32_t)P.mpc;
     pm_photon *slots = P.slots + (size_t)(st.pid - (uint64_t)P.slot_path_base) * mpc;
     const float2 z = make_float2(0.f, 0.f);
@@ -338,6 +353,8 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceParams P) {
             if (!alive) {
                 if (COUNT) deposits += st.stored;
                 finish_path(P, st);
+            } else {
+                flush_rank(P, st); /* the path state moves through LDS below */
             }
         }
         next += n_new;
