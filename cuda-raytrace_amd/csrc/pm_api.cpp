@@ -81,7 +81,7 @@ struct Ctx {
     DevBuf d_slots;
     int64_t slots_used = 0;
     /* photon buckets */
-    DevBuf d_count, d_cell_start, d_scratch, d_pha, d_phb, d_phc;
+    DevBuf d_count, d_cell_start, d_scratch, d_pha, d_phb;
     struct { bool valid = false; int64_t n = 0; GridDesc grid{}; } fused; /* counts made by the last trace */
     GridDesc grid{};
     int map_kind = -1;
@@ -303,7 +303,7 @@ GatherParams gather_params(Ctx *c, const pm_render_params *p) {
     G.ppm_alpha = p->ppm_alpha;
     G.grid = c->grid;
     G.cell_start = c->d_cell_start.as<uint32_t>();
-    G.ph_a = c->d_pha.as<float4>(); G.ph_b = c->d_phb.as<float4>(); G.ph_c = c->d_phc.as<float>();
+    G.ph_a = c->d_pha.as<float4>(); G.ph_b = c->d_phb.as<float4>();
     G.kd_nodes = c->d_kd.as<pm_photon>(); G.kd_count = c->kd_count;
     G.counters = c->d_counters.as<unsigned long long>();
     if (c->view_active) { G.view_rank = c->d_vrank.as<uint32_t>(); G.view_list = c->d_vlist.as<uint32_t>(); }
@@ -424,7 +424,7 @@ void pm_destroy(void *ptr) {
         }
     DevBuf *bufs[] = {&c->d_scene, &c->d_rays, &c->d_rand2d, &c->d_pos, &c->d_nrm, &c->d_state, &c->d_n,
                       &c->d_dl, &c->d_slots, &c->d_count, &c->d_scratch, &c->d_vflags, &c->d_vrank, &c->d_vlist, &c->d_vsums,
-                      &c->d_cell_start, &c->d_pha, &c->d_phb, &c->d_phc,
+                      &c->d_cell_start, &c->d_pha, &c->d_phb,
                       &c->d_kd, &c->d_out, &c->d_counters};
     for (DevBuf *b : bufs) b->release();
     (void)hipStreamDestroy(c->stream);
@@ -923,11 +923,11 @@ int pm_build_photon_map(void *ptr, const pm_render_params *p, int64_t n_slots, v
         HIPCHK(c, c->d_scratch.ensure(bucket_scratch_words(n_slots, g.ncells) * 4));
         HIPCHK(c, count_zeroed(c, (size_t)g.ncells + 1, s));
     }
-    HIPCHK(c, c->d_pha.ensure(n * 16)); HIPCHK(c, c->d_phb.ensure(n * 16)); HIPCHK(c, c->d_phc.ensure(n * 4));
+    HIPCHK(c, c->d_pha.ensure(n * 16)); HIPCHK(c, c->d_phb.ensure(n * 32));
     timer_begin(c, "build", s);
     HIPCHK(c, launch_bucket_build(c->d_slots.as<pm_photon>(), n_slots, g, c->d_count.as<uint32_t>(),
                                   c->d_cell_start.as<uint32_t>(), c->d_scratch.as<uint32_t>(), c->d_pha.as<float4>(),
-                                  c->d_phb.as<float4>(), c->d_phc.as<float>(), counted, s));
+                                  c->d_phb.as<float4>(), counted, s));
     /* the scan left the counters zeroed */
     c->count_zero_words = (size_t)g.ncells + 1;
     c->count_zero_ptr = c->d_count.p;

@@ -17,7 +17,10 @@
  *                      number of valid photons. The counters are zeroed as
  *                      they are read, so the next pass needs no memset.
  *   3. k_bucket_fill   slot -> cell_start[key] + rank, written straight into
- *                      the SoA arrays the gather streams (ph_a, ph_b, ph_c)
+ *                      the arrays the gather reads: ph_a (position, wi.x;
+ *                      16 B, streamed by every range test) and ph_b (alpha,
+ *                      wi.y | wi.z, pad: one 32-B sector, read only for
+ *                      photons inside the radius)
  * The order inside a bucket depends on atomic arrival order. Results do not:
  * the bucket gather (pm_gather.hip) sums flux in exact 64-bit fixed point
  * and counts photons as integers, so any order gives identical bits.
@@ -151,7 +154,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_down(const uint32_t *in, in
 
 __global__ __launch_bounds__(256) void k_bucket_fill(const pm_photon *slots, int64_t n, const uint32_t *key,
                                                      const uint32_t *rank, const uint32_t *cell_start, float4 *ph_a,
-                                                     float4 *ph_b, float *ph_c) {
+                                                     float4 *ph_b) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const uint32_t k = key[i];
@@ -161,8 +164,11 @@ __global__ __launch_bounds__(256) void k_bucket_fill(const pm_photon *slots, int
     const float2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
     /* a = (bits, p.x) b = (p.y, p.z) c = (alpha.x, alpha.y) d = (alpha.z, wi.x) e = (wi.y, wi.z) */
     ph_a[dst] = make_float4(a.y, b.x, b.y, d.y);
-    ph_b[dst] = make_float4(c.x, c.y, d.x, e.x);
-    ph_c[dst] = e.y;
+    /* one whole 32-B sector per photon: scattered stores cost a sector
+     * write-back each, so (alpha, wi.y) + wi.z as one sector instead of two
+     * arrays saves a third of the fill's write traffic */
+    ph_b[2 * (size_t)dst] = make_float4(c.x, c.y, d.x, e.x);
+    ph_b[2 * (size_t)dst + 1] = make_float4(e.y, 0.f, 0.f, 0.f);
 }
 /* Measured (PMC WRITE_SIZE): ~55 MB written per launch for ~20 MB of photon
  * data — the scattered 16-B stores cost whole-line write-backs. Giving each
@@ -186,7 +192,7 @@ size_t bucket_scratch_words(int64_t n_slots, uint32_t ncells) {
 }
 
 hipError_t launch_bucket_build(const pm_photon *slots, int64_t n, GridDesc g, uint32_t *count, uint32_t *cell_start,
-                               uint32_t *scratch, float4 *ph_a, float4 *ph_b, float *ph_c, bool counted, hipStream_t s) {
+                               uint32_t *scratch, float4 *ph_a, float4 *ph_b, bool counted, hipStream_t s) {
     const int64_t nc = (int64_t)g.ncells + 1; /* last counter stays 0 -> cell_start[ncells] = total */
     uint32_t *key = scratch, *rank = scratch + n, *sums = scratch + 2 * n;
     if (n > 0 && !counted)
@@ -198,7 +204,7 @@ hipError_t launch_bucket_build(const pm_photon *slots, int64_t n, GridDesc g, ui
     pm_launch(k_scan_down, dim3(ntile), dim3(SCAN_BLOCK), 0, s, count, nc, sums, cell_start, count);
     if (n > 0)
         pm_launch(k_bucket_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slots, n, key, rank,
-                           cell_start, ph_a, ph_b, ph_c);
+                           cell_start, ph_a, ph_b);
     return hipGetLastError();
 }
 

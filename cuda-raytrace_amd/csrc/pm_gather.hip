@@ -85,8 +85,8 @@ __global__ __launch_bounds__(GATHER_BLOCK, 8) void k_gather_grid(GatherParams P)
                     float dist2 = diff.x * diff.x + diff.y * diff.y + diff.z * diff.z;
                     if (dist2 < r2) {
                         M++;
-                        float4 bb = P.ph_b[j];
-                        float wz = P.ph_c[j];
+                        const float4 bb = P.ph_b[2 * (size_t)j];
+                        const float wz = reinterpret_cast<const float *>(P.ph_b)[8 * (size_t)j + 4];
                         v3 wi = mk(a.w, bb.w, wz);
                         v3 c = fabsf(dot(ns, wi)) * fv * xyz(bb); /* processPhoton, gathering.cu:17-23 */
                         Lf.x += to_fx(c.x, sc); Lf.y += to_fx(c.y, sc); Lf.z += to_fx(c.z, sc);

@@ -102,8 +102,7 @@ struct GatherParams {
     GridDesc grid;
     const uint32_t *cell_start; /* ncells + 1 */
     const float4 *ph_a;         /* x, y, z, wi.x */
-    const float4 *ph_b;         /* alpha.rgb, wi.y */
-    const float *ph_c;          /* wi.z */
+    const float4 *ph_b;         /* 2 per photon: (alpha.rgb, wi.y), (wi.z, 0, 0, 0) */
     /* kd-tree (reference layout) */
     const pm_photon *kd_nodes;
     int64_t kd_count;
@@ -146,7 +145,7 @@ hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s);
  * otherwise count must arrive zeroed. count leaves zeroed (cleared by the scan). */
 size_t bucket_scratch_words(int64_t n_slots, uint32_t ncells);
 hipError_t launch_bucket_build(const pm_photon *slots, int64_t n, GridDesc g, uint32_t *count, uint32_t *cell_start,
-                               uint32_t *scratch, float4 *ph_a, float4 *ph_b, float *ph_c, bool counted, hipStream_t s);
+                               uint32_t *scratch, float4 *ph_a, float4 *ph_b, bool counted, hipStream_t s);
 /* gather: structure 0 grid, 1 kd; mode 0 fused PPM, 1 partial */
 hipError_t launch_gather(const GatherParams &p, int structure, int partial, int count, hipStream_t s);
 hipError_t launch_ppm_update(const GatherParams &p, const long long *partial, int64_t rec_begin, int64_t rec_count,
