@@ -1212,6 +1212,16 @@ int pm_trace_counters(void *ptr, int64_t out[4]) {
     return PM_OK;
 }
 
+int pm_scene_info(void *ptr, int64_t out[7]) {
+    GETCTX(ptr);
+    if (!c->S.blob) FAIL(c, PM_ERR_INVALID, "no scene committed");
+    const SceneDev &S = c->S;
+    out[0] = S.n_tris; out[1] = S.n_disks; out[2] = S.n_spheres; out[3] = S.n_nodes; out[4] = c->bvh_depth;
+    out[5] = scene_mode(S) == MODE_BRUTE ? 2 : scene_mode(S) == MODE_LDS ? 1 : 0;
+    out[6] = S.blob_bytes;
+    return PM_OK;
+}
+
 int pm_trace_profile(void *ptr, int64_t out[8], int reset) {
     GETCTX(ptr);
     unsigned long long h[8];

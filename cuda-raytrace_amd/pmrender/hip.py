@@ -73,6 +73,7 @@ def load_library(path=None):
         "pm_download_kdtree": (c_int, [vp, vp, i64]),
         "pm_gather_counters": (c_int, [vp, ctypes.POINTER(i64)]),
         "pm_trace_counters": (c_int, [vp, ctypes.POINTER(i64)]),
+        "pm_scene_info": (c_int, [vp, ctypes.POINTER(i64)]),
         "pm_trace_profile": (c_int, [vp, ctypes.POINTER(i64), c_int]),
         "pm_set_counting": (c_int, [vp, c_int]),
         "pm_set_stage_timing": (c_int, [vp, ctypes.c_char_p]),
@@ -333,6 +334,14 @@ class Context:
         out = (ctypes.c_int64 * 4)()
         self._chk(self.lib.pm_trace_counters(self.h, out))
         return tuple(int(v) for v in out)
+
+    def scene_info(self):
+        """dict: triangles, disks, spheres, bvh_nodes, bvh_depth, mode ("bvh-hbm" | "bvh-lds" | "brute"), bytes."""
+        out = (ctypes.c_int64 * 7)()
+        self._chk(self.lib.pm_scene_info(self.h, out))
+        v = [int(x) for x in out]
+        return {"triangles": v[0], "disks": v[1], "spheres": v[2], "bvh_nodes": v[3], "bvh_depth": v[4],
+                "mode": ("bvh-hbm", "bvh-lds", "brute")[v[5]], "bytes": v[6]}
 
     def trace_profile(self, reset=False):
         """k_trace phase cycles (profiling builds, lib/libpmhip_prof.so): dict of summed cycles."""

@@ -242,6 +242,10 @@ int pm_gather_counters(void *ctx, int64_t out[4]);
  * [1] BVH nodes entered, [2] primitive intersection tests, [3] photons
  * deposited (the traffic census behind the trace roofline) */
 int pm_trace_counters(void *ctx, int64_t out[4]);
+/* the loaded scene as the traversal kernels see it: [0] triangles, [1] disks,
+ * [2] spheres, [3] BVH nodes, [4] BVH depth, [5] traversal mode (0 BVH in
+ * HBM, 1 BVH in LDS, 2 brute force over an LDS-sized scene), [6] scene bytes */
+int pm_scene_info(void *ctx, int64_t out[7]);
 /* Phase profile of the trace kernel, summed over waves and launches since the
  * last reset: shader-clock cycles in [0] emission, [1] BVH traversal,
  * [2] shading + bounce + deposit, [3] compaction barrier, [4] state exchange,

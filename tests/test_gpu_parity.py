@@ -89,6 +89,20 @@ def test_trace_census(cornell):
     assert nodes >= rays and prims >= deposits
 
 
+def test_scene_info(cornell, hip_mod):
+    """Traversal mode chosen per scene: the Cornell box (30 triangles + the
+    disk light) is brute-forced; a few thousand triangles get a BVH."""
+    ctx, _ = cornell
+    info = ctx.scene_info()
+    assert info["mode"] == "brute" and info["triangles"] == 30 and info["disks"] == 1
+    big = scenes.triangle_soup(3000, 32, 24).load_into(hip_mod.Context(0))
+    try:
+        bi = big.scene_info()
+        assert bi["mode"] in ("bvh-hbm", "bvh-lds") and bi["triangles"] >= 3000 and bi["bvh_nodes"] > 1
+    finally:
+        big.close()
+
+
 @pytest.mark.parametrize("structure", [PM_GATHER_GRID, PM_GATHER_KDTREE])
 def test_deferred_reset(cornell, structure):
     """pm_reset_records is deferred: a fused full gather consumes it (same
