@@ -185,9 +185,10 @@ void CudaRender::objectInstance(const void *instance, const Transform &tr) {
 void CudaRender::createSubRenderer(const RenderSettings &settings, const std::string &rendername) {
     delete renderer_;
     renderer_ = nullptr;
-    if (rendername == "simple") warning("renderer '%s' is not on the MI355X path; using photon mapping",
-                                        rendername.c_str());
-    renderer_ = new PhotonMappingRenderer(settings); /* cudarender.cpp:126-134 */
+    if (rendername == "simple") /* cudarender.cpp:126-134 */
+        renderer_ = new SimpleRenderer(settings);
+    else
+        renderer_ = new PhotonMappingRenderer(settings);
 }
 
 /* CudaLight::setupLight (cudalight.cpp:16-59) */
@@ -226,25 +227,22 @@ void CudaRender::Render(const std::vector<Light> &lights, Camera &camera) {
 }
 
 /* ------------------------------------------------------------ renderer */
-void PhotonMappingRenderer::render(CudaRender *r, const std::vector<Light> &, Camera &camera) {
-    void *ctx = r->context();
-    int64_t n;
+static int64_t set_camera(void *ctx, const Camera &camera) {
     if (camera.pinhole) {
         check(ctx, pm_set_pinhole(ctx, camera.eye, camera.fwd, camera.right, camera.up, camera.width, camera.height),
               "pm_set_pinhole");
-        n = (int64_t)camera.width * camera.height;
-    } else {
-        n = (int64_t)(camera.rays.size() / 6);
-        check(ctx, pm_set_eye_rays(ctx, camera.rays.data(), n, camera.rand2d.empty() ? nullptr : camera.rand2d.data(),
-                                   camera.n2d),
-              "pm_set_eye_rays");
+        return (int64_t)camera.width * camera.height;
     }
-    /* eye pass -> (photon pass -> photon map -> gather) x passes -> final
-     * (photonmappingrenderer.cpp:31-45), NaN / negative / inf -> black */
-    rgb.assign((size_t)(3 * n), 0.f);
-    check(ctx, pm_render(ctx, &settings.params, rgb.data(), &stats), "pm_render");
+    const int64_t n = (int64_t)(camera.rays.size() / 6);
+    check(ctx, pm_set_eye_rays(ctx, camera.rays.data(), n, camera.rand2d.empty() ? nullptr : camera.rand2d.data(),
+                               camera.n2d),
+          "pm_set_eye_rays");
+    return n;
+}
+
+/* film splat (photonmappingrenderer.cpp:247-272, simplerender.cpp:68-89) */
+static void splat(Camera &camera, const std::vector<float> &rgb, int64_t n) {
     if (!camera.film) return;
-    /* film splat (photonmappingrenderer.cpp:247-272) */
     for (int64_t i = 0; i < n; ++i) {
         CameraSample cs;
         if (camera.pinhole) {
@@ -256,6 +254,24 @@ void PhotonMappingRenderer::render(CudaRender *r, const std::vector<Light> &, Ca
         camera.film->AddSample(cs, &rgb[3 * i]);
     }
     camera.film->WriteImage();
+}
+
+void SimpleRenderer::render(CudaRender *r, const std::vector<Light> &, Camera &camera) {
+    void *ctx = r->context();
+    const int64_t n = set_camera(ctx, camera);
+    rgb.assign((size_t)(3 * n), 0.f);
+    check(ctx, pm_render_simple(ctx, &settings.params, rgb.data(), &stats), "pm_render_simple");
+    splat(camera, rgb, n);
+}
+
+void PhotonMappingRenderer::render(CudaRender *r, const std::vector<Light> &, Camera &camera) {
+    void *ctx = r->context();
+    const int64_t n = set_camera(ctx, camera);
+    /* eye pass -> (photon pass -> photon map -> gather) x passes -> final
+     * (photonmappingrenderer.cpp:31-45), NaN / negative / inf -> black */
+    rgb.assign((size_t)(3 * n), 0.f);
+    check(ctx, pm_render(ctx, &settings.params, rgb.data(), &stats), "pm_render");
+    splat(camera, rgb, n);
 }
 
 /* ------------------------------------------------------------ cudaapi.h */

@@ -141,6 +141,19 @@ public:
     std::vector<float> rgb; /* last output: per sample (rays) or raster (pinhole) */
 };
 
+/* SimpleRenderer (simple_render/simplerender.cpp:18-103): direct light only,
+ * scene_epsilon 0.01 (simplerender.cpp:23) -> pm_render_simple -> splat */
+class SimpleRenderer : public CudaRenderer {
+public:
+    explicit SimpleRenderer(const RenderSettings &s) : settings(s) {
+        settings.params.scene_epsilon = PM_SIMPLE_SCENE_EPSILON;
+    }
+    void render(CudaRender *render, const std::vector<Light> &lights, Camera &camera) override;
+    RenderSettings settings;
+    pm_stats stats{};
+    std::vector<float> rgb;
+};
+
 class CudaRender {
 public:
     explicit CudaRender(int device = 0);

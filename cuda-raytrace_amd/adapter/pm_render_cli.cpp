@@ -7,17 +7,23 @@
  * that this host path produces the same image as the Python stage driver.
  *
  *   pm_render_cli --scene cornell --width W --height H --camera e0 e1 e2 f0 f1 f2 r0 r1 r2 u0 u1 u2
- *                 [--paths N] [--passes P] [--structure grid|kd] [--instanced] --out img.pfm
+ *                 [--paths N] [--passes P] [--structure grid|kd] [--instanced]
+ *                 [--renderer photonmapping|simple] --out img.pfm
+ *   pm_render_cli --pbrt scene.pbrt [--out img.pfm] [--renderer R] [--paths N] [--passes P] [--structure S]
+ *                 (a pbrt-v2 scene file through pm_pbrt.h; command-line options override the file)
+ *   pm_render_cli --pbrt scene.pbrt --dump   (parse only, no device: the plugin calls as JSON)
  *   pm_render_cli --selftest      (host-only checks, no device needed)
  */
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
 #include "pm_cudarender.h"
+#include "pm_pbrt.h"
 
 using namespace pmcuda;
 
@@ -134,14 +140,138 @@ int selftest() {
     return bad ? 1 : 0;
 }
 
+/* --dump: records the plugin calls a scene file produces, as JSON (floats
+ * printed round-trip exact) — the parse checked without a device */
+struct DumpSink : PbrtSink {
+    std::string out;
+    std::map<const void *, int> keys;
+    static void arr(std::string &o, const float *v, size_t n) {
+        o += "[";
+        char b[32];
+        for (size_t i = 0; i < n; ++i) { std::snprintf(b, sizeof b, "%s%.9g", i ? ", " : "", v[i]); o += b; }
+        o += "]";
+    }
+    int key(const void *k) {
+        if (!k) return -1;
+        auto it = keys.find(k);
+        if (it != keys.end()) return it->second;
+        const int id = (int)keys.size();
+        keys[k] = id;
+        return id;
+    }
+    void shape(const std::string &name, const Shape &s, const void *inst, const Material *m, int li) override {
+        char b[160];
+        if (!out.empty()) out += ",\n";
+        std::snprintf(b, sizeof b, "{\"call\": \"shape\", \"name\": \"%s\", \"instance\": %d, \"light\": %d, ",
+                      name.c_str(), key(inst), li);
+        out += b;
+        const int kind = !m ? -1 : (int)m->kind;
+        const float k[3] = {m ? m->k.r : 0.f, m ? m->k.g : 0.f, m ? m->k.b : 0.f};
+        std::snprintf(b, sizeof b, "\"material\": %d, \"k\": ", kind);
+        out += b;
+        arr(out, k, 3);
+        out += ", \"P\": "; arr(out, s.P.data(), s.P.size());
+        out += ", \"N\": "; arr(out, s.N.data(), s.N.size());
+        out += ", \"uv\": "; arr(out, s.uv.data(), s.uv.size());
+        out += ", \"indices\": [";
+        for (size_t i = 0; i < s.indices.size(); ++i) out += (i ? ", " : "") + std::to_string(s.indices[i]);
+        out += "], \"o2w\": "; arr(out, s.o2w.m, 16);
+        out += ", \"w2o\": "; arr(out, s.o2w.minv, 16);
+        const float sc[4] = {s.radius, s.height, s.inner_radius, s.phi_max};
+        out += ", \"radius_height_inner_phimax\": "; arr(out, sc, 4);
+        out += "}";
+    }
+    void objectInstance(const void *k, const Transform &tr) override {
+        if (!out.empty()) out += ",\n";
+        out += "{\"call\": \"instance\", \"instance\": " + std::to_string(key(k)) + ", \"o2w\": ";
+        arr(out, tr.m, 16);
+        out += "}";
+    }
+};
+
+int dump(const std::string &path) {
+    DumpSink sink;
+    PbrtOptions o;
+    PbrtParser parser;
+    parser.parseFile(path, sink, o);
+    std::string lights;
+    for (const Light &L : o.lights) {
+        if (!lights.empty()) lights += ",\n";
+        char b[128];
+        if (L.kind == Light::Point) {
+            const float I[3] = {L.intensity.r, L.intensity.g, L.intensity.b};
+            lights += "{\"kind\": \"point\", \"pos\": ";
+            DumpSink::arr(lights, L.pos, 3);
+            lights += ", \"I\": ";
+            DumpSink::arr(lights, I, 3);
+        } else {
+            const float Le[3] = {L.Lemit.r, L.Lemit.g, L.Lemit.b};
+            std::snprintf(b, sizeof b, "{\"kind\": \"disk\", \"nsamples\": %d, \"Le\": ", L.n_samples);
+            lights += b;
+            DumpSink::arr(lights, Le, 3);
+            lights += ", \"o2w\": ";
+            DumpSink::arr(lights, L.disk.o2w.m, 16);
+            const float sc[4] = {L.disk.radius, L.disk.height, L.disk.inner_radius, L.disk.phi_max};
+            lights += ", \"radius_height_inner_phimax\": ";
+            DumpSink::arr(lights, sc, 4);
+        }
+        lights += "}";
+    }
+    const Camera &c = o.camera;
+    std::printf("{\"calls\": [\n%s],\n\"lights\": [\n%s],\n\"camera\": {\"width\": %d, \"height\": %d, \"eye\": ",
+                sink.out.c_str(), lights.c_str(), c.width, c.height);
+    std::string cam;
+    DumpSink::arr(cam, c.eye, 3); cam += ", \"fwd\": ";
+    DumpSink::arr(cam, c.fwd, 3); cam += ", \"right\": ";
+    DumpSink::arr(cam, c.right, 3); cam += ", \"up\": ";
+    DumpSink::arr(cam, c.up, 3);
+    const pm_render_params &p = o.settings.params;
+    std::printf("%s},\n\"renderer\": \"%s\", \"paths\": %lld, \"passes\": %d, \"gather\": %d, \"film\": \"%s\", "
+                "\"warnings\": %d}\n",
+                cam.c_str(), o.renderer.c_str(), (long long)p.paths_per_pass, p.passes, p.gather_structure,
+                o.film_filename.c_str(), o.warnings);
+    return 0;
+}
+
+/* a .pbrt scene through the plugin surface, as pbrt-v2 + the reference would run it */
+int render_pbrt(const std::string &path, std::string out, const std::string &renderer, long long paths, int passes,
+                const std::string &structure) {
+    CudaRenderInit(0);
+    PbrtOptions o;
+    CudaApiSink sink;
+    PbrtParser parser;
+    parser.parseFile(path, sink, o);
+    if (!renderer.empty()) o.renderer = renderer;
+    pm_render_params &p = o.settings.params;
+    if (paths > 0) p.paths_per_pass = paths;
+    if (passes > 0) p.passes = passes;
+    if (!structure.empty()) p.gather_structure = structure == "kd" ? PM_GATHER_KDTREE : PM_GATHER_GRID;
+    if (out.empty()) out = o.film_filename;
+    CudaRender *render = CreateCudaRenderer(o.settings, o.renderer);
+    PixelFilm film(o.camera.width, o.camera.height, out);
+    o.camera.film = &film;
+    render->Render(o.lights, o.camera);
+    if (auto *pm = dynamic_cast<PhotonMappingRenderer *>(render->subRenderer()))
+        std::printf("{\"renderer\": \"photonmapping\", \"paths_emitted\": %lld, \"photons_valid\": %lld, "
+                    "\"gather_points\": %lld}\n",
+                    (long long)pm->stats.paths_emitted, (long long)pm->stats.photons_valid,
+                    (long long)pm->stats.gather_points);
+    else
+        std::printf("{\"renderer\": \"simple\", \"samples\": %lld}\n",
+                    (long long)static_cast<SimpleRenderer *>(render->subRenderer())->stats.gather_points);
+    delete render;
+    return 0;
+}
+
 } // namespace
 
 int main(int argc, char **argv) {
-    std::string scene = "cornell", out = "out.pfm", structure = "grid";
+    std::string scene = "cornell", out, structure, renderer, pbrt;
+    bool dump_only = false;
     int W = 64, H = 48;
     long long paths = 512 * 512;
     int passes = 1;
-    bool instanced = false, have_cam = false;
+    bool instanced = false, have_cam = false, paths_set = false, passes_set = false;
     float cam[12] = {0};
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -153,16 +283,29 @@ int main(int argc, char **argv) {
         else if (a == "--scene") scene = next();
         else if (a == "--width") W = std::atoi(next());
         else if (a == "--height") H = std::atoi(next());
-        else if (a == "--paths") paths = std::atoll(next());
-        else if (a == "--passes") passes = std::atoi(next());
+        else if (a == "--paths") { paths = std::atoll(next()); paths_set = true; }
+        else if (a == "--passes") { passes = std::atoi(next()); passes_set = true; }
         else if (a == "--structure") structure = next();
         else if (a == "--instanced") instanced = true;
+        else if (a == "--renderer") renderer = next();
+        else if (a == "--pbrt") pbrt = next();
+        else if (a == "--dump") dump_only = true;
         else if (a == "--out") out = next();
         else if (a == "--camera") {
             for (float &c : cam) c = std::strtof(next(), nullptr);
             have_cam = true;
         } else { std::fprintf(stderr, "unknown argument %s\n", a.c_str()); return 2; }
     }
+    if (!pbrt.empty()) {
+        try {
+            if (dump_only) return dump(pbrt);
+            return render_pbrt(pbrt, out, renderer, paths_set ? paths : 0, passes_set ? passes : 0, structure);
+        } catch (const Error &e) {
+            std::fprintf(stderr, "pm_render_cli: %s\n", e.what());
+            return 1;
+        }
+    }
+    if (out.empty()) out = "out.pfm";
     if (scene != "cornell" || !have_cam) {
         std::fprintf(stderr, "usage: %s --scene cornell --camera <12 floats> [--width W --height H] --out f.pfm\n",
                      argv[0]);
@@ -176,7 +319,7 @@ int main(int argc, char **argv) {
         settings.params.paths_per_pass = paths;
         settings.params.passes = passes;
         settings.params.gather_structure = structure == "kd" ? PM_GATHER_KDTREE : PM_GATHER_GRID;
-        CudaRender *render = CreateCudaRenderer(settings, "photonmapping");
+        CudaRender *render = CreateCudaRenderer(settings, renderer.empty() ? "photonmapping" : renderer);
         PixelFilm film(W, H, out);
         Camera camera;
         camera.pinhole = true;
@@ -188,7 +331,8 @@ int main(int argc, char **argv) {
         camera.height = H;
         camera.film = &film;
         render->Render(lights, camera);
-        const pm_stats &st = static_cast<PhotonMappingRenderer *>(render->subRenderer())->stats;
+        auto *pmr = dynamic_cast<PhotonMappingRenderer *>(render->subRenderer());
+        const pm_stats &st = pmr ? pmr->stats : static_cast<SimpleRenderer *>(render->subRenderer())->stats;
         std::printf("{\"paths_emitted\": %lld, \"photons_valid\": %lld, \"gather_points\": %lld}\n",
                     (long long)st.paths_emitted, (long long)st.photons_valid, (long long)st.gather_points);
         delete render;

@@ -1095,6 +1095,49 @@ int pm_render(void *ptr, const pm_render_params *p, float *out_rgb, pm_stats *st
     return PM_OK;
 }
 
+/* ------------------------------------------------------- simple renderer */
+int pm_simple_pass(void *ptr, const pm_render_params *p, void *d_out, void *stream) {
+    GETCTX(ptr);
+    if (!p) FAIL(c, PM_ERR_INVALID, "null params");
+    if (!c->committed) FAIL(c, PM_ERR_INVALID, "scene not committed (call pm_commit)");
+    if (!d_out) FAIL(c, PM_ERR_INVALID, "null output");
+    const int64_t n = num_records(c);
+    if (n <= 0) FAIL(c, PM_ERR_INVALID, "no eye samples (call pm_set_pinhole or pm_set_eye_rays)");
+    if (!c->pinhole && c->rand2d_total > c->n2d)
+        FAIL(c, PM_ERR_INVALID, "eye rays carry %d 2D samples, lights need %d", c->n2d, c->rand2d_total);
+    hipStream_t s = pick(c, stream);
+    EyeParams E{};
+    E.S = c->S;
+    E.R.count = n; /* the simple renderer keeps no records */
+    E.pinhole = c->pinhole; E.W = c->W; E.H = c->H; E.n2d = c->n2d;
+    E.eye = f4(c->eye[0], c->eye[1], c->eye[2], 0); E.fwd = f4(c->fwd[0], c->fwd[1], c->fwd[2], 0);
+    E.right = f4(c->right[0], c->right[1], c->right[2], 0); E.up = f4(c->up[0], c->up[1], c->up[2], 0);
+    E.rays = c->d_rays.as<float>(); E.rand2d = c->d_rand2d.as<float>();
+    E.eps = p->scene_epsilon; E.light_seed = p->light_rng_seed;
+    timer_begin(c, "simple", s);
+    HIPCHK(c, launch_simple(E, (float *)d_out, s));
+    timer_end(c, "simple", s);
+    return PM_OK;
+}
+
+int pm_render_simple(void *ptr, const pm_render_params *p, float *out_rgb, pm_stats *st) {
+    GETCTX(ptr);
+    if (!out_rgb) FAIL(c, PM_ERR_INVALID, "null output");
+    const int64_t nout = c->pinhole ? (int64_t)c->W * c->H : c->nrays;
+    if (nout > 0) HIPCHK(c, c->d_out.ensure(nout * 3 * sizeof(float)));
+    hipStream_t s = c->stream;
+    int rc;
+    if ((rc = pm_simple_pass(c, p, c->d_out.p, s))) return rc;
+    HIPCHK(c, hipMemcpyAsync(out_rgb, c->d_out.p, nout * 3 * sizeof(float), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (st) {
+        std::memset(st, 0, sizeof(*st));
+        st->gather_points = nout;
+        st->ms_eye = timer_ms(c, "simple");
+    }
+    return PM_OK;
+}
+
 /* ------------------------------------------------------- buffers / tests */
 int64_t pm_num_records(void *ptr) {
     Ctx *c = (Ctx *)ptr;

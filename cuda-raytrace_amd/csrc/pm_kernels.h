@@ -136,6 +136,9 @@ struct FinalParams {
 inline int scene_mode(const SceneDev &S) { return S.lds_bytes ? (S.brute ? MODE_BRUTE : MODE_LDS) : MODE_GLOBAL; }
 
 hipError_t launch_eye(const EyeParams &p, hipStream_t s);
+/* simple renderer (simplerender.cu): direct light per eye sample into out
+ * (float3, raster / sample order); only p.R.count of the records is read */
+hipError_t launch_simple(const EyeParams &p, float *out, hipStream_t s);
 /* writes every slot of its paths (deposits, then zeros); count: census */
 hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s);
 /* photon-bucket build (pm_bucket.hip): count + rank, scan, fill.

@@ -138,6 +138,96 @@ hipError_t launch_eye(const EyeParams &p, hipStream_t s) {
 }
 
 /* ====================================================================== */
+/* simple renderer (direct light only, simple_render/simplerender.cu)     */
+/* ====================================================================== */
+/* One lane per eye sample: closest hit of the camera ray (no specular
+ * chain), then for every light one shadow-tested sample (iSample 0, no pdf
+ * division, no emitted term): L += att·|ns·wi|·f·li (simplerender.cu:40-72);
+ * a miss is black (:75-79). The host's NaN / negative / infinite check
+ * (simplerender.cpp:70-87) is fused into the store. Output: raster order
+ * (pinhole) or sample order (host rays), float3 per sample. */
+template <int MODE>
+__global__ __launch_bounds__(EYE_BLOCK) void k_simple(EyeParams P, float *out) {
+    extern __shared__ __attribute__((aligned(16))) int stk[];
+    int *stack = stk + threadIdx.x;
+    const SceneDev S = scene_view<MODE != MODE_GLOBAL>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * EYE_BLOCK),
+                                                       threadIdx.x, EYE_BLOCK);
+    if (MODE != MODE_GLOBAL) __syncthreads();
+    const int64_t r = (int64_t)blockIdx.x * EYE_BLOCK + threadIdx.x;
+    if (r >= P.R.count) return;
+
+    Ray ray;
+    int64_t pixel;
+    if (P.pinhole) {
+        int px, py;
+        rec_to_pixel(r, P.W, &px, &py);
+        if (px >= P.W || py >= P.H) return;
+        pixel = (int64_t)py * P.W + px;
+        float sx = (2.0f * ((float)px + 0.5f)) / (float)P.W - 1.0f;
+        float sy = 1.0f - (2.0f * ((float)py + 0.5f)) / (float)P.H;
+        v3 d = xyz(P.fwd) + sx * xyz(P.right) + sy * xyz(P.up);
+        ray.o = xyz(P.eye);
+        ray.d = normalize(d);
+    } else {
+        pixel = r;
+        const float *q = P.rays + 6 * r;
+        ray.o = mk(q[0], q[1], q[2]);
+        ray.d = mk(q[3], q[4], q[5]);
+    }
+    ray.tmin = P.eps;
+    ray.tmax = RT_DEFAULT_MAX;
+
+    v3 L = mk(0.f, 0.f, 0.f);
+    Hit h;
+    if (traverse<false, MODE>(S, ray, h, stack, EYE_BLOCK)) {
+        const Geo g = shade(S, ray, h);
+        const v3 point = ray.o + ray.d * h.t;
+        const float4 m = S.materials[g.material];
+        const v3 fv = fbits(m.w) == PM_MATTE ? xyz(m) * INV_PI : mk(0.f, 0.f, 0.f); /* f(wo, wi) */
+        for (int i = 0; i < S.n_lights; ++i) {
+            const LightDev Lt = S.lights[i];
+            float u1 = 0.f, u2 = 0.f;
+            if (fbits(Lt.o_type.w) == PM_LIGHT_AREA_DISK) {
+                const int slot = fbits(Lt.p2_r2d.w); /* random2DStart + iSample 0 */
+                if (P.pinhole) {
+                    uint32_t o4[4];
+                    pmdm_philox4x32_10((uint32_t)pixel, (uint32_t)slot, 0u, 0u, P.light_seed, 0u, o4);
+                    u1 = pmdm_u01(o4[0]); u2 = pmdm_u01(o4[1]);
+                } else {
+                    const float *q = P.rand2d + ((size_t)pixel * P.n2d + slot) * 2;
+                    u1 = q[0]; u2 = q[1];
+                }
+            }
+            v3 uwi; float pdf;
+            const v3 li = sample_l_shading(Lt, point, u1, u2, &uwi, &pdf);
+            Ray sr;
+            sr.o = point; sr.d = uwi; sr.tmin = 0.001f; sr.tmax = 1.0f - 0.001f;
+            Hit sh;
+            const float atten = traverse<true, MODE>(S, sr, sh, stack, EYE_BLOCK) ? 0.0f : 1.0f;
+            const v3 wi = normalize(uwi);
+            L = L + (atten * fabsf(dot(g.ns, wi))) * fv * li;
+        }
+    }
+    const float y = 0.212671f * L.x + 0.715160f * L.y + 0.072169f * L.z; /* pbrt RGBSpectrum::y */
+    if (isnan(L.x) || isnan(L.y) || isnan(L.z) || y < -1e-5f || isinf(y)) L = mk(0.f, 0.f, 0.f);
+    out[3 * pixel + 0] = L.x;
+    out[3 * pixel + 1] = L.y;
+    out[3 * pixel + 2] = L.z;
+}
+
+hipError_t launch_simple(const EyeParams &p, float *out, hipStream_t s) {
+    if (p.R.count <= 0) return hipSuccess;
+    unsigned grid = (unsigned)((p.R.count + EYE_BLOCK - 1) / EYE_BLOCK);
+    const size_t lds = (size_t)p.S.stack_depth * EYE_BLOCK * 4 + p.S.lds_bytes;
+    switch (scene_mode(p.S)) {
+    case MODE_BRUTE: pm_launch(k_simple<MODE_BRUTE>, dim3(grid), dim3(EYE_BLOCK), lds, s, p, out); break;
+    case MODE_LDS: pm_launch(k_simple<MODE_LDS>, dim3(grid), dim3(EYE_BLOCK), lds, s, p, out); break;
+    default: pm_launch(k_simple<MODE_GLOBAL>, dim3(grid), dim3(EYE_BLOCK), lds, s, p, out); break;
+    }
+    return hipGetLastError();
+}
+
+/* ====================================================================== */
 /* photon pass                                                            */
 /* ====================================================================== */
 PMD void store_photon(pm_photon *dst, v3 p, v3 a, v3 wi) {

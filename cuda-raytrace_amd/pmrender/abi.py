@@ -58,6 +58,17 @@ class RenderParams(ctypes.Structure):
         p.rng_seed = 777             # cudarandom.h:15
         p.light_rng_seed = 2047
         p.gather_structure = PM_GATHER_GRID
+        return p._apply(kw)
+
+    @classmethod
+    def simple_defaults(cls, **kw):
+        """the SimpleRenderer's constants: scene_epsilon 0.01 (simplerender.cpp:23)"""
+        p = cls.defaults()
+        p.scene_epsilon = 0.01
+        return p._apply(kw)
+
+    def _apply(self, kw):
+        p = self
         for k, v in kw.items():
             if not hasattr(p, k):
                 raise AttributeError(f"unknown render parameter {k!r}")

@@ -55,6 +55,8 @@ def load_library(path=None):
         "pm_set_eye_rays": (c_int, [vp, P_f, i64, P_f, c_int]),
         "pm_commit": (c_int, [vp]),
         "pm_render": (c_int, [vp, ctypes.POINTER(RenderParams), P_f, ctypes.POINTER(Stats)]),
+        "pm_render_simple": (c_int, [vp, ctypes.POINTER(RenderParams), P_f, ctypes.POINTER(Stats)]),
+        "pm_simple_pass": (c_int, [vp, ctypes.POINTER(RenderParams), vp, vp]),
         "pm_eye_pass": (c_int, [vp, ctypes.POINTER(RenderParams), vp]),
         "pm_trace_photons": (c_int, [vp, ctypes.POINTER(RenderParams), c_int, i64, i64, i64, vp]),
         "pm_build_photon_map": (c_int, [vp, ctypes.POINTER(RenderParams), i64, vp]),
@@ -202,6 +204,20 @@ class Context:
         if self.pinhole:
             out = out.reshape(self.height, self.width, 3)
         return out, st.as_dict()
+
+    def render_simple(self, params=None):
+        """SimpleRenderer (simplerender.cpp:18-103): direct light only."""
+        params = params or RenderParams.simple_defaults()
+        n = self.width * self.height if self.pinhole else self.num_records()
+        out = np.zeros((n, 3), np.float32)
+        st = Stats()
+        self._chk(self.lib.pm_render_simple(self.h, ctypes.byref(params), fptr(out), ctypes.byref(st)))
+        if self.pinhole:
+            out = out.reshape(self.height, self.width, 3)
+        return out, st.as_dict()
+
+    def simple_pass(self, params, d_out, stream=None):
+        self._chk(self.lib.pm_simple_pass(self.h, ctypes.byref(params), d_out, stream))
 
     # ---- stages ---------------------------------------------------------------
     def eye_pass(self, params, stream=None):

@@ -29,6 +29,7 @@
  *   pm_build_photon_map           CreatePhotonMap                  photonmappingrenderer.cpp:150-180
  *   pm_gather                     PhotonGatheringPass              photonmappingrenderer.cpp:228-232 (+ gathering.cu:104-126)
  *   pm_final                      FinalGatheringPass               photonmappingrenderer.cpp:234-277 (+ gathering.cu:129-146)
+ *   pm_render_simple              SimpleRenderer::render           simple_render/simplerender.cpp:18-103 (+ simplerender.cu)
  */
 #ifndef PM_API_H
 #define PM_API_H
@@ -172,6 +173,19 @@ int pm_commit(void *ctx);
  * raster order), NaN/negative/inf sanitized to black like
  * photonmappingrenderer.cpp:251-268. stats may be NULL. */
 int pm_render(void *ctx, const pm_render_params *params, float *out_rgb, pm_stats *stats);
+
+/* ---- simple renderer (SimpleRenderer::render, simple_render/simplerender.cpp:18-103)
+ * Direct light only: closest hit of each eye sample, one shadow-tested sample
+ * per light (sample index 0, no pdf division, no emitted term,
+ * simplerender.cu:40-72), miss = black; NaN / negative / inf sanitized like
+ * simplerender.cpp:70-87. The reference sets scene_epsilon to 0.01 for it
+ * (simplerender.cpp:23, PM_SIMPLE_SCENE_EPSILON); params->scene_epsilon is
+ * used as given, and params->light_rng_seed feeds the pinhole mode's disk
+ * samples. out_rgb as pm_render. */
+#define PM_SIMPLE_SCENE_EPSILON 0.01f
+int pm_render_simple(void *ctx, const pm_render_params *params, float *out_rgb, pm_stats *stats);
+/* the same into a device buffer (float3 per output sample) on `stream` */
+int pm_simple_pass(void *ctx, const pm_render_params *params, void *d_out, void *stream);
 
 /* ---- stage-level API (device-resident state, explicit stream) ---------- */
 /* `stream` is a hipStream_t (NULL = the context's own stream). */

@@ -55,6 +55,7 @@ def load():
         "orc_gather_partial": (None, [vp, vp, i64, vp, i64, vp, c_int]),
         "orc_final": (None, [vp, vp, i64, c_double, P_f, c_int]),
         "orc_render": (c_int, [vp, RP, P_f, ctypes.POINTER(Stats), c_int]),
+        "orc_render_simple": (None, [vp, RP, P_f, c_int]),
         "orc_concentric_sample_disk": (None, [c_float, c_float, P_f]),
         "orc_uniform_sample_sphere": (None, [c_float, c_float, P_f]),
         "orc_intersect_triangle": (c_int, [P_f, P_f, P_f, P_f, P_f, c_float, c_float, P_f]),
@@ -189,6 +190,13 @@ class Oracle:
         if self.pinhole:
             out = out.reshape(self.height, self.width, 3)
         return out, st.as_dict()
+
+    def render_simple(self, params):
+        """SimpleRenderer (simplerender.cpp:18-103): direct light only."""
+        n = self.width * self.height if self.pinhole else self.num_records()
+        out = np.zeros((n, 3), np.float32)
+        self.lib.orc_render_simple(self.h, ctypes.byref(params), fptr(out), self.nthreads)
+        return out.reshape(self.height, self.width, 3) if self.pinhole else out
 
 
 # ---- primitive KAT helpers ---------------------------------------------------

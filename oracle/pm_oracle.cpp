@@ -693,6 +693,64 @@ void eye_record(const Scene &S, const pm_render_params &P, int64_t r, pm_record 
     rec->dl[0] = L.x; rec->dl[1] = L.y; rec->dl[2] = L.z;
 }
 
+/* ------------------------------------------------------- simple renderer
+ * simple_render/simplerender.cu:26-79 (simple_camera, simple_cloest_hit,
+ * simple_miss, simple_shadow_any_hit) + the host check of
+ * simplerender.cpp:70-87. Writes the sample's output in output order. */
+void simple_sample(const Scene &S, const pm_render_params &P, int64_t r, float *out_rgb) {
+    Ray ray;
+    int64_t pixel;
+    if (S.pinhole) {
+        int px, py;
+        rec_to_pixel(r, S.W, &px, &py);
+        if (px >= S.W || py >= S.H) return;
+        pixel = (int64_t)py * S.W + px;
+        float sx = (2.0f * ((float)px + 0.5f)) / (float)S.W - 1.0f;
+        float sy = 1.0f - (2.0f * ((float)py + 0.5f)) / (float)S.H;
+        f3 d = S.fwd + sx * S.right + sy * S.up;
+        ray.o = S.eye;
+        ray.d = normalize(d);
+    } else {
+        pixel = r;
+        ray.o = ld3(&S.rays[6 * r]);
+        ray.d = ld3(&S.rays[6 * r + 3]);
+    }
+    ray.tmin = P.scene_epsilon; /* simple_camera: Ray(o, d, 0, scene_epsilon) :26-32 */
+    ray.tmax = RT_DEFAULT_MAX;
+    f3 L = mk(0.f, 0.f, 0.f);
+    Hit h;
+    if (closest_hit(S, ray, &h)) {
+        const Geo g = shade(S, ray, h);
+        const f3 point = ray.o + ray.d * h.t;            /* :46 */
+        const f3 fv = bsdf_f(S, g.material);            /* f(wo, wi): Lambert Kd/pi, else black */
+        for (int i = 0; i < (int)S.lights.size(); ++i) { /* :53-72 */
+            const Light &Lt = S.lights[i];
+            float u1 = 0.f, u2 = 0.f;
+            if (Lt.type == PM_LIGHT_AREA_DISK) {
+                int slot = Lt.rand2d_start; /* Sample_L(i, point, uwi, pdf, 0) */
+                if (S.pinhole) {
+                    uint32_t o4[4];
+                    pmdm_philox4x32_10((uint32_t)pixel, (uint32_t)slot, 0u, 0u, P.light_rng_seed, 0u, o4);
+                    u1 = pmdm_u01(o4[0]); u2 = pmdm_u01(o4[1]);
+                } else {
+                    const float *q = &S.rand2d[((size_t)pixel * S.n2d + slot) * 2];
+                    u1 = q[0]; u2 = q[1];
+                }
+            }
+            f3 uwi; float pdf;
+            f3 li = sample_l_shading(Lt, point, u1, u2, &uwi, &pdf);
+            Ray sr{point, uwi, 0.001f, 1.0f - 0.001f};
+            float atten = any_hit(S, sr) ? 0.0f : 1.0f;
+            f3 wi = normalize(uwi);
+            L = L + (atten * fabsf(dot(g.ns, wi))) * fv * li;
+        }
+    }
+    float y = 0.212671f * L.x + 0.715160f * L.y + 0.072169f * L.z; /* pbrt RGBSpectrum::y */
+    if (std::isnan(L.x) || std::isnan(L.y) || std::isnan(L.z) || y < -1e-5f || std::isinf(y))
+        L = mk(0.f, 0.f, 0.f);
+    out_rgb[3 * pixel + 0] = L.x; out_rgb[3 * pixel + 1] = L.y; out_rgb[3 * pixel + 2] = L.z;
+}
+
 /* ------------------------------------------------------------ photon pass
  * photontracing.cu:80-185 with the recursion unrolled into a loop. */
 void trace_path(const Scene &S, const pm_render_params &P, const uint32_t *perm, int pass,
@@ -1104,6 +1162,13 @@ int orc_render(void *s, const pm_render_params *P, float *out_rgb, pm_stats *st,
         st->photons_in_radius = counters[1];
     }
     return PM_OK;
+}
+
+/* SimpleRenderer::render (simple_render/simplerender.cpp:18-103); out_rgb in
+ * output order (raster for pinhole, ray order otherwise), zero-initialised */
+void orc_render_simple(void *s, const pm_render_params *P, float *out_rgb, int nthreads) {
+    Scene &S = *(Scene *)s;
+    parallel_for(num_records(S), nthreads, [&](int64_t r) { simple_sample(S, *P, r, out_rgb); });
 }
 
 /* ---- primitive entry points for known-answer tests -------------------- */
