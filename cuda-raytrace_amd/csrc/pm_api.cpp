@@ -937,7 +937,7 @@ int pm_build_photon_map(void *ptr, const pm_render_params *p, int64_t n_slots, v
 }
 
 static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, int64_t rec_begin, int64_t rec_count,
-                         void *stream) {
+                         void *stream, int *count = nullptr, long long *flux = nullptr) {
     int rc;
     if ((rc = check_params(c, p))) return rc;
     if (c->nrec <= 0) FAIL(c, PM_ERR_INVALID, "no records (run pm_eye_pass first)");
@@ -946,16 +946,21 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
     hipStream_t s = pick(c, stream);
     GatherParams G = gather_params(c, p);
     G.partial = partial;
+    G.count = count;
+    G.flux = flux;
     G.rec_begin = rec_begin;
     G.rec_end = rec_begin + rec_count;
     /* a pending reset is consumed by a fused gather over all records (it starts
-     * from the initial PPM state and writes it); any other gather needs it applied */
-    const bool consume = c->rec_fresh && !partial && rec_begin == 0 && rec_count == c->nrec;
-    if (consume) { G.fresh = 1; G.r2init = c->rec_fresh_r2; }
+     * from the initial PPM state and writes it); a split partial gather reads
+     * the initial radius and leaves the reset to pm_ppm_update_split, which
+     * writes every view record; any other gather needs it applied */
+    const bool split = count != nullptr;
+    const bool consume = c->rec_fresh && !partial && !split && rec_begin == 0 && rec_count == c->nrec;
+    if (consume || (split && c->rec_fresh)) { G.fresh = 1; G.r2init = c->rec_fresh_r2; }
     else if ((rc = materialize_reset(c, s))) return rc;
     if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters.p, 0, 32, s));
     timer_begin(c, "gather", s);
-    HIPCHK(c, launch_gather(G, p->gather_structure, partial != nullptr, c->counting, s));
+    HIPCHK(c, launch_gather(G, p->gather_structure, partial != nullptr || split, c->counting, s));
     timer_end(c, "gather", s);
     if (consume) c->rec_fresh = false;
     return PM_OK;
@@ -975,6 +980,32 @@ int pm_gather_partial(void *ptr, const pm_render_params *p, void *d_partial, voi
     GETCTX(ptr);
     if (!d_partial) FAIL(c, PM_ERR_INVALID, "null partial buffer");
     return gather_common(c, p, (long long *)d_partial, 0, c->nrec, stream);
+}
+
+int pm_gather_split(void *ptr, const pm_render_params *p, void *d_count, void *d_flux, void *stream) {
+    GETCTX(ptr);
+    if (!d_count || !d_flux) FAIL(c, PM_ERR_INVALID, "null count / flux buffer");
+    return gather_common(c, p, nullptr, 0, c->nrec, stream, (int *)d_count, (long long *)d_flux);
+}
+
+int pm_ppm_update_split(void *ptr, const pm_render_params *p, const void *d_count, const void *d_flux_chunk,
+                        int64_t v_begin, int64_t v_count, void *stream) {
+    GETCTX(ptr);
+    int rc;
+    if ((rc = check_params(c, p))) return rc;
+    const int64_t n = view_size(c);
+    if (!d_count || (v_count > 0 && !d_flux_chunk) || v_begin < 0 || v_count < 0 || v_begin + v_count > n)
+        FAIL(c, PM_ERR_INVALID, "bad view chunk");
+    hipStream_t s = pick(c, stream);
+    GatherParams G = gather_params(c, p);
+    const int fresh = c->rec_fresh ? 1 : 0;
+    G.r2init = c->rec_fresh_r2;
+    timer_begin(c, "update", s);
+    HIPCHK(c, launch_ppm_update_split(G, (const int *)d_count, (const long long *)d_flux_chunk, n, v_begin, v_count,
+                                      fresh, s));
+    timer_end(c, "update", s);
+    c->rec_fresh = false; /* every view record written (records outside the view are inactive) */
+    return PM_OK;
 }
 
 int pm_ppm_update(void *ptr, const pm_render_params *p, const void *d_partial, int64_t rec_begin, int64_t rec_count,

@@ -38,14 +38,23 @@ PMD void ppm_apply(float4 &st, float &N, int M, v3 L, float alpha) {
 struct Fx3 { long long x, y, z; };
 /* where record r's partial goes: its rank in the record view (active records
  * only, -1 = not in the view) or r itself (all-records view) */
-PMD long long *partial_slot(const GatherParams &P, int64_t r) {
-    if (!P.view_rank) return P.partial + 4 * r;
+PMD int64_t partial_index(const GatherParams &P, int64_t r) {
+    if (!P.view_rank) return r;
     const uint32_t k = P.view_rank[r];
-    return k == 0xffffffffu ? nullptr : P.partial + 4 * (int64_t)k;
+    return k == 0xffffffffu ? -1 : (int64_t)k;
 }
 PMD long long to_fx(float c, float scale) { return (long long)rintf(c * scale); }
-PMD void write_partial(long long *p, int M, Fx3 L) {
-    longlong2 *q = reinterpret_cast<longlong2 *>(p);
+/* partial of view record k: (M, L) as four int64, or split into an int32
+ * count and three int64 flux words (the "reduce" exchange's layout) */
+PMD void write_partial(const GatherParams &P, int64_t k, int M, Fx3 L) {
+    if (k < 0) return;
+    if (P.count) {
+        P.count[k] = M;
+        long long *f = P.flux + 3 * k;
+        f[0] = L.x; f[1] = L.y; f[2] = L.z;
+        return;
+    }
+    longlong2 *q = reinterpret_cast<longlong2 *>(P.partial + 4 * k);
     q[0] = make_longlong2((long long)M, L.x);
     q[1] = make_longlong2(L.y, L.z);
 }
@@ -61,7 +70,7 @@ __global__ __launch_bounds__(GATHER_BLOCK, 8) void k_gather_grid(GatherParams P)
         float4 pos = P.R.pos[r];
         uint32_t flags = (uint32_t)__float_as_int(pos.w);
         if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) {
-            if (PARTIAL) { if (long long *q = partial_slot(P, r)) write_partial(q, 0, Fx3{0, 0, 0}); }
+            if (PARTIAL) write_partial(P, partial_index(P, r), 0, Fx3{0, 0, 0});
         } else {
             float4 st = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : P.R.state[r];
             float4 nrm = P.R.nrm[r];
@@ -124,7 +133,7 @@ __global__ __launch_bounds__(GATHER_BLOCK, 8) void k_gather_grid(GatherParams P)
             }
             if (COUNT) { hits += (unsigned long long)M; act++; }
             if (PARTIAL) {
-                write_partial(partial_slot(P, r), M, Lf);
+                write_partial(P, partial_index(P, r), M, Lf);
             } else {
                 const double inv = P.fx_inv;
                 v3 L = mk((float)((double)Lf.x * inv), (float)((double)Lf.y * inv), (float)((double)Lf.z * inv));
@@ -149,7 +158,7 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_kd(GatherParams P) {
         float4 pos = P.R.pos[r];
         uint32_t flags = (uint32_t)__float_as_int(pos.w);
         if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) {
-            if (PARTIAL) { if (long long *q = partial_slot(P, r)) write_partial(q, 0, Fx3{0, 0, 0}); }
+            if (PARTIAL) write_partial(P, partial_index(P, r), 0, Fx3{0, 0, 0});
         } else {
             float4 st = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : P.R.state[r];
             float4 nrm = P.R.nrm[r];
@@ -200,7 +209,7 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_kd(GatherParams P) {
             if (COUNT) { hits += (unsigned long long)M; act++; }
             if (PARTIAL) {
                 const float sc = P.fx_scale;
-                write_partial(partial_slot(P, r), M, Fx3{to_fx(L.x, sc), to_fx(L.y, sc), to_fx(L.z, sc)});
+                write_partial(P, partial_index(P, r), M, Fx3{to_fx(L.x, sc), to_fx(L.y, sc), to_fx(L.z, sc)});
             } else {
                 float N = P.fresh ? 0.f : P.R.n[r];
                 ppm_apply(st, N, M, L, P.ppm_alpha);
@@ -281,6 +290,43 @@ hipError_t launch_ppm_update(const GatherParams &p, const long long *partial, in
     if (rec_count <= 0) return hipSuccess;
     pm_launch(k_ppm_update, dim3((unsigned)((rec_count + 255) / 256)), dim3(256), 0, s, p.R, partial,
                        rec_begin, rec_count, p.ppm_alpha, p.fx_inv, p.view_list);
+    return hipGetLastError();
+}
+
+/* PPM update of the split exchange: every rank holds the global photon
+ * count M of every view record (all-reduced), so it updates every radius and
+ * photon count itself — no radius exchange — while the summed flux arrives
+ * only for its own chunk [v_begin, v_begin + v_count) (reduce-scattered).
+ * fresh: the records are in a deferred reset — start from the initial state
+ * and write every view record. */
+__global__ __launch_bounds__(256) void k_ppm_update_split(RecordsDev R, const int *count, const long long *flux,
+                                                          int64_t n_view, int64_t v_begin, int64_t v_count, float alpha,
+                                                          double inv, const uint32_t *view, int fresh, float r2init) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_view) return;
+    const int64_t r = view ? (int64_t)view[i] : i;
+    const uint32_t flags = (uint32_t)__float_as_int(R.pos[r].w);
+    if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) return;
+    const int M = count[i];
+    if (M <= 0 && !fresh) return;
+    float4 st = fresh ? make_float4(0.f, 0.f, 0.f, r2init) : R.state[r];
+    float N = fresh ? 0.f : R.n[r];
+    v3 L = mk(0.f, 0.f, 0.f);
+    const int64_t k = i - v_begin;
+    if (k >= 0 && k < v_count) {
+        const long long *f = flux + 3 * k;
+        L = mk((float)((double)f[0] * inv), (float)((double)f[1] * inv), (float)((double)f[2] * inv));
+    }
+    ppm_apply(st, N, M, L, alpha);
+    R.state[r] = st;
+    R.n[r] = N;
+}
+
+hipError_t launch_ppm_update_split(const GatherParams &p, const int *count, const long long *flux, int64_t n_view,
+                                   int64_t v_begin, int64_t v_count, int fresh, hipStream_t s) {
+    if (n_view <= 0) return hipSuccess;
+    pm_launch(k_ppm_update_split, dim3((unsigned)((n_view + 255) / 256)), dim3(256), 0, s, p.R, count, flux, n_view,
+              v_begin, v_count, p.ppm_alpha, p.fx_inv, p.view_list, fresh, p.r2init);
     return hipGetLastError();
 }
 

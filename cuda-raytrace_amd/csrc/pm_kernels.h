@@ -109,8 +109,11 @@ struct GatherParams {
     /* fixed-point flux: contribution c -> rint(c * fx_scale), fx_inv = 1/fx_scale (2^-S) */
     float fx_scale;
     double fx_inv;
-    /* partial mode: per record int64 (M, L.x, L.y, L.z) in fixed point */
+    /* partial mode: per record int64 (M, L.x, L.y, L.z) in fixed point, or
+     * (count != null) split: int32 M in count[k], three int64 in flux[3k..] */
     long long *partial;
+    int *count;
+    long long *flux;
     /* fresh: records are in a deferred reset (pm_reset_records): read the
      * initial PPM state (flux 0, N 0, r2init) instead of memory, write it back */
     int fresh;
@@ -153,6 +156,8 @@ hipError_t launch_bucket_build(const pm_photon *slots, int64_t n, GridDesc g, ui
 hipError_t launch_gather(const GatherParams &p, int structure, int partial, int count, hipStream_t s);
 hipError_t launch_ppm_update(const GatherParams &p, const long long *partial, int64_t rec_begin, int64_t rec_count,
                              hipStream_t s);
+hipError_t launch_ppm_update_split(const GatherParams &p, const int *count, const long long *flux, int64_t n_view,
+                                   int64_t v_begin, int64_t v_count, int fresh, hipStream_t s);
 hipError_t launch_final(const FinalParams &p, hipStream_t s);
 hipError_t launch_radius2_io(const RecordsDev &R, float *buf, int64_t rec_begin, int64_t rec_count, int to_records,
                              const uint32_t *view, hipStream_t s);

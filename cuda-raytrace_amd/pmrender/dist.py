@@ -13,14 +13,17 @@ Work split:
 Two exchange strategies:
   * "reduce" (default): each rank builds a map of ITS photons and gathers all
     records against it; the PPM estimator's sums (M, L) are linear in the
-    photon set, so a reduce-scatter of one int64x4 per active record (M and
-    the flux in the gather's exact fixed point) gives every owner the global
-    (M, L) of its chunk, bit-identical to a 1-GPU gather; the owner then
-    applies the PPM update and the new radii are all-gathered. Bytes on xGMI
-    per pass: 32 B + 4 B per active record (39 MB at 1080p), independent of
-    the photon count. The reduce-scatter is issued asynchronously and only
-    waited for after the NEXT pass's trace and bucket build (which do not
-    read records), so it overlaps them; flush() completes the last one.
+    photon set, so summing the per-rank partials (M as int32, the flux as
+    three int64 in the gather's exact fixed point) gives the 1-GPU result
+    bit for bit. The radius / photon-count update needs only M, so the
+    counts are ALL-REDUCED and every rank updates every radius itself (no
+    radius exchange); the flux is REDUCE-SCATTERED to the owner of each
+    view chunk, which updates its flux. Bytes on xGMI per pass: 4 B
+    (all-reduce) + 24 B (reduce-scatter) per active record, independent of
+    the photon count. Both collectives are issued asynchronously right after
+    the gather and only waited for after the NEXT pass's trace and bucket
+    build (which do not read records), so they overlap them; flush()
+    completes the last one.
   * "allgather": the reference-style exchange: all-gather the
     40-B photon slots into a replicated map, gather locally owned chunks.
     Bytes per pass: 40 B x slots x (N-1)/N per rank.
@@ -84,6 +87,12 @@ class HipEngine:
     def gather_partial(self, p, out):
         self.ctx.gather_partial(p, out.data_ptr(), self._s())
 
+    def gather_split(self, p, count, flux):
+        self.ctx.gather_split(p, count.data_ptr(), flux.data_ptr(), self._s())
+
+    def ppm_update_split(self, p, count, flux_chunk, v_begin, v_count):
+        self.ctx.ppm_update_split(p, count.data_ptr(), flux_chunk.data_ptr(), v_begin, v_count, self._s())
+
     def ppm_update(self, p, partial, rec_begin, rec_count):
         self.ctx.ppm_update(p, partial.data_ptr(), rec_begin, rec_count, self._s())
 
@@ -115,19 +124,18 @@ class PassRunner:
         self.n_records = n
         self.rec_begin, self.rec_count, self.rec_per = _chunk(n, world, rank)   # final image split
         self.padded = self.rec_per * world
-        self.partial = None
-        self.chunk = None
         self.slot_buf = None
         self._pending = None
         if world > 1 and exchange == "reduce":
             # exchange over the active records only, owned in contiguous chunks of the view
             self.n_view = engine.set_record_view(True)
             self.v_begin, self.v_count, self.v_per = _chunk(self.n_view, world, rank)
-            # per active record (M, L.rgb) as int64 fixed point: the sum over ranks is exact;
-            # rows past n_view stay zero
-            self.partial = engine.alloc((self.v_per * world, 4), torch.int64)
-            self.chunk = engine.alloc((self.v_per, 4), torch.int64)
-            self.r2_all = engine.alloc((self.v_per * world,), torch.float32)
+            # per active record: photon count M (int32, all-reduced) and flux L.rgb
+            # (int64 fixed point, reduce-scattered); the sums over ranks are exact.
+            # Rows past n_view stay zero.
+            self.count = engine.alloc((self.v_per * world,), torch.int32)
+            self.flux = engine.alloc((self.v_per * world, 3), torch.int64)
+            self.flux_chunk = engine.alloc((self.v_per, 3), torch.int64)
         if world > 1 and exchange == "allgather":
             self.slot_buf = engine.alloc((world * self.slots_per_rank * PHOTON_DTYPE.itemsize,), torch.uint8)
             engine.use_slot_buffer(self.slot_buf)
@@ -154,26 +162,25 @@ class PassRunner:
         if self._gloo():
             self._pending = ("gloo", None)   # done synchronously in _finish_exchange
         else:
-            self._pending = ("rs", dist.reduce_scatter_tensor(self.chunk, self.partial, async_op=True))
+            self._pending = ("rccl", [dist.all_reduce(self.count, async_op=True),
+                                      dist.reduce_scatter_tensor(self.flux_chunk, self.flux, async_op=True)])
 
     def _finish_exchange(self):
-        """Complete the previous pass: summed (M, L) -> owner PPM update -> radii to every rank."""
+        """Complete the previous pass: global counts -> every radius; summed flux -> owner's chunk."""
         if self._pending is None:
             return
-        kind, work = self._pending
+        kind, works = self._pending
         self._pending = None
-        if kind == "gloo":                   # all-reduce + slice
-            host = self.partial.cpu()
-            dist.all_reduce(host)
-            self.chunk.copy_(host[self.rank * self.v_per:(self.rank + 1) * self.v_per])
+        if kind == "gloo":                   # gloo has no reduce_scatter: all-reduce + slice, via host
+            for t in (self.count, self.flux):
+                host = t.cpu()
+                dist.all_reduce(host)
+                t.copy_(host)
+            self.flux_chunk.copy_(self.flux[self.rank * self.v_per:(self.rank + 1) * self.v_per])
         else:
-            work.wait()                      # the compute stream waits for the collective
-        e, p = self.e, self.p
-        e.ppm_update(p, self.chunk, self.v_begin, self.v_count)
-        mine = self.r2_all[self.rank * self.v_per:(self.rank + 1) * self.v_per]
-        e.get_radius2(self.v_begin, self.v_count, mine)
-        self._all_gather(self.r2_all, mine)
-        e.set_radius2(self.r2_all, 0, self.n_view)
+            for w in works:
+                w.wait()                     # the compute stream waits for the collectives
+        self.e.ppm_update_split(self.p, self.count, self.flux_chunk, self.v_begin, self.v_count)
 
     def flush(self):
         """Finish the exchange still in flight (call before reading records or timing)."""
@@ -196,7 +203,7 @@ class PassRunner:
             self._finish_exchange()
             if reset:
                 e.reset_records(p)
-            e.gather_partial(p, self.partial)
+            e.gather_split(p, self.count, self.flux)
             self._start_exchange()
         else:
             if reset:

@@ -62,6 +62,8 @@ def load_library(path=None):
         "pm_build_photon_map": (c_int, [vp, ctypes.POINTER(RenderParams), i64, vp]),
         "pm_gather": (c_int, [vp, ctypes.POINTER(RenderParams), vp]),
         "pm_gather_partial": (c_int, [vp, ctypes.POINTER(RenderParams), vp, vp]),
+        "pm_gather_split": (c_int, [vp, ctypes.POINTER(RenderParams), vp, vp, vp]),
+        "pm_ppm_update_split": (c_int, [vp, ctypes.POINTER(RenderParams), vp, vp, i64, i64, vp]),
         "pm_ppm_update": (c_int, [vp, ctypes.POINTER(RenderParams), vp, i64, i64, vp]),
         "pm_final": (c_int, [vp, c_double, i64, i64, vp, vp]),
         "pm_num_records": (i64, [vp]),
@@ -243,6 +245,13 @@ class Context:
 
     def gather_partial(self, params, d_partial, stream=None):
         self._chk(self.lib.pm_gather_partial(self.h, ctypes.byref(params), ctypes.c_void_p(d_partial), stream))
+
+    def gather_split(self, params, d_count, d_flux, stream=None):
+        self._chk(self.lib.pm_gather_split(self.h, ctypes.byref(params), d_count, d_flux, stream))
+
+    def ppm_update_split(self, params, d_count, d_flux_chunk, v_begin, v_count, stream=None):
+        self._chk(self.lib.pm_ppm_update_split(self.h, ctypes.byref(params), d_count, d_flux_chunk, int(v_begin),
+                                               int(v_count), stream))
 
     def ppm_update(self, params, d_partial, rec_begin, rec_count, stream=None):
         self._chk(self.lib.pm_ppm_update(self.h, ctypes.byref(params), ctypes.c_void_p(d_partial), int(rec_begin),

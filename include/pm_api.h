@@ -207,6 +207,20 @@ int pm_gather_range(void *ctx, const pm_render_params *params, int64_t rec_begin
  * pm_set_record_view); L is in the gather's exact fixed point, so partials of
  * photon shards sum to the 1-GPU result. */
 int pm_gather_partial(void *ctx, const pm_render_params *params, void *d_partial, void *stream);
+/* The "reduce" exchange's split partials: per view record an int32 photon
+ * count M (d_count, n_view entries) and the flux sum as three int64 in the
+ * gather's fixed point (d_flux, 3 x n_view, record-major). Summed over the
+ * photon shards they equal a 1-GPU gather exactly. A pending pm_reset_records
+ * is honoured (initial radius) and left to pm_ppm_update_split. */
+int pm_gather_split(void *ctx, const pm_render_params *params, void *d_count, void *d_flux, void *stream);
+/* PPM update (gathering.cu:115-125) from split partials summed over ranks:
+ * radius2 and photon count of EVERY view record from the global counts
+ * (d_count, n_view int32: all-reduced, so every rank updates every radius
+ * itself and no radius exchange is needed), flux of view records
+ * [v_begin, v_begin + v_count) from d_flux_chunk (3 int64 each:
+ * reduce-scattered to the owner). Consumes a pending pm_reset_records. */
+int pm_ppm_update_split(void *ctx, const pm_render_params *params, const void *d_count, const void *d_flux_chunk,
+                        int64_t v_begin, int64_t v_count, void *stream);
 /* Record view of pm_gather_partial, pm_ppm_update, pm_get_radius2 and
  * pm_set_radius2 (their rec_begin / rec_count and buffers index the view):
  * active_only = 0 -> all records (default); 1 -> only active records (not

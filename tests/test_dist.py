@@ -101,6 +101,37 @@ class OracleEngine:
             self.recs[ri]["radius2"], self.recs[ri]["photon_count"] = r2[0], N[0]
             self.recs[ri]["flux"] = flux
 
+    def gather_split(self, p, count, flux):
+        part = self.orc.gather_partial(self.nodes, self.recs)
+        if self.view is not None:
+            part = part[self.view]
+        n = len(part)
+        count[:n] = torch.from_numpy(part[:, 0].astype(np.int32))
+        flux[:n] = torch.from_numpy(np.rint(part[:, 1:].astype(np.float64) * self.FX).astype(np.int64))
+
+    def ppm_update_split(self, p, count, flux_chunk, v_begin, v_count):
+        """every view record's radius / photon count from the global counts;
+        flux from the summed chunk for [v_begin, v_begin + v_count) only"""
+        import ctypes
+        lib = self.oracle.load()
+        fp = ctypes.POINTER(ctypes.c_float)
+        C, F = count.numpy(), flux_chunk.numpy()
+        n_view = len(self.view) if self.view is not None else len(self.recs)
+        for i in range(n_view):
+            ri = self._rec(i)
+            r = self.recs[ri]
+            if r["flags"] & 7 or C[i] <= 0:
+                continue
+            r2 = np.float32([r["radius2"]])
+            N = np.float32([r["photon_count"]])
+            fl = np.ascontiguousarray(r["flux"], np.float32)
+            own = v_begin <= i < v_begin + v_count
+            L = (F[i - v_begin].astype(np.float64) / self.FX).astype(np.float32) if own else np.zeros(3, np.float32)
+            lib.orc_ppm_update(r2.ctypes.data_as(fp), N.ctypes.data_as(fp), fl.ctypes.data_as(fp), int(C[i]),
+                               L.ctypes.data_as(fp), float(p.ppm_alpha))
+            self.recs[ri]["radius2"], self.recs[ri]["photon_count"] = r2[0], N[0]
+            self.recs[ri]["flux"] = fl
+
     def get_radius2(self, b, n, out):
         idx = self.view[b:b + n] if self.view is not None else np.arange(b, b + n)
         out[:n] = torch.from_numpy(self.recs["radius2"][idx].copy())
