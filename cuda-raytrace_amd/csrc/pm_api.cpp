@@ -103,6 +103,7 @@ struct Ctx {
     int64_t trace_wave_paths = 64; /* per-lane kernel: paths per wave (env PM_TRACE_WAVE_PATHS) */
     int trace_refill_min = 32;     /* per-lane kernel: idle lanes that trigger a refill (env PM_TRACE_REFILL_MIN) */
     bool fuse_count = true;        /* bucket counting inside the trace kernel (env PM_FUSE_COUNT=0 disables) */
+    bool gather_wave = false;      /* wave-cooperative bucket gather (env PM_GATHER_WAVE=1; measured 2x slower) */
     /* leading words of d_count known to be zero (the bucket scan clears the
      * counters it reads); valid while d_count.p == count_zero_ptr */
     size_t count_zero_words = 0;
@@ -306,6 +307,7 @@ GatherParams gather_params(Ctx *c, const pm_render_params *p) {
     G.ph_a = c->d_pha.as<float4>(); G.ph_b = c->d_phb.as<float4>();
     G.kd_nodes = c->d_kd.as<pm_photon>(); G.kd_count = c->kd_count;
     G.counters = c->d_counters.as<unsigned long long>();
+    G.wave = c->gather_wave ? 1 : 0;
     if (c->view_active) { G.view_rank = c->d_vrank.as<uint32_t>(); G.view_list = c->d_vlist.as<uint32_t>(); }
     /* fixed-point scale 2^S: a single contribution is bounded by
      * alpha_max * Kd_max / pi with alpha_max = emission * Kd_max^mpc (Lambert
@@ -396,6 +398,7 @@ int pm_create(void **out, const pm_config *cfg) {
     if (const char *e = getenv("PM_TRACE_WAVE_PATHS")) c->trace_wave_paths = std::max(64LL, atoll(e));
     if (const char *e = getenv("PM_TRACE_REFILL_MIN")) c->trace_refill_min = std::max(1, std::min(64, atoi(e)));
     if (const char *e = getenv("PM_FUSE_COUNT")) c->fuse_count = atoi(e) != 0;
+    if (const char *e = getenv("PM_GATHER_WAVE")) c->gather_wave = atoi(e) != 0;
     if (const char *e = getenv("PM_STAGE_TIMERS")) if (atoi(e) == 0) c->timed_stages.clear();
     (void)hipSetDevice(dev);
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);

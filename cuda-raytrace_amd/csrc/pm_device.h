@@ -344,6 +344,8 @@ PMD void consider(Hit &best, float t, float b, float g, uint32_t ref, uint32_t g
  * lane: broadcast LDS reads, no divergence, no stack) */
 typedef const float __attribute__((address_space(4))) *const_f32_ptr;
 typedef const uint32_t __attribute__((address_space(4))) *const_u32_ptr;
+/* 16 B through the scalar cache (wave-uniform address) */
+PMD float4 ldc4(const_f32_ptr q) { return make_float4(q[0], q[1], q[2], q[3]); }
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 PMD f2 bc2(float x) { return f2{x, x}; }

@@ -122,6 +122,8 @@ struct GatherParams {
      * view_list[i] = record of view position i (update); null = all records */
     const uint32_t *view_rank;
     const uint32_t *view_list;
+    /* grid gather kernel: 1 = wave-cooperative (k_gather_wave, experiment), 0 = per lane (k_gather_grid, default) */
+    int wave;
     unsigned long long *counters; /* [0] visited, [1] in radius */
 };
 

@@ -170,6 +170,38 @@ def test_grid_gather_parity(cornell, radius2):
     compare_gathered_records(ctx.download_records(), ref)
 
 
+@pytest.mark.parametrize("radius2", [4.0, 25.0, 400.0])
+def test_wave_gather_equals_lane_gather(radius2, oracle_mod, hip_mod, monkeypatch):
+    """The wave-cooperative bucket gather (default) and the per-lane kernel
+    (PM_GATHER_WAVE=0) find the same photons: fused records and split
+    partials bit-identical. radius2 400 exceeds the grid's design radius for
+    uploaded records -> the wave kernel's per-lane fallback."""
+    torch = pytest.importorskip("torch")
+    sc = scenes.cornell_box(64, 48)
+    orc = sc.load_into(oracle_mod.Oracle())
+    p, recs, slots = _gather_inputs(orc, radius2=radius2)
+    p.gather_structure = PM_GATHER_GRID
+    outs = []
+    for wave in ("1", "0"):
+        monkeypatch.setenv("PM_GATHER_WAVE", wave)
+        ctx = sc.load_into(hip_mod.Context(0))
+        try:
+            ctx.upload_records(recs)
+            ctx.upload_slots(slots)
+            ctx.build_photon_map(p, len(slots))
+            part = torch.zeros((len(recs), 4), dtype=torch.int64, device="cuda")
+            torch.cuda.synchronize()
+            ctx.gather_partial(p, part.data_ptr())
+            ctx.synchronize()
+            ctx.gather(p)
+            outs.append((ctx.download_records(), part.cpu().numpy()))
+        finally:
+            ctx.close()
+    assert (outs[0][1][:, 0] > 0).sum() > 100
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert_bitexact(outs[0][0], outs[1][0], "wave vs per-lane gather")
+
+
 def test_partial_plus_update_equals_fused(cornell):
     torch = pytest.importorskip("torch")
     ctx, orc = cornell
