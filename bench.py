@@ -39,6 +39,11 @@ def parse():
     ap.add_argument("--structure", default="grid", choices=["grid", "kd"])
     ap.add_argument("--exchange", default="reduce", choices=["reduce", "allgather"])
     ap.add_argument("--paths", type=int, default=512 * 512, help="photon paths per GPU per pass")
+    ap.add_argument("--estimator", default="ppm", choices=["ppm", "knn"],
+                    help="ppm: the reference's fixed-radius PPM gather (headline); knn: pbrt-v2 LPhoton kNN")
+    ap.add_argument("--knn-k", type=int, default=50, help="kNN photons per lookup (pbrt 'nused')")
+    ap.add_argument("--radius2", type=float, default=None,
+                    help="initial / maximum search radius^2 (default: 4 for ppm = raytracing.cu:123, 100 for knn)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-census", action="store_true")
@@ -113,15 +118,20 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from pmrender import hip
-    from pmrender.abi import PM_GATHER_GRID, PM_GATHER_KDTREE, PM_REC_EXCEPTION, PM_REC_INVALID, PM_REC_MISS, \
-        RenderParams
+    from pmrender.abi import PM_ESTIMATOR_KNN, PM_ESTIMATOR_PPM, PM_GATHER_GRID, PM_GATHER_KDTREE, \
+        PM_REC_EXCEPTION, PM_REC_INVALID, PM_REC_MISS, RenderParams
     from pmrender.dist import HipEngine, PassRunner
 
     scene, workload = build_scene(args.config)
     t_setup = time.perf_counter()
     ctx = scene.load_into(hip.Context(local))
     structure = PM_GATHER_KDTREE if args.structure == "kd" else PM_GATHER_GRID
-    p = RenderParams.defaults(paths_per_pass=args.paths, gather_structure=structure)
+    knn = args.estimator == "knn"
+    if knn and world > 1:
+        args.exchange = "allgather"        # the kNN estimate is not a sum over photon shards
+    radius2 = args.radius2 if args.radius2 is not None else (100.0 if knn else 4.0)
+    est = dict(estimator=PM_ESTIMATOR_KNN if knn else PM_ESTIMATOR_PPM, knn_lookup=args.knn_k, initial_radius2=radius2)
+    p = RenderParams.defaults(paths_per_pass=args.paths, gather_structure=structure, **est)
     stream = torch.cuda.Stream()
     with torch.cuda.stream(stream):
         eng = HipEngine(ctx)
@@ -175,7 +185,7 @@ def main():
             census = ctx.gather_counters(full=True)
             tcensus = ctx.trace_counters()
             ctx.set_counting(False)
-            if rank == 0 and world == 1 and structure == PM_GATHER_GRID:
+            if rank == 0 and world == 1 and structure == PM_GATHER_GRID and not knn:
                 # SURVEY.md §8d's per-unit figure counts V on the canonical pbrt kd-tree
                 pk = RenderParams.defaults(paths_per_pass=args.paths, gather_structure=PM_GATHER_KDTREE)
                 ctx.set_counting(True)
@@ -199,7 +209,12 @@ def main():
     if census is not None:
         vis, hits, rows, act = census
         inactive = n_rec - act
-        if structure == PM_GATHER_GRID:
+        if knn:
+            # records as below; 8 B per bucket row; 16 B per photon tested; per
+            # photon found: its slot id (4 B, ph_b) + alpha and wi from the slot (24 B)
+            bytes_launch = 72 * act + 16 * inactive + 8 * rows + 16 * vis + 28 * hits
+            formula = "72*G_act + 16*G_inactive + 8*bucket_rows + 16*photons_tested + 28*photons_found"
+        elif structure == PM_GATHER_GRID:
             # records: pos 16 + nrm 16 + state 16 + N 4 read, state 16 + N 4 written (active);
             # pos 16 read (inactive); 8 B of bucket bounds per row; 16 B per photon tested;
             # 20 B (alpha + wi.y, wi.z) per photon inside the radius
@@ -209,10 +224,12 @@ def main():
             bytes_launch = 72 * act + 16 * inactive + 16 * vis + 24 * hits
             formula = "72*G_act + 16*G_inactive + 16*kd_nodes_visited + 24*photons_in_radius"
         achieved = bytes_launch / (gather_ms * 1e-3) / 1e9
-        traffic, traffic_src = load_pmc_traffic("k_gather_grid" if structure == PM_GATHER_GRID else "k_gather_kd")
+        traffic, traffic_src = load_pmc_traffic(
+            "k_gather_knn" if knn else "k_gather_grid" if structure == PM_GATHER_GRID else "k_gather_kd")
         roofline = {
             "bound": "hbm",
-            "kernel": "k_gather_grid<0,0> (fused range query + PPM update)" if structure == PM_GATHER_GRID
+            "kernel": "k_gather_knn<0> (pbrt LPhoton kNN, fused record update)" if knn
+            else "k_gather_grid<0,0> (fused range query + PPM update)" if structure == PM_GATHER_GRID
             else "k_gather_kd<0,0>",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
@@ -222,7 +239,7 @@ def main():
             "algorithmic_bytes_per_launch": int(bytes_launch),
             "formula": formula,
             "units": {"G_act": act, "G_inactive": inactive, "bucket_rows": rows, "photons_tested": vis,
-                      "photons_in_radius": hits},
+                      "photons_found" if knn else "photons_in_radius": hits},
             "avg_launch_ms": round(gather_ms, 5),
             "launches_timed": gather_launches,
         }
@@ -286,6 +303,8 @@ def main():
             "gather_points": g_points,
             "active_gather_points": active,
             "structure": args.structure,
+            "estimator": args.estimator + (f" (k={args.knn_k})" if knn else ""),
+            "radius2": radius2,
             "exchange": args.exchange if world > 1 else "none",
             "parallelism": f"photon-shard x{world}" if world > 1 else "single",
         },
@@ -301,7 +320,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(scene, RenderParams.defaults(paths_per_pass=args.paths),
+            out["cpu_baseline"] = cpu_baseline(scene, RenderParams.defaults(paths_per_pass=args.paths, **est),
                                                args.cpu_threads)
         except Exception as exc:  # the baseline is reported, never required for the GPU number
             out["cpu_baseline"] = {"error": repr(exc)}

@@ -99,6 +99,9 @@ struct Ctx {
     /* pm_reset_records is deferred: records read as (flux 0, N 0, r2 = rec_fresh_r2) */
     bool rec_fresh = false;
     float rec_fresh_r2 = 0.f;
+    /* estimator of the last gather: what the records' flux / radius2 /
+     * photon_count mean for the final pass (PPM state or kNN sums) */
+    int rec_estimator = PM_ESTIMATOR_PPM;
     int64_t trace_per_block = 0; /* 0: per-lane paths (default); >0: block-compacting pool (env PM_TRACE_PATHS_PER_BLOCK) */
     int64_t trace_wave_paths = 64; /* per-lane kernel: paths per wave (env PM_TRACE_WAVE_PATHS) */
     int trace_refill_min = 32;     /* per-lane kernel: idle lanes that trigger a refill (env PM_TRACE_REFILL_MIN) */
@@ -359,6 +362,14 @@ int check_params(Ctx *c, const pm_render_params *p) {
         FAIL(c, PM_ERR_INVALID, "light_source_index %d out of range (%zu lights)", p->light_source_index,
              c->lights.size());
     if (!(p->initial_radius2 > 0.f)) FAIL(c, PM_ERR_INVALID, "initial_radius2 must be > 0");
+    if (p->estimator != PM_ESTIMATOR_PPM && p->estimator != PM_ESTIMATOR_KNN)
+        FAIL(c, PM_ERR_INVALID, "unknown estimator %d", p->estimator);
+    if (p->estimator == PM_ESTIMATOR_KNN) {
+        if (p->knn_lookup < 1 || p->knn_lookup > PM_KNN_MAX)
+            FAIL(c, PM_ERR_INVALID, "knn_lookup must be in [1, %d]", PM_KNN_MAX);
+        if (p->gather_structure != PM_GATHER_GRID)
+            FAIL(c, PM_ERR_INVALID, "the kNN estimator runs on the photon buckets (PM_GATHER_GRID)");
+    }
     return PM_OK;
 }
 
@@ -381,6 +392,8 @@ void pm_default_params(pm_render_params *p) {
     p->rng_seed = 777u;
     p->light_rng_seed = 2047u;
     p->gather_structure = PM_GATHER_GRID;
+    p->estimator = PM_ESTIMATOR_PPM;
+    p->knn_lookup = 50; /* pbrt-v2 PhotonIntegrator "nused" */
 }
 
 int pm_create(void **out, const pm_config *cfg) {
@@ -812,7 +825,10 @@ int pm_set_slot_buffer(void *ptr, void *d, int64_t n) {
 static GridDesc make_grid(const Ctx *c, const pm_render_params *p) {
     GridDesc g{};
     const float rq = sqrtf(p->initial_radius2) * 1.0001f + 1e-4f;
-    float cs = 2.0f * rq * 1.001f;
+    /* PPM: cell edge >= 2 r_max, so a query reads at most 2x2x2 cells. kNN:
+     * r_max / 2 — the query visits rows nearest first and prunes cells
+     * beyond the shrinking k-th distance (k_gather_knn) */
+    float cs = (p->estimator == PM_ESTIMATOR_KNN ? 0.5f : 2.0f) * rq * 1.001f;
     float ext[3];
     for (int a = 0; a < 3; ++a) ext[a] = std::max(c->bbox_hi[a] - c->bbox_lo[a], 1e-3f);
     int64_t dims[3];
@@ -945,6 +961,9 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
     if ((rc = check_params(c, p))) return rc;
     if (c->nrec <= 0) FAIL(c, PM_ERR_INVALID, "no records (run pm_eye_pass first)");
     if (c->map_kind != p->gather_structure) FAIL(c, PM_ERR_INVALID, "photon map not built for this gather structure");
+    if (p->estimator == PM_ESTIMATOR_KNN && (partial || count))
+        FAIL(c, PM_ERR_INVALID, "the kNN estimator is not linear in the photon set: no partial / split gathers "
+                                "(multi-GPU: all-gather the photons, then pm_gather_range)");
     if (rec_begin < 0 || rec_count < 0 || rec_begin + rec_count > c->nrec) FAIL(c, PM_ERR_INVALID, "bad record range");
     hipStream_t s = pick(c, stream);
     GatherParams G = gather_params(c, p);
@@ -963,8 +982,20 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
     else if ((rc = materialize_reset(c, s))) return rc;
     if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters.p, 0, 32, s));
     timer_begin(c, "gather", s);
-    HIPCHK(c, launch_gather(G, p->gather_structure, partial != nullptr || split, c->counting, s));
+    if (p->estimator == PM_ESTIMATOR_KNN) {
+        G.knn_k = p->knn_lookup;
+        G.knn_r2 = p->initial_radius2; /* pbrt's maxDistSquared: the buckets cover it */
+        /* every term (kernel <= 3/pi < 1) is <= alpha_max / r_k^2: 2^50 of the
+         * per-record scale per term, 64 terms fit an int64 */
+        const double amax = c->emit_max * std::pow(c->kd_max, (double)p->max_photon_count) * 4.0;
+        G.knn_fx = (float)(std::ldexp(1.0, 50) / std::max(amax, 1e-30));
+        G.slots = c->d_slots.as<pm_photon>();
+        HIPCHK(c, launch_gather_knn(G, c->counting, s));
+    } else {
+        HIPCHK(c, launch_gather(G, p->gather_structure, partial != nullptr || split, c->counting, s));
+    }
     timer_end(c, "gather", s);
+    c->rec_estimator = p->estimator;
     if (consume) c->rec_fresh = false;
     return PM_OK;
 }
@@ -1056,6 +1087,7 @@ int pm_final(void *ptr, double emitted, int64_t rec_begin, int64_t rec_count, vo
     if ((rc = materialize_reset(c, s))) return rc;
     FinalParams F{};
     F.R = recs(c);
+    F.knn = c->rec_estimator == PM_ESTIMATOR_KNN; F.materials = c->S.materials;
     F.emitted = (float)emitted; /* gContext["emittingPhotons"]->setFloat((float)totalPhotons) */
     F.rec_begin = rec_begin; F.rec_count = rec_count; F.out = (float *)d_out; F.raster = 0; F.W = c->W;
     timer_begin(c, "final", s);
@@ -1104,6 +1136,7 @@ int pm_render(void *ptr, const pm_render_params *p, float *out_rgb, pm_stats *st
     HIPCHK(c, c->d_out.ensure(nout * 3 * sizeof(float)));
     FinalParams F{};
     F.R = recs(c);
+    F.knn = c->rec_estimator == PM_ESTIMATOR_KNN; F.materials = c->S.materials;
     F.emitted = (float)emitted;
     F.rec_begin = 0; F.rec_count = c->nrec; F.out = c->d_out.as<float>(); F.raster = c->pinhole; F.W = c->W;
     timer_begin(c, "final", s);
@@ -1318,6 +1351,7 @@ int pm_final_view(void *ptr, double emitted, int64_t v_begin, int64_t v_count, v
     if ((rc = materialize_reset(c, s))) return rc;
     FinalParams F{};
     F.R = recs(c);
+    F.knn = c->rec_estimator == PM_ESTIMATOR_KNN; F.materials = c->S.materials;
     F.emitted = (float)emitted;
     F.rec_begin = v_begin; F.rec_count = v_count; F.out = (float *)d_out; F.raster = 0; F.W = c->W;
     F.view = c->d_vlist.as<uint32_t>();

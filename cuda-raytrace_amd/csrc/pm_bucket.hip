@@ -168,7 +168,9 @@ __global__ __launch_bounds__(256) void k_bucket_fill(const pm_photon *slots, int
      * write-back each, so (alpha, wi.y) + wi.z as one sector instead of two
      * arrays saves a third of the fill's write traffic */
     ph_b[2 * (size_t)dst] = make_float4(c.x, c.y, d.x, e.x);
-    ph_b[2 * (size_t)dst + 1] = make_float4(e.y, 0.f, 0.f, 0.f);
+    /* + the slot index: the kNN estimator's tie-break and its handle on the
+     * photon (pm_gather.hip k_gather_knn) */
+    ph_b[2 * (size_t)dst + 1] = make_float4(e.y, __uint_as_float((uint32_t)i), 0.f, 0.f);
 }
 /* Measured (PMC WRITE_SIZE): ~55 MB written per launch for ~20 MB of photon
  * data — the scattered 16-B stores cost whole-line write-backs. Giving each

@@ -280,6 +280,174 @@ __global__ __launch_bounds__(GATHER_BLOCK, 8) void k_gather_wave(GatherParams P)
     }
 }
 
+/* ---------------------------------------------------------------------- */
+/* kNN estimator: pbrt-v2 PhotonIntegrator::LPhoton (integrators/photonmap.cpp,
+ * diffuse branch) with PhotonProcess / KdTree::Lookup semantics, over the
+ * photon buckets. Per record (one lane): the K photons with the smallest
+ * keys (d^2, slot) among those with d^2 < maxD2 (the buckets cover that
+ * radius) are kept in a max-heap in LDS — the set pbrt's lookup finds, up to
+ * the order among photons at exactly equal d^2, where the lower slot wins
+ * here and the first visited in pbrt. r_k^2 = the heap top's d^2 once K
+ * were found (pbrt's shrunk maxDistSquared), else maxD2. Then
+ *     S = sum over found photons with Dot(Nf, wi) > 0 of
+ *         (3/pi (1 - d^2/r_k^2)^2 / r_k^2) * alpha        (kernel(), photonmap.cpp)
+ * with Nf = Faceforward(ns, wo) (PM_REC_BACKFACE). The sum is exact and
+ * order-free in int64 fixed point (scale: the power of two below
+ * knn_fx * r_k^2, every term being <= alpha_max / r_k^2). Fused record
+ * update: flux += S, radius2 = r_k^2, photon_count = found; the final pass
+ * applies 1/paths and rho/pi = Kd/pi (k_final). */
+PMD bool key_less(uint32_t ad, uint32_t as, uint32_t bd, uint32_t bs) { return ad < bd || (ad == bd && as < bs); }
+PMD float sq(float x) { return x * x; }
+/* distance, in cell units, from coordinate u (cell units) to cell c of an
+ * axis with dim cells — the border cells extend to infinity (cell_axis
+ * clamps) — less a 1e-3 margin that covers the float rounding of u and of the
+ * photons' own d^2, so pruning with it never drops a photon the heap takes */
+PMD float cell_gap(float u, uint32_t c, int dim) {
+    const float lo = c == 0 ? -INFINITY : (float)c, hi = (int)c + 1 == dim ? INFINITY : (float)(c + 1);
+    return fmaxf(fmaxf(lo - u, u - hi) - 1e-3f, 0.f);
+}
+/* max-heap of (d^2 bits, slot) in LDS columns: entry k of this lane at [k * KNN_BLOCK] */
+PMD void heap_push(uint32_t *hd, uint32_t *hs, int n, uint32_t d, uint32_t sl) {
+    int i = n;
+    while (i > 0) {
+        const int pa = (i - 1) >> 1;
+        const uint32_t pd = hd[pa * KNN_BLOCK], ps = hs[pa * KNN_BLOCK];
+        if (!key_less(pd, ps, d, sl)) break;
+        hd[i * KNN_BLOCK] = pd; hs[i * KNN_BLOCK] = ps;
+        i = pa;
+    }
+    hd[i * KNN_BLOCK] = d; hs[i * KNN_BLOCK] = sl;
+}
+PMD void heap_replace_top(uint32_t *hd, uint32_t *hs, int n, uint32_t d, uint32_t sl) {
+    int i = 0;
+    while (true) {
+        int c = 2 * i + 1;
+        if (c >= n) break;
+        uint32_t cd = hd[c * KNN_BLOCK], cs = hs[c * KNN_BLOCK];
+        if (c + 1 < n) {
+            const uint32_t rd = hd[(c + 1) * KNN_BLOCK], rs = hs[(c + 1) * KNN_BLOCK];
+            if (key_less(cd, cs, rd, rs)) { c = c + 1; cd = rd; cs = rs; }
+        }
+        if (!key_less(d, sl, cd, cs)) break;
+        hd[i * KNN_BLOCK] = cd; hs[i * KNN_BLOCK] = cs;
+        i = c;
+    }
+    hd[i * KNN_BLOCK] = d; hs[i * KNN_BLOCK] = sl;
+}
+
+template <int COUNT>
+__global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn(GatherParams P) {
+    extern __shared__ uint32_t kheap[]; /* [K][KNN_BLOCK] d^2 bits, then [K][KNN_BLOCK] slots */
+    const int K = P.knn_k;
+    uint32_t *hd = kheap + threadIdx.x, *hs = kheap + K * KNN_BLOCK + threadIdx.x;
+    const int64_t r = P.rec_begin + (int64_t)blockIdx.x * KNN_BLOCK + threadIdx.x;
+    unsigned long long vis = 0, hits = 0, rows = 0, act = 0;
+    if (r < P.rec_end) {
+        const float4 pos = P.R.pos[r];
+        const uint32_t flags = (uint32_t)__float_as_int(pos.w);
+        if (!(flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID))) {
+            float4 st = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : P.R.state[r];
+            const float4 nrm = P.R.nrm[r];
+            const float4 m = P.materials[__float_as_int(nrm.w)];
+            const float maxd2 = P.knn_r2;
+            const v3 p = xyz(pos), ns = xyz(nrm);
+            int cnt = 0;
+            float md2 = maxd2;
+            Fx3 acc{0, 0, 0};
+            float sc = 1.f;
+            bool nan = false;
+            if (__float_as_int(m.w) == PM_MATTE) { /* non-specular BSDF components only */
+                const GridDesc &g = P.grid;
+                const float rq = sqrtf(maxd2) * 1.0001f + 1e-4f;
+                const uint32_t x0 = cell_axis(p.x - rq, g.gx, g.inv_cs, g.dx), x1 = cell_axis(p.x + rq, g.gx, g.inv_cs, g.dx);
+                const uint32_t y0 = cell_axis(p.y - rq, g.gy, g.inv_cs, g.dy), y1 = cell_axis(p.y + rq, g.gy, g.inv_cs, g.dy);
+                const uint32_t z0 = cell_axis(p.z - rq, g.gz, g.inv_cs, g.dz), z1 = cell_axis(p.z + rq, g.gz, g.inv_cs, g.dz);
+                const int cyc = (int)cell_axis(p.y, g.gy, g.inv_cs, g.dy), czc = (int)cell_axis(p.z, g.gz, g.inv_cs, g.dz);
+                /* the query point in cell units (cell_axis before the floor) */
+                const float ux = (p.x - g.gx) * g.inv_cs, uy = (p.y - g.gy) * g.inv_cs, uz = (p.z - g.gz) * g.inv_cs;
+                const float inv2 = g.inv_cs * g.inv_cs;
+                const int rings = max((int)(y1 - y0), (int)(z1 - z0));
+                uint32_t topd = 0xffffffffu, tops = 0xffffffffu; /* heap top, once full */
+                const float *phb = reinterpret_cast<const float *>(P.ph_b);
+                /* rows (y, z) in rings around the query's row, nearest first, so
+                 * the heap fills early and the k-th distance prunes the rest:
+                 * a row / cell is skipped when its (margin-reduced) distance
+                 * exceeds the current bound — every photon in it would fail
+                 * d^2 < maxD2, or d^2 <= top once the heap is full */
+                for (int ring = 0; ring <= rings; ++ring)
+                    for (uint32_t cz = z0; cz <= z1; ++cz)
+                        for (uint32_t cy = y0; cy <= y1; ++cy) {
+                            if (max(abs((int)cy - cyc), abs((int)cz - czc)) != ring) continue;
+                            const float bound = (cnt == K ? __uint_as_float(topd) : maxd2) * inv2;
+                            const float gy = cell_gap(uy, cy, g.dy), gz = cell_gap(uz, cz, g.dz);
+                            const float lim = bound - (gy * gy + gz * gz);
+                            if (lim < 0.f) continue;
+                            uint32_t xa = x0, xb = x1;
+                            while (xa <= xb && sq(cell_gap(ux, xa, g.dx)) > lim) ++xa;
+                            while (xb > xa && sq(cell_gap(ux, xb, g.dx)) > lim) --xb;
+                            if (xa > xb) continue;
+                            const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+                            const uint32_t b = P.cell_start[row + xa], e = P.cell_start[row + xb + 1];
+                            if (COUNT) { vis += e - b; rows++; }
+                            for (uint32_t j = b; j < e; ++j) {
+                                const float4 a = P.ph_a[j];
+                                const v3 diff = p - xyz(a);
+                                const float d2 = diff.x * diff.x + diff.y * diff.y + diff.z * diff.z;
+                                if (!(d2 < maxd2)) continue;
+                                const uint32_t db = __float_as_uint(d2); /* d2 >= 0: bits order = value order */
+                                if (cnt == K && db > topd) continue;
+                                const uint32_t sl = __float_as_uint(phb[8 * (size_t)j + 5]);
+                                if (cnt < K) {
+                                    heap_push(hd, hs, cnt, db, sl);
+                                    if (++cnt == K) { topd = hd[0]; tops = hs[0]; }
+                                } else if (db < topd || sl < tops) {
+                                    heap_replace_top(hd, hs, K, db, sl);
+                                    topd = hd[0]; tops = hs[0];
+                                }
+                            }
+                        }
+                if (cnt == K) md2 = __uint_as_float(topd);
+                const bool back = (flags & PM_REC_BACKFACE) != 0;
+                sc = __uint_as_float(__float_as_uint(P.knn_fx * md2) & 0xff800000u); /* power of two: exact scaling */
+                if (md2 == 0.f) sc = 1.f;
+                for (int k = 0; k < cnt; ++k) {
+                    const float d2 = __uint_as_float(hd[k * KNN_BLOCK]);
+                    const float2 *q = reinterpret_cast<const float2 *>(P.slots + hs[k * KNN_BLOCK]);
+                    const float2 q2 = q[2], q3 = q[3], q4 = q[4]; /* (alpha.x, alpha.y) (alpha.z, wi.x) (wi.y, wi.z) */
+                    float dn = dot(ns, mk(q3.y, q4.x, q4.y));
+                    if (back) dn = -dn; /* Dot(Faceforward(ns, wo), wi) */
+                    if (dn > 0.f && md2 == 0.f) { /* K photons at distance 0: pbrt's kernel() is 0/0 */
+                        nan = true;
+                    } else if (dn > 0.f) {
+                        const float s = 1.f - d2 / md2;
+                        const float kk = 3.f * INV_PI * s * s;
+                        const v3 c = (kk / md2) * mk(q2.x, q2.y, q3.x);
+                        acc.x += to_fx(c.x, sc); acc.y += to_fx(c.y, sc); acc.z += to_fx(c.z, sc);
+                    }
+                }
+            }
+            if (COUNT) { hits += (unsigned long long)cnt; act++; }
+            const double inv = 1.0 / (double)sc;
+            v3 L = mk((float)((double)acc.x * inv), (float)((double)acc.y * inv), (float)((double)acc.z * inv));
+            if (nan) L = mk(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
+            const v3 flux = xyz(st) + L;
+            P.R.state[r] = make_float4(flux.x, flux.y, flux.z, md2);
+            P.R.n[r] = (float)cnt;
+        }
+    }
+    if (COUNT) count4(P.counters, vis, hits, rows, act);
+}
+
+hipError_t launch_gather_knn(const GatherParams &p, int count, hipStream_t s) {
+    if (p.rec_end <= p.rec_begin) return hipSuccess;
+    if (p.knn_k < 1 || p.knn_k > PM_KNN_MAX) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)((p.rec_end - p.rec_begin + KNN_BLOCK - 1) / KNN_BLOCK);
+    const uint32_t lds = (uint32_t)(2 * p.knn_k * KNN_BLOCK * sizeof(uint32_t));
+    if (count) pm_launch(k_gather_knn<1>, dim3(grid), dim3(KNN_BLOCK), lds, s, p);
+    else pm_launch(k_gather_knn<0>, dim3(grid), dim3(KNN_BLOCK), lds, s, p);
+    return hipGetLastError();
+}
+
 /* kd-tree range query in the reference layout (gathering.cu:25-96):
  * same visiting order, same accumulation order -> bit-exact with it. */
 template <int PARTIAL, int COUNT>
@@ -520,7 +688,13 @@ __global__ __launch_bounds__(256) void k_final(FinalParams P) {
         float4 dl = P.R.dl[r], st = P.R.state[r];
         float N = P.R.n[r];
         v3 IDL = mk(0.f, 0.f, 0.f);
-        if (N != 0) IDL = xyz(st) * INV_PI / (st.w * P.emitted);
+        if (P.knn) { /* LPhoton: Lr * rho / pi with Lr's 1/nPaths = 1/emitted (passes averaged) */
+            const float4 m = P.materials[__float_as_int(P.R.nrm[r].w)];
+            const v3 fv = __float_as_int(m.w) == PM_MATTE ? xyz(m) * INV_PI : mk(0.f, 0.f, 0.f);
+            IDL = (xyz(st) / P.emitted) * fv;
+        } else if (N != 0) {
+            IDL = xyz(st) * INV_PI / (st.w * P.emitted);
+        }
         out = xyz(dl) + IDL;
         float y = 0.212671f * out.x + 0.715160f * out.y + 0.072169f * out.z;
         if (isnan(out.x) || isnan(out.y) || isnan(out.z) || y < -1e-5f || isinf(y)) out = mk(0.f, 0.f, 0.f);

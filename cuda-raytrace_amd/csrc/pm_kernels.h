@@ -36,6 +36,7 @@ constexpr int TRACE_BLOCK = 256;    /* k_trace: 4 waves compact paths together *
 constexpr int BVH_STACK = BVH_STACK_DEPTH; /* >= max BVH depth (builder enforces it) */
 constexpr int GATHER_BLOCK = 256;
 constexpr int KD_STACK = 32;       /* >= pbrt median kd-tree depth for < 2^31 photons */
+constexpr int KNN_BLOCK = 64;      /* k_gather_knn: one wave per block, LDS heaps [K][64] */
 
 /* device SoA record arrays */
 struct RecordsDev {
@@ -124,11 +125,20 @@ struct GatherParams {
     const uint32_t *view_list;
     /* grid gather kernel: 1 = wave-cooperative (k_gather_wave, experiment), 0 = per lane (k_gather_grid, default) */
     int wave;
+    /* kNN estimator (k_gather_knn): knn_k nearest photons with d^2 < knn_r2;
+     * per-record fixed-point scale = power of two below knn_fx * r_k^2;
+     * slots = the slot buffer the buckets were built from (ph_b carries the
+     * slot index) */
+    int knn_k;
+    float knn_r2, knn_fx;
+    const pm_photon *slots;
     unsigned long long *counters; /* [0] visited, [1] in radius */
 };
 
 struct FinalParams {
     RecordsDev R;
+    int knn;                     /* records hold kNN sums: out = DL + flux / emitted * Kd/pi */
+    const float4 *materials;
     float emitted;
     int64_t rec_begin, rec_count;
     float *out;     /* float3 */
@@ -156,6 +166,8 @@ hipError_t launch_bucket_build(const pm_photon *slots, int64_t n, GridDesc g, ui
                                uint32_t *scratch, float4 *ph_a, float4 *ph_b, bool counted, hipStream_t s);
 /* gather: structure 0 grid, 1 kd; mode 0 fused PPM, 1 partial */
 hipError_t launch_gather(const GatherParams &p, int structure, int partial, int count, hipStream_t s);
+/* kNN estimator (pbrt LPhoton) over the photon buckets, fused record update */
+hipError_t launch_gather_knn(const GatherParams &p, int count, hipStream_t s);
 hipError_t launch_ppm_update(const GatherParams &p, const long long *partial, int64_t rec_begin, int64_t rec_count,
                              hipStream_t s);
 hipError_t launch_ppm_update_split(const GatherParams &p, const int *count, const long long *flux, int64_t n_view,

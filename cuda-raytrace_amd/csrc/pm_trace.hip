@@ -118,7 +118,10 @@ __global__ __launch_bounds__(EYE_BLOCK) void k_eye(EyeParams P) {
             }
         }
     }
-    P.R.pos[r] = make_float4(point.x, point.y, point.z, __int_as_float(0));
+    /* Faceforward(nn, wo) side, for the kNN estimator (the reference keeps
+     * record.direction itself, raytracing.cu:117) */
+    const uint32_t side = dot(ns, -dir) < 0.f ? PM_REC_BACKFACE : 0u;
+    P.R.pos[r] = make_float4(point.x, point.y, point.z, __uint_as_float(side));
     P.R.nrm[r] = make_float4(ns.x, ns.y, ns.z, __int_as_float(g.material));
     P.R.state[r] = make_float4(0.f, 0.f, 0.f, P.r2init);
     P.R.n[r] = 0.f;

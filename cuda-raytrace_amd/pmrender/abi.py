@@ -12,8 +12,11 @@ PM_ERR_NOMEM = 4
 
 PM_MATTE, PM_MIRROR, PM_GLASS = 0, 1, 2
 PM_LIGHT_POINT, PM_LIGHT_AREA_DISK = 1, 3
-PM_REC_EXCEPTION, PM_REC_MISS, PM_REC_INVALID = 0x1, 0x2, 0x4
+PM_REC_EXCEPTION, PM_REC_MISS, PM_REC_INVALID, PM_REC_BACKFACE = 0x1, 0x2, 0x4, 0x8
+PM_REC_INACTIVE = PM_REC_EXCEPTION | PM_REC_MISS | PM_REC_INVALID
 PM_GATHER_GRID, PM_GATHER_KDTREE = 0, 1
+PM_ESTIMATOR_PPM, PM_ESTIMATOR_KNN = 0, 1
+PM_KNN_MAX = 64
 PM_PHOTON_MAX_RIGHT_CHILD = (1 << 29) - 1
 
 # pm_photon == reference CudaPhoton (photon_mapping/photonmapping.h:32-41), 40 B
@@ -41,7 +44,9 @@ class RenderParams(ctypes.Structure):
         ("rng_seed", ctypes.c_uint32),
         ("light_rng_seed", ctypes.c_uint32),
         ("gather_structure", ctypes.c_int),
-        ("reserved", ctypes.c_int * 6),
+        ("estimator", ctypes.c_int),
+        ("knn_lookup", ctypes.c_int),
+        ("reserved", ctypes.c_int * 4),
     ]
 
     @classmethod
@@ -58,6 +63,8 @@ class RenderParams(ctypes.Structure):
         p.rng_seed = 777             # cudarandom.h:15
         p.light_rng_seed = 2047
         p.gather_structure = PM_GATHER_GRID
+        p.estimator = PM_ESTIMATOR_PPM
+        p.knn_lookup = 50            # pbrt-v2 PhotonIntegrator "nused"
         return p._apply(kw)
 
     @classmethod

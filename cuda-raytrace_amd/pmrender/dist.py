@@ -116,6 +116,9 @@ class PassRunner:
     def __init__(self, engine, params, rank=0, world=1, exchange="reduce"):
         if exchange not in ("reduce", "allgather"):
             raise ValueError(exchange)
+        if world > 1 and exchange == "reduce" and int(getattr(params, "estimator", 0)) != 0:
+            # the kNN estimate is not a sum over photon shards
+            raise ValueError("the kNN estimator needs the all-gather exchange")
         self.e, self.p, self.rank, self.world, self.exchange = engine, params, rank, world, exchange
         self.paths = int(params.paths_per_pass)           # per rank
         self.path_begin = rank * self.paths

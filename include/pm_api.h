@@ -60,12 +60,20 @@ extern "C" {
 #define PM_REC_EXCEPTION 0x01u
 #define PM_REC_MISS 0x02u
 #define PM_REC_INVALID 0x04u
+/* the eye ray hit the back of the shading normal: dot(ns, wo) < 0 with
+ * wo = -ray.direction (RayTracingRecord::direction, photonmapping.h:18) —
+ * what pbrt's Faceforward(nn, wo) needs in the kNN estimator */
+#define PM_REC_BACKFACE 0x08u
 /* gather structures */
 #define PM_GATHER_GRID 0   /* hashed uniform grid of photon buckets (default, fastest) */
 #define PM_GATHER_KDTREE 1 /* reference-layout kd-tree (CudaPhoton nodes, pbrt median split) */
 /* multi-GPU photon exchange */
 #define PM_EXCHANGE_REDUCE 0   /* local maps, per-record (M, L) reduce-scatter */
 #define PM_EXCHANGE_ALLGATHER 1 /* all-gather photon slots, replicated map */
+/* radiance estimators of the gather (pm_render_params::estimator) */
+#define PM_ESTIMATOR_PPM 0 /* the reference's: fixed-radius query + progressive update (gathering.cu:17-146) */
+#define PM_ESTIMATOR_KNN 1 /* pbrt-v2 PhotonIntegrator::LPhoton: k nearest photons, Simpson kernel */
+#define PM_KNN_MAX 64      /* largest knn_lookup */
 
 /* ---- POD layouts shared with tests / other hosts ----------------------- */
 
@@ -83,7 +91,10 @@ typedef struct pm_photon {
 
 /* Gather-point record (the subset of RayTracingRecord, photonmapping.h:7-24,
  * that the gather and final passes read). 64 bytes, AoS for exchange; the
- * device keeps it as SoA. */
+ * device keeps it as SoA. Under PM_ESTIMATOR_KNN,
+ * flux accumulates the per-pass sums, radius2 holds the last pass's r_k^2
+ * (pbrt's shrunk maxDistSquared) and photon_count its number of photons
+ * found. */
 typedef struct pm_record {
     float pos[3];
     uint32_t flags;
@@ -114,7 +125,15 @@ typedef struct pm_render_params {
     uint32_t rng_seed;       /* 777   util/random/cudarandom.h:15 */
     uint32_t light_rng_seed; /* 2047  (cudalight.cpp:530, commented-out light RNG seed) */
     int gather_structure;    /* PM_GATHER_GRID */
-    int reserved[6];
+    /* PM_ESTIMATOR_PPM (default) or PM_ESTIMATOR_KNN: per pass, the knn_lookup
+     * nearest photons with d^2 < initial_radius2 (pbrt's maxdist^2) give
+     * sum_i Simpson(d_i^2, r_k^2) / r_k^2 * alpha_i over photons on the
+     * viewer's side (pbrt photonmap.cpp LPhoton, diffuse branch); passes are
+     * averaged. Photon-bucket gather only; not linear in the photon set, so
+     * no partial/split gathers (multi-GPU: the all-gather exchange). */
+    int estimator;
+    int knn_lookup;          /* 50    pbrt PhotonIntegrator "nused" */
+    int reserved[4];
 } pm_render_params;
 
 typedef struct pm_stats {

@@ -54,6 +54,7 @@ def load():
         "orc_gather": (None, [vp, vp, i64, vp, i64, RP, ctypes.POINTER(i64), c_int]),
         "orc_gather_partial": (None, [vp, vp, i64, vp, i64, vp, c_int]),
         "orc_final": (None, [vp, vp, i64, c_double, P_f, c_int]),
+        "orc_final_est": (None, [vp, vp, i64, c_double, c_int, P_f, c_int]),
         "orc_render": (c_int, [vp, RP, P_f, ctypes.POINTER(Stats), c_int]),
         "orc_render_simple": (None, [vp, RP, P_f, c_int]),
         "orc_concentric_sample_disk": (None, [c_float, c_float, P_f]),
@@ -161,7 +162,9 @@ class Oracle:
         return nodes[:n]
 
     def gather(self, nodes, recs, params):
-        """In-place kd-tree range query + PPM update; returns (visited, in_radius)."""
+        """In-place kd-tree gather: range query + PPM update, or (params.estimator
+        == PM_ESTIMATOR_KNN) pbrt's k-nearest lookup + LPhoton sum; returns
+        (kd nodes visited, photons in radius / found)."""
         cnt = (ctypes.c_int64 * 2)()
         self.lib.orc_gather(self.h, nodes.ctypes.data, len(nodes), recs.ctypes.data, len(recs), ctypes.byref(params),
                             cnt, self.nthreads)
@@ -174,10 +177,11 @@ class Oracle:
                                     out.ctypes.data, self.nthreads)
         return out
 
-    def final(self, recs, emitted):
+    def final(self, recs, emitted, estimator=0):
         n = self.width * self.height if self.pinhole else len(recs)
         out = np.zeros((n, 3), np.float32)
-        self.lib.orc_final(self.h, recs.ctypes.data, len(recs), float(emitted), fptr(out), self.nthreads)
+        self.lib.orc_final_est(self.h, recs.ctypes.data, len(recs), float(emitted), int(estimator), fptr(out),
+                               self.nthreads)
         return out.reshape(self.height, self.width, 3) if self.pinhole else out
 
     def render(self, params):

@@ -650,7 +650,9 @@ void eye_record(const Scene &S, const pm_render_params &P, int64_t r, pm_record 
             ray.o = point; ray.d = wi; ray.tmin = P.scene_epsilon; ray.tmax = RT_DEFAULT_MAX;
             continue;
         }
-        rec->flags = 0;
+        /* Faceforward(nn, wo) side for the kNN estimator; the reference keeps
+         * the direction itself (record.direction, raytracing.cu:117) */
+        rec->flags = dot(g.ns, -ray.d) < 0.f ? PM_REC_BACKFACE : 0u;
         rec->pos[0] = point.x; rec->pos[1] = point.y; rec->pos[2] = point.z;
         rec->ns[0] = g.ns.x; rec->ns[1] = g.ns.y; rec->ns[2] = g.ns.z;
         rec->material = g.material;
@@ -898,14 +900,92 @@ void ppm_update(pm_record &rec, int M, f3 L, float alpha) {
     }
 }
 
-/* gathering.cu:129-146 + host sanity check photonmappingrenderer.cpp:252-268 */
-void final_radiance(const pm_record &rec, float emitted, float out[3]) {
+/* ---- kNN estimator (PM_ESTIMATOR_KNN): pbrt-v2's photon map lookup --------
+ * Restated from pbrt-v2 (unvendored submodule):
+ * KdTree::privateLookup (core/kdtree.h), PhotonProcess + ClosePhoton + kernel()
+ * + LPhoton's diffuse branch (integrators/photonmap.cpp). Parity unpinned. */
+struct ClosePhoton {
+    const pm_photon *photon;
+    float d2;
+    bool operator<(const ClosePhoton &o) const { return d2 == o.d2 ? photon < o.photon : d2 < o.d2; }
+};
+struct PhotonProcess {
+    ClosePhoton *photons;
+    uint32_t nLookup, nFound;
+    void operator()(const pm_photon &ph, float d2, float &maxD2) {
+        if (nFound < nLookup) { /* unordered until full, then a max-heap */
+            photons[nFound++] = ClosePhoton{&ph, d2};
+            if (nFound == nLookup) {
+                std::make_heap(photons, photons + nLookup);
+                maxD2 = photons[0].d2;
+            }
+        } else { /* replace the most distant photon */
+            std::pop_heap(photons, photons + nLookup);
+            photons[nLookup - 1] = ClosePhoton{&ph, d2};
+            std::push_heap(photons, photons + nLookup);
+            maxD2 = photons[0].d2;
+        }
+    }
+};
+/* KdTree::privateLookup: children first (near side, then far side if the
+ * splitting plane is within the current radius), then the node itself */
+void kd_knn(const pm_photon *nodes, int64_t nnodes, uint32_t nodeNum, f3 p, PhotonProcess &proc, float &maxD2,
+            int64_t *visited) {
+    const pm_photon &nd = nodes[nodeNum];
+    const uint32_t axis = (nd.bits >> 1) & 3u, hasLeft = nd.bits & 1u, right = nd.bits >> 3;
+    if (axis != 3) {
+        const float pa = comp(p, (int)axis), split = nd.p[axis];
+        const float dist2 = (pa - split) * (pa - split);
+        if (pa <= split) {
+            if (hasLeft) kd_knn(nodes, nnodes, nodeNum + 1, p, proc, maxD2, visited);
+            if (dist2 < maxD2 && (int64_t)right < nnodes) kd_knn(nodes, nnodes, right, p, proc, maxD2, visited);
+        } else {
+            if ((int64_t)right < nnodes) kd_knn(nodes, nnodes, right, p, proc, maxD2, visited);
+            if (dist2 < maxD2 && hasLeft) kd_knn(nodes, nnodes, nodeNum + 1, p, proc, maxD2, visited);
+        }
+    }
+    (*visited)++;
+    const f3 diff = ld3(nd.p) - p; /* DistanceSquared(nodeData[nodeNum].p, p) */
+    const float d2 = diff.x * diff.x + diff.y * diff.y + diff.z * diff.z;
+    if (d2 < maxD2) proc(nd, d2, maxD2);
+}
+/* One pass of LPhoton (diffuse branch) at a record: S = sum over the found
+ * photons with Dot(Nf, wi) > 0 of kernel(d2) / maxD2 * alpha, where Nf =
+ * Faceforward(nn, wo) and maxD2 is the lookup's shrunk radius. The 1/nPaths
+ * and rho/pi = Kd/pi factors are applied at the final pass (final_radiance). */
+f3 knn_estimate(const pm_photon *nodes, int64_t nnodes, const pm_record &rec, int K, float maxD2_0, int *nFound,
+                float *maxD2_out, int64_t *visited) {
+    ClosePhoton buf[PM_KNN_MAX];
+    PhotonProcess proc{buf, (uint32_t)std::max(1, std::min(K, PM_KNN_MAX)), 0u};
+    float maxD2 = maxD2_0;
+    const f3 p = ld3(rec.pos);
+    kd_knn(nodes, nnodes, 0, p, proc, maxD2, visited);
+    const f3 ns = ld3(rec.ns);
+    const f3 Nf = (rec.flags & PM_REC_BACKFACE) ? -ns : ns;
+    f3 L = mk(0.f, 0.f, 0.f);
+    for (uint32_t i = 0; i < proc.nFound; ++i) {
+        const pm_photon &ph = *buf[i].photon;
+        if (dot(Nf, ld3(ph.wi)) > 0.f) {
+            const float s = (1.f - buf[i].d2 / maxD2);
+            const float k = 3.f * INV_PI * s * s; /* kernel(): Simpson */
+            L = L + (k / maxD2) * ld3(ph.alpha);
+        }
+    }
+    *nFound = (int)proc.nFound;
+    *maxD2_out = maxD2;
+    return L;
+}
+
+/* gathering.cu:129-146 + host sanity check photonmappingrenderer.cpp:252-268;
+ * kNN: L = direct + (sum of the passes' S / paths emitted) * rho/pi */
+void final_radiance(const Scene &S, const pm_record &rec, float emitted, int estimator, float out[3]) {
     if ((rec.flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) != 0) {
         out[0] = out[1] = out[2] = 0.f;
         return;
     }
     f3 DL = ld3(rec.dl), IDL = mk(0.f, 0.f, 0.f);
-    if (rec.photon_count != 0) IDL = ld3(rec.flux) * INV_PI / (rec.radius2 * emitted);
+    if (estimator == PM_ESTIMATOR_KNN) IDL = (ld3(rec.flux) / emitted) * bsdf_f(S, rec.material);
+    else if (rec.photon_count != 0) IDL = ld3(rec.flux) * INV_PI / (rec.radius2 * emitted);
     f3 o = DL + IDL;
     float y = 0.212671f * o.x + 0.715160f * o.y + 0.072169f * o.z; /* pbrt RGBSpectrum::y */
     if (std::isnan(o.x) || std::isnan(o.y) || std::isnan(o.z) || y < -1e-5f || std::isinf(y))
@@ -1090,8 +1170,19 @@ void orc_gather(void *s, const pm_photon *nodes, int64_t nnodes, pm_record *recs
         int M = 0;
         int64_t v = 0;
         f3 L;
-        kd_lookup(nodes, rec, bsdf_f(S, rec.material), rec.radius2, &M, &L, &v);
-        ppm_update(rec, M, L, P->ppm_alpha);
+        if (P->estimator == PM_ESTIMATOR_KNN) {
+            float md2 = P->initial_radius2;
+            L = mk(0.f, 0.f, 0.f);
+            if (S.mats[rec.material].type == PM_MATTE) /* non-specular BSDF components only */
+                L = knn_estimate(nodes, nnodes, rec, P->knn_lookup, P->initial_radius2, &M, &md2, &v);
+            const f3 flux = ld3(rec.flux) + L;
+            rec.flux[0] = flux.x; rec.flux[1] = flux.y; rec.flux[2] = flux.z;
+            rec.radius2 = md2;
+            rec.photon_count = (float)M;
+        } else {
+            kd_lookup(nodes, rec, bsdf_f(S, rec.material), rec.radius2, &M, &L, &v);
+            ppm_update(rec, M, L, P->ppm_alpha);
+        }
         vis += v;
         hits += M;
     });
@@ -1118,7 +1209,8 @@ void orc_gather_partial(void *s, const pm_photon *nodes, int64_t nnodes, const p
 }
 
 /* final radiance in output order (raster for pinhole, ray order otherwise) */
-void orc_final(void *s, const pm_record *recs, int64_t nrec, double emitted, float *out_rgb, int nthreads) {
+void orc_final_est(void *s, const pm_record *recs, int64_t nrec, double emitted, int estimator, float *out_rgb,
+                   int nthreads) {
     Scene &S = *(Scene *)s;
     float E = (float)emitted;
     parallel_for(nrec, nthreads, [&](int64_t r) {
@@ -1129,8 +1221,11 @@ void orc_final(void *s, const pm_record *recs, int64_t nrec, double emitted, flo
             if (px >= S.W || py >= S.H) return;
             pix = (int64_t)py * S.W + px;
         }
-        final_radiance(recs[r], E, &out_rgb[3 * pix]);
+        final_radiance(S, recs[r], E, estimator, &out_rgb[3 * pix]);
     });
+}
+void orc_final(void *s, const pm_record *recs, int64_t nrec, double emitted, float *out_rgb, int nthreads) {
+    orc_final_est(s, recs, nrec, emitted, PM_ESTIMATOR_PPM, out_rgb, nthreads);
 }
 
 /* whole pipeline: PhotonMappingRenderer::render (photonmappingrenderer.cpp:31-45) */
@@ -1150,7 +1245,7 @@ int orc_render(void *s, const pm_render_params *P, float *out_rgb, pm_stats *st,
         orc_gather(s, nodes.data(), nvalid, recs.data(), nrec, P, counters, nthreads);
     }
     double emitted = (double)P->paths_per_pass * P->passes;
-    orc_final(s, recs.data(), nrec, emitted, out_rgb, nthreads);
+    orc_final_est(s, recs.data(), nrec, emitted, P->estimator, out_rgb, nthreads);
     if (st) {
         std::memset(st, 0, sizeof(*st));
         st->paths_emitted = (int64_t)emitted;

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Generates tests/golden/golden_v1.npz — regression fixtures for the photon
+"""Generates tests/golden/golden_v2.npz — regression fixtures for the photon
 mapper, produced by the CPU oracle (oracle/pm_oracle.cpp).
 
 The reference ships no tests, fixtures or golden vectors and cannot be built
@@ -10,7 +10,7 @@ tests/test_golden.py checks the oracle (CPU) and the HIP path (GPU) against
 them. Arrays are raw bytes of the C-ABI structs (pm_record 64 B, pm_photon
 40 B) or plain numeric arrays; no pickled objects.
 
-    python tests/golden/make_golden.py        # rewrites golden_v1.npz
+    python tests/golden/make_golden.py        # rewrites golden_v2.npz
 """
 import json
 import os
@@ -22,7 +22,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path[:0] = [os.path.join(ROOT, "cuda-raytrace_amd"), os.path.join(ROOT, "oracle")]
 
-OUT = os.path.join(HERE, "golden_v1.npz")
+OUT = os.path.join(HERE, "golden_v2.npz")
 
 CASES = {
     # name: (scene builder args, paths per pass, passes, initial r^2)

@@ -28,3 +28,50 @@ def compare_gathered_records(gpu, ref, flux_rtol=2e-5):
     scale = np.maximum(np.abs(ref["flux"]), 1e-30)
     rel = np.abs(gpu["flux"] - ref["flux"]) / scale
     assert rel.max() <= flux_rtol, f"flux rel err {rel.max():.3g}"
+
+
+def knn_reference(recs, photons, K, maxd2):
+    """Brute-force statement of pbrt-v2's kNN photon lookup + LPhoton diffuse
+    sum (integrators/photonmap.cpp; see oracle knn_estimate) for records whose
+    material is matte: per record (photons found, r_k^2, S) with S the sum
+    over found photons with Dot(Faceforward(ns, wo), wi) > 0 of
+    3/pi (1 - d^2/r_k^2)^2 / r_k^2 * alpha (float64 accumulate). d^2 in
+    float32 with the kernels' operation order."""
+    from pmrender.abi import PM_REC_BACKFACE
+    n = len(recs)
+    found = np.zeros(n, np.int64)
+    r2 = np.full(n, np.float32(maxd2), np.float32)
+    S = np.zeros((n, 3), np.float64)
+    for i in range(n):
+        diff = recs["pos"][i][None, :] - photons["p"]
+        d2 = (diff[:, 0] * diff[:, 0] + diff[:, 1] * diff[:, 1]) + diff[:, 2] * diff[:, 2]
+        idx = np.nonzero(d2 < np.float32(maxd2))[0]
+        idx = idx[np.argsort(d2[idx], kind="stable")][:K]
+        found[i] = len(idx)
+        if len(idx) == K:
+            r2[i] = d2[idx[-1]]
+        ns = recs["ns"][i].astype(np.float64)
+        if recs["flags"][i] & PM_REC_BACKFACE:
+            ns = -ns
+        md2 = np.float64(r2[i])
+        for j in idx:
+            if float(photons["wi"][j].astype(np.float64) @ ns) > 0:
+                if md2 == 0.0:   # K photons at distance 0: pbrt's kernel() is 0/0
+                    S[i] = np.nan
+                    continue
+                s = 1.0 - float(d2[j]) / md2
+                S[i] += 3.0 / np.pi * s * s / md2 * photons["alpha"][j].astype(np.float64)
+    return found, r2, S
+
+
+def compare_knn_records(got, found, r2, flux, flux_rtol=1e-4):
+    """kNN records: photons found and r_k^2 exact; flux to fp32 summation tolerance."""
+    assert np.array_equal(got["photon_count"].astype(np.int64), found), "kNN photons found differ"
+    assert np.array_equal(u32(got["radius2"]), u32(np.asarray(r2, np.float32))), "kNN r_k^2 differs"
+    flux = np.asarray(flux, np.float64)
+    g = np.asarray(got["flux"], np.float64)
+    assert np.array_equal(np.isnan(g), np.isnan(flux)), "kNN NaN records differ"
+    ok = ~np.isnan(flux)
+    scale = max(float(np.abs(flux[ok]).max()), 1e-30)
+    err = float(np.abs(g[ok] - flux[ok]).max())
+    assert err <= flux_rtol * scale, f"kNN flux err {err:.3g} of max {scale:.3g}"

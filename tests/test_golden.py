@@ -1,4 +1,4 @@
-"""Committed golden fixtures (tests/golden/golden_v1.npz, made by
+"""Committed golden fixtures (tests/golden/golden_v2.npz, made by
 tests/golden/make_golden.py from the CPU oracle). The reference has no
 golden vectors of its own, so these freeze the oracle's
 restatement: the oracle must reproduce them on the CPU, and the HIP path must
@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "golden"))
 import make_golden  # noqa: E402
 
-GOLDEN = np.load(os.path.join(HERE, "golden", "golden_v1.npz"), allow_pickle=False)
+GOLDEN = np.load(os.path.join(HERE, "golden", "golden_v2.npz"), allow_pickle=False)
 
 
 def test_fixture_metadata_matches_generator():

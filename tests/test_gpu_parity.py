@@ -172,8 +172,8 @@ def test_grid_gather_parity(cornell, radius2):
 
 @pytest.mark.parametrize("radius2", [4.0, 25.0, 400.0])
 def test_wave_gather_equals_lane_gather(radius2, oracle_mod, hip_mod, monkeypatch):
-    """The wave-cooperative bucket gather (default) and the per-lane kernel
-    (PM_GATHER_WAVE=0) find the same photons: fused records and split
+    """The wave-cooperative bucket gather (PM_GATHER_WAVE=1, experiment) and
+    the per-lane kernel (default) find the same photons: fused records and split
     partials bit-identical. radius2 400 exceeds the grid's design radius for
     uploaded records -> the wave kernel's per-lane fallback."""
     torch = pytest.importorskip("torch")
@@ -441,3 +441,60 @@ def test_full_size_c2_parity(oracle_mod, hip_mod):
     ref, st_ref = orc.render(p)
     assert st["photons_valid"] == st_ref["photons_valid"]
     assert rmse(img, ref) < 1e-3
+
+
+# ---- kNN estimator (pbrt-v2 LPhoton, PM_ESTIMATOR_KNN) ----------------------
+@pytest.mark.parametrize("K,radius2", [(50, 900.0), (16, 400.0), (64, 2500.0), (1, 25.0)])
+def test_knn_gather_parity(cornell, K, radius2):
+    """k_gather_knn over the photon buckets vs the oracle's pbrt kd-tree
+    lookup (shrinking radius, PhotonProcess heap): photons found and r_k^2
+    bit-exact, flux to fp32 summation order; two passes accumulate."""
+    from parity_util import compare_knn_records
+    from pmrender.abi import PM_ESTIMATOR_KNN
+    ctx, orc = cornell
+    p = RenderParams.defaults(paths_per_pass=16384, initial_radius2=radius2, estimator=PM_ESTIMATOR_KNN,
+                              knn_lookup=K)
+    recs = orc.eye_pass(p)
+    ref = recs.copy()
+    ctx.upload_records(recs)
+    for pass_index in range(2):
+        slots = orc.trace_photons(p, pass_index, 0, 16384)
+        ctx.upload_slots(slots)
+        ctx.build_photon_map(p, len(slots))
+        ctx.gather(p)
+        orc.gather(orc.build_kdtree(slots), ref, p)
+    got = ctx.download_records()
+    act = (ref["flags"] & 7) == 0
+    assert (ref["photon_count"][act] == K).mean() > 0.2 and (ref["photon_count"][act] < K).any()
+    compare_knn_records(got, ref["photon_count"].astype(np.int64), ref["radius2"], ref["flux"])
+
+
+def test_knn_render_parity(cornell):
+    """Whole render with the kNN estimator: image RMSE < 1e-3 vs the oracle,
+    deterministic run to run."""
+    from pmrender.abi import PM_ESTIMATOR_KNN
+    ctx, orc = cornell
+    p = RenderParams.defaults(paths_per_pass=32768, passes=2, initial_radius2=400.0, estimator=PM_ESTIMATOR_KNN)
+    img, st = ctx.render(p)
+    ref, st_ref = orc.render(p)
+    assert st["photons_valid"] == st_ref["photons_valid"]
+    assert rmse(img, ref) < 1e-3
+    assert np.abs(img - ref).max() <= 1e-4 * max(1.0, float(ref.max()))
+    again, _ = ctx.render(p)
+    assert np.array_equal(img.view(np.uint32), again.view(np.uint32))
+
+
+def test_knn_rejects_partial_gathers(cornell, hip_mod):
+    torch = pytest.importorskip("torch")
+    from pmrender.abi import PM_ESTIMATOR_KNN
+    ctx, orc = cornell
+    p = RenderParams.defaults(paths_per_pass=4096, estimator=PM_ESTIMATOR_KNN)
+    ctx.eye_pass(p)
+    ctx.trace_photons(p, 0, 0, 4096)
+    ctx.build_photon_map(p, 4096 * 4)
+    part = torch.zeros((ctx.num_records(), 4), dtype=torch.int64, device="cuda")
+    with pytest.raises(hip_mod.PMError):
+        ctx.gather_partial(p, part.data_ptr())
+    with pytest.raises(hip_mod.PMError):
+        ctx.gather(RenderParams.defaults(paths_per_pass=4096, estimator=PM_ESTIMATOR_KNN,
+                                         gather_structure=PM_GATHER_KDTREE))

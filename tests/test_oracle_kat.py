@@ -287,3 +287,47 @@ def test_oracle_render_deterministic_and_sane(oracle_mod):
     assert sa["photons_valid"] == sb["photons_valid"] > 0
     assert np.isfinite(ia).all() and (ia >= 0).all()
     assert ia.max() == pytest.approx(17.0)   # pixels seeing the emitter: Le = 17 (lightL, cudalight.cu.h:128-138)
+
+
+# ---- kNN estimator (pbrt-v2 PhotonIntegrator LPhoton, PM_ESTIMATOR_KNN) -----
+@pytest.mark.parametrize("K,maxd2", [(50, 16.0), (8, 1.0), (64, 9.0), (1, 0.5)])
+def test_kdtree_knn_matches_brute_force(oracle_mod, K, maxd2):
+    """pbrt's kd-tree kNN lookup with the shrinking radius (oracle kd_knn +
+    PhotonProcess heap) == sorting all photons by d^2: same photons found,
+    same r_k^2 bits, same LPhoton sum; back-facing records use -ns."""
+    from parity_util import compare_knn_records, knn_reference
+    from pmrender.abi import PM_ESTIMATOR_KNN, PM_REC_BACKFACE
+    ph = _random_photons(6000, 5)
+    nodes = oracle_mod.Oracle.build_kdtree(ph)
+    valid = ph[(ph["bits"] & 1) == 1]
+    orc = oracle_mod.Oracle(nthreads=2)
+    orc.add_material(PM_MATTE, (0.5, 0.25, 1.0))
+    rng = np.random.RandomState(6)
+    recs = np.zeros(400, dtype=RECORD_DTYPE)
+    recs["pos"] = rng.uniform(0, 20, (400, 3)).astype(np.float32)
+    recs["pos"][:40] = valid["p"][:40]
+    ns = rng.normal(size=(400, 3))
+    recs["ns"] = (ns / np.linalg.norm(ns, axis=1, keepdims=True)).astype(np.float32)
+    recs["flags"][::3] = PM_REC_BACKFACE
+    recs["flux"] = 0.25
+    p = RenderParams.defaults(estimator=PM_ESTIMATOR_KNN, knn_lookup=K, initial_radius2=maxd2)
+    out = recs.copy()
+    orc.gather(nodes, out, p)
+    found, r2, S = knn_reference(recs, valid, K, maxd2)
+    assert found.max() == K                  # heaps fill (radius shrinks) for some records
+    compare_knn_records(out, found, r2, 0.25 + S)
+
+
+def test_knn_final_radiance(oracle_mod):
+    """kNN final pass: L = direct + flux / paths * Kd/pi (LPhoton's rho/pi)."""
+    from pmrender.abi import PM_ESTIMATOR_KNN
+    orc = oracle_mod.Oracle(nthreads=1)
+    orc.add_material(PM_MATTE, (0.5, 0.25, 1.0))
+    recs = np.zeros(2, dtype=RECORD_DTYPE)
+    recs["flux"] = [[100.0, 200.0, 300.0], [1.0, 1.0, 1.0]]
+    recs["dl"] = [[1.0, 2.0, 3.0], [0.0, 0.0, 0.0]]
+    recs["flags"][1] = 2  # MISS: black
+    img = orc.final(recs, 1000.0, estimator=PM_ESTIMATOR_KNN)
+    kd = np.float32([0.5, 0.25, 1.0]) * np.float32(0.31830988618379067154)
+    want = np.float32([1, 2, 3]) + (np.float32([100, 200, 300]) * (np.float32(1) / np.float32(1000))) * kd
+    assert np.array_equal(img[0], want) and not img[1].any()
