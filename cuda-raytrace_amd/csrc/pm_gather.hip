@@ -283,63 +283,113 @@ __global__ __launch_bounds__(GATHER_BLOCK, 8) void k_gather_wave(GatherParams P)
 /* ---------------------------------------------------------------------- */
 /* kNN estimator: pbrt-v2 PhotonIntegrator::LPhoton (integrators/photonmap.cpp,
  * diffuse branch) with PhotonProcess / KdTree::Lookup semantics, over the
- * photon buckets. Per record (one lane): the K photons with the smallest
- * keys (d^2, slot) among those with d^2 < maxD2 (the buckets cover that
- * radius) are kept in a max-heap in LDS — the set pbrt's lookup finds, up to
- * the order among photons at exactly equal d^2, where the lower slot wins
- * here and the first visited in pbrt. r_k^2 = the heap top's d^2 once K
- * were found (pbrt's shrunk maxDistSquared), else maxD2. Then
+ * photon buckets. Per record (one lane), the found set is the K photons with
+ * the smallest keys (d^2, slot) among those with d^2 < maxD2 — the set pbrt's
+ * lookup finds, up to the order among photons at exactly equal d^2, where
+ * the lower slot wins here and the first visited in pbrt. r_k^2 = the K-th
+ * smallest d^2 once K were found (pbrt's shrunk maxDistSquared), else maxD2.
  *     S = sum over found photons with Dot(Nf, wi) > 0 of
  *         (3/pi (1 - d^2/r_k^2)^2 / r_k^2) * alpha        (kernel(), photonmap.cpp)
- * with Nf = Faceforward(ns, wo) (PM_REC_BACKFACE). The sum is exact and
- * order-free in int64 fixed point (scale: the power of two below
- * knn_fx * r_k^2, every term being <= alpha_max / r_k^2). Fused record
- * update: flux += S, radius2 = r_k^2, photon_count = found; the final pass
- * applies 1/paths and rho/pi = Kd/pi (k_final). */
-PMD bool key_less(uint32_t ad, uint32_t as, uint32_t bd, uint32_t bs) { return ad < bd || (ad == bd && as < bs); }
+ * with Nf = Faceforward(ns, wo) (PM_REC_BACKFACE).
+ * Two passes over the buckets: (1) a max-heap of d^2 values alone (4 B per
+ * entry, LDS columns [K][64]) finds r_k^2; (2) a rescan bounded by r_k^2 sums
+ * the photons with d^2 < r_k^2 and, of those at exactly r_k^2, the lowest
+ * slots (slot ids ride in ph_b; a third scan runs only when more ties than
+ * places exist). The sum is exact and order-free in int64 fixed point
+ * (scale: the power of two below knn_fx * r_k^2, every term being
+ * <= alpha_max / r_k^2). Fused record update: flux += S, radius2 = r_k^2,
+ * photon_count = found; the final pass applies 1/paths and rho/pi = Kd/pi
+ * (k_final). Both passes visit rows in rings around the query's row,
+ * nearest first, and skip rows / cells beyond the current bound. */
 PMD float sq(float x) { return x * x; }
 /* distance, in cell units, from coordinate u (cell units) to cell c of an
  * axis with dim cells — the border cells extend to infinity (cell_axis
  * clamps) — less a 1e-3 margin that covers the float rounding of u and of the
- * photons' own d^2, so pruning with it never drops a photon the heap takes */
+ * photons' own d^2, so pruning with it never drops a photon that counts */
 PMD float cell_gap(float u, uint32_t c, int dim) {
     const float lo = c == 0 ? -INFINITY : (float)c, hi = (int)c + 1 == dim ? INFINITY : (float)(c + 1);
     return fmaxf(fmaxf(lo - u, u - hi) - 1e-3f, 0.f);
 }
-/* max-heap of (d^2 bits, slot) in LDS columns: entry k of this lane at [k * KNN_BLOCK] */
-PMD void heap_push(uint32_t *hd, uint32_t *hs, int n, uint32_t d, uint32_t sl) {
+/* max-heap of d^2 bits in LDS columns: entry k of this lane at h[k * KNN_BLOCK] */
+PMD void heap_push(uint32_t *h, int n, uint32_t d) {
     int i = n;
     while (i > 0) {
         const int pa = (i - 1) >> 1;
-        const uint32_t pd = hd[pa * KNN_BLOCK], ps = hs[pa * KNN_BLOCK];
-        if (!key_less(pd, ps, d, sl)) break;
-        hd[i * KNN_BLOCK] = pd; hs[i * KNN_BLOCK] = ps;
+        const uint32_t pd = h[pa * KNN_BLOCK];
+        if (pd >= d) break;
+        h[i * KNN_BLOCK] = pd;
         i = pa;
     }
-    hd[i * KNN_BLOCK] = d; hs[i * KNN_BLOCK] = sl;
+    h[i * KNN_BLOCK] = d;
 }
-PMD void heap_replace_top(uint32_t *hd, uint32_t *hs, int n, uint32_t d, uint32_t sl) {
+PMD void heap_replace_top(uint32_t *h, int n, uint32_t d) {
     int i = 0;
     while (true) {
         int c = 2 * i + 1;
         if (c >= n) break;
-        uint32_t cd = hd[c * KNN_BLOCK], cs = hs[c * KNN_BLOCK];
+        uint32_t cd = h[c * KNN_BLOCK];
         if (c + 1 < n) {
-            const uint32_t rd = hd[(c + 1) * KNN_BLOCK], rs = hs[(c + 1) * KNN_BLOCK];
-            if (key_less(cd, cs, rd, rs)) { c = c + 1; cd = rd; cs = rs; }
+            const uint32_t rd = h[(c + 1) * KNN_BLOCK];
+            if (rd > cd) { c = c + 1; cd = rd; }
         }
-        if (!key_less(d, sl, cd, cs)) break;
-        hd[i * KNN_BLOCK] = cd; hs[i * KNN_BLOCK] = cs;
+        if (d >= cd) break;
+        h[i * KNN_BLOCK] = cd;
         i = c;
     }
-    hd[i * KNN_BLOCK] = d; hs[i * KNN_BLOCK] = sl;
+    h[i * KNN_BLOCK] = d;
 }
+
+/* the bucket rows around p within sqrt(maxd2), nearest rings first; bound()
+ * (in world units^2) is re-read per row; visit(j, d2) per photon of the kept
+ * cells. Returns nothing; COUNT census through vis / rows. */
+struct KnnGrid {
+    const GridDesc *g;
+    uint32_t x0, x1, y0, y1, z0, z1;
+    int cyc, czc, rings;
+    float ux, uy, uz, inv2;
+    PMD void init(const GridDesc &G, v3 p, float maxd2) {
+        g = &G;
+        const float rq = sqrtf(maxd2) * 1.0001f + 1e-4f;
+        x0 = cell_axis(p.x - rq, G.gx, G.inv_cs, G.dx); x1 = cell_axis(p.x + rq, G.gx, G.inv_cs, G.dx);
+        y0 = cell_axis(p.y - rq, G.gy, G.inv_cs, G.dy); y1 = cell_axis(p.y + rq, G.gy, G.inv_cs, G.dy);
+        z0 = cell_axis(p.z - rq, G.gz, G.inv_cs, G.dz); z1 = cell_axis(p.z + rq, G.gz, G.inv_cs, G.dz);
+        cyc = (int)cell_axis(p.y, G.gy, G.inv_cs, G.dy); czc = (int)cell_axis(p.z, G.gz, G.inv_cs, G.dz);
+        /* the query point in cell units (cell_axis before the floor) */
+        ux = (p.x - G.gx) * G.inv_cs; uy = (p.y - G.gy) * G.inv_cs; uz = (p.z - G.gz) * G.inv_cs;
+        inv2 = G.inv_cs * G.inv_cs;
+        rings = max((int)(y1 - y0), (int)(z1 - z0));
+    }
+    template <class B, class V>
+    PMD void scan(const uint32_t *cell_start, const float4 *ph_a, v3 p, B bound, V visit, unsigned long long &vis,
+                  unsigned long long &rows) const {
+        for (int ring = 0; ring <= rings; ++ring)
+            for (uint32_t cz = z0; cz <= z1; ++cz)
+                for (uint32_t cy = y0; cy <= y1; ++cy) {
+                    if (max(abs((int)cy - cyc), abs((int)cz - czc)) != ring) continue;
+                    const float gy = cell_gap(uy, cy, g->dy), gz = cell_gap(uz, cz, g->dz);
+                    const float lim = bound() * inv2 - (gy * gy + gz * gz);
+                    if (lim < 0.f) continue;
+                    uint32_t xa = x0, xb = x1;
+                    while (xa <= xb && sq(cell_gap(ux, xa, g->dx)) > lim) ++xa;
+                    while (xb > xa && sq(cell_gap(ux, xb, g->dx)) > lim) --xb;
+                    if (xa > xb) continue;
+                    const uint32_t row = (cz * (uint32_t)g->dy + cy) * (uint32_t)g->dx;
+                    const uint32_t b = cell_start[row + xa], e = cell_start[row + xb + 1];
+                    vis += e - b; rows++;
+                    for (uint32_t j = b; j < e; ++j) {
+                        const float4 a = ph_a[j];
+                        const v3 diff = p - xyz(a);
+                        visit(j, a, diff.x * diff.x + diff.y * diff.y + diff.z * diff.z);
+                    }
+                }
+    }
+};
 
 template <int COUNT>
 __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn(GatherParams P) {
-    extern __shared__ uint32_t kheap[]; /* [K][KNN_BLOCK] d^2 bits, then [K][KNN_BLOCK] slots */
+    extern __shared__ uint32_t kheap[]; /* [K][KNN_BLOCK] d^2 bits */
     const int K = P.knn_k;
-    uint32_t *hd = kheap + threadIdx.x, *hs = kheap + K * KNN_BLOCK + threadIdx.x;
+    uint32_t *h = kheap + threadIdx.x;
     const int64_t r = P.rec_begin + (int64_t)blockIdx.x * KNN_BLOCK + threadIdx.x;
     unsigned long long vis = 0, hits = 0, rows = 0, act = 0;
     if (r < P.rec_end) {
@@ -357,74 +407,70 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn(GatherParams P) {
             float sc = 1.f;
             bool nan = false;
             if (__float_as_int(m.w) == PM_MATTE) { /* non-specular BSDF components only */
-                const GridDesc &g = P.grid;
-                const float rq = sqrtf(maxd2) * 1.0001f + 1e-4f;
-                const uint32_t x0 = cell_axis(p.x - rq, g.gx, g.inv_cs, g.dx), x1 = cell_axis(p.x + rq, g.gx, g.inv_cs, g.dx);
-                const uint32_t y0 = cell_axis(p.y - rq, g.gy, g.inv_cs, g.dy), y1 = cell_axis(p.y + rq, g.gy, g.inv_cs, g.dy);
-                const uint32_t z0 = cell_axis(p.z - rq, g.gz, g.inv_cs, g.dz), z1 = cell_axis(p.z + rq, g.gz, g.inv_cs, g.dz);
-                const int cyc = (int)cell_axis(p.y, g.gy, g.inv_cs, g.dy), czc = (int)cell_axis(p.z, g.gz, g.inv_cs, g.dz);
-                /* the query point in cell units (cell_axis before the floor) */
-                const float ux = (p.x - g.gx) * g.inv_cs, uy = (p.y - g.gy) * g.inv_cs, uz = (p.z - g.gz) * g.inv_cs;
-                const float inv2 = g.inv_cs * g.inv_cs;
-                const int rings = max((int)(y1 - y0), (int)(z1 - z0));
-                uint32_t topd = 0xffffffffu, tops = 0xffffffffu; /* heap top, once full */
-                const float *phb = reinterpret_cast<const float *>(P.ph_b);
-                /* rows (y, z) in rings around the query's row, nearest first, so
-                 * the heap fills early and the k-th distance prunes the rest:
-                 * a row / cell is skipped when its (margin-reduced) distance
-                 * exceeds the current bound — every photon in it would fail
-                 * d^2 < maxD2, or d^2 <= top once the heap is full */
-                for (int ring = 0; ring <= rings; ++ring)
-                    for (uint32_t cz = z0; cz <= z1; ++cz)
-                        for (uint32_t cy = y0; cy <= y1; ++cy) {
-                            if (max(abs((int)cy - cyc), abs((int)cz - czc)) != ring) continue;
-                            const float bound = (cnt == K ? __uint_as_float(topd) : maxd2) * inv2;
-                            const float gy = cell_gap(uy, cy, g.dy), gz = cell_gap(uz, cz, g.dz);
-                            const float lim = bound - (gy * gy + gz * gz);
-                            if (lim < 0.f) continue;
-                            uint32_t xa = x0, xb = x1;
-                            while (xa <= xb && sq(cell_gap(ux, xa, g.dx)) > lim) ++xa;
-                            while (xb > xa && sq(cell_gap(ux, xb, g.dx)) > lim) --xb;
-                            if (xa > xb) continue;
-                            const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
-                            const uint32_t b = P.cell_start[row + xa], e = P.cell_start[row + xb + 1];
-                            if (COUNT) { vis += e - b; rows++; }
-                            for (uint32_t j = b; j < e; ++j) {
-                                const float4 a = P.ph_a[j];
-                                const v3 diff = p - xyz(a);
-                                const float d2 = diff.x * diff.x + diff.y * diff.y + diff.z * diff.z;
-                                if (!(d2 < maxd2)) continue;
-                                const uint32_t db = __float_as_uint(d2); /* d2 >= 0: bits order = value order */
-                                if (cnt == K && db > topd) continue;
-                                const uint32_t sl = __float_as_uint(phb[8 * (size_t)j + 5]);
-                                if (cnt < K) {
-                                    heap_push(hd, hs, cnt, db, sl);
-                                    if (++cnt == K) { topd = hd[0]; tops = hs[0]; }
-                                } else if (db < topd || sl < tops) {
-                                    heap_replace_top(hd, hs, K, db, sl);
-                                    topd = hd[0]; tops = hs[0];
-                                }
-                            }
-                        }
-                if (cnt == K) md2 = __uint_as_float(topd);
+                KnnGrid G;
+                G.init(P.grid, p, maxd2);
+                /* pass 1: r_k^2 */
+                uint32_t topd = 0xffffffffu;
+                G.scan(P.cell_start, P.ph_a, p, [&]() { return cnt == K ? __uint_as_float(topd) : maxd2; },
+                       [&](uint32_t, const float4 &, float d2) {
+                           if (!(d2 < maxd2)) return;
+                           const uint32_t db = __float_as_uint(d2); /* d2 >= 0: bits order = value order */
+                           if (cnt < K) {
+                               heap_push(h, cnt, db);
+                               if (++cnt == K) topd = h[0];
+                           } else if (db < topd) {
+                               heap_replace_top(h, K, db);
+                               topd = h[0];
+                           }
+                       }, vis, rows);
+                const bool full = cnt == K;
+                if (full) md2 = __uint_as_float(topd);
+                sc = md2 == 0.f ? 1.f : __uint_as_float(__float_as_uint(P.knn_fx * md2) & 0xff800000u); /* 2^n: exact */
                 const bool back = (flags & PM_REC_BACKFACE) != 0;
-                sc = __uint_as_float(__float_as_uint(P.knn_fx * md2) & 0xff800000u); /* power of two: exact scaling */
-                if (md2 == 0.f) sc = 1.f;
-                for (int k = 0; k < cnt; ++k) {
-                    const float d2 = __uint_as_float(hd[k * KNN_BLOCK]);
-                    const float2 *q = reinterpret_cast<const float2 *>(P.slots + hs[k * KNN_BLOCK]);
-                    const float2 q2 = q[2], q3 = q[3], q4 = q[4]; /* (alpha.x, alpha.y) (alpha.z, wi.x) (wi.y, wi.z) */
-                    float dn = dot(ns, mk(q3.y, q4.x, q4.y));
+                const float *phb = reinterpret_cast<const float *>(P.ph_b);
+                /* contribution of photon j (LPhoton term) into a */
+                auto add = [&](Fx3 &a, uint32_t j, const float4 &pa, float d2) {
+                    const float4 b0 = P.ph_b[2 * (size_t)j];
+                    float dn = dot(ns, mk(pa.w, b0.w, phb[8 * (size_t)j + 4]));
                     if (back) dn = -dn; /* Dot(Faceforward(ns, wo), wi) */
-                    if (dn > 0.f && md2 == 0.f) { /* K photons at distance 0: pbrt's kernel() is 0/0 */
-                        nan = true;
-                    } else if (dn > 0.f) {
-                        const float s = 1.f - d2 / md2;
-                        const float kk = 3.f * INV_PI * s * s;
-                        const v3 c = (kk / md2) * mk(q2.x, q2.y, q3.x);
-                        acc.x += to_fx(c.x, sc); acc.y += to_fx(c.y, sc); acc.z += to_fx(c.z, sc);
+                    if (!(dn > 0.f)) return;
+                    if (md2 == 0.f) { nan = true; return; } /* K photons at distance 0: kernel() is 0/0 */
+                    const float s = 1.f - d2 / md2;
+                    const float kk = 3.f * INV_PI * s * s;
+                    const v3 c = (kk / md2) * xyz(b0);
+                    a.x += to_fx(c.x, sc); a.y += to_fx(c.y, sc); a.z += to_fx(c.z, sc);
+                };
+                /* pass 2: every photon below r_k^2 (all below maxD2 when not full);
+                 * ties at r_k^2 aside */
+                int less = 0, ties = 0;
+                Fx3 acc_eq{0, 0, 0};
+                G.scan(P.cell_start, P.ph_a, p, [&]() { return md2; },
+                       [&](uint32_t j, const float4 &pa, float d2) {
+                           if (d2 < md2) { less++; add(acc, j, pa, d2); }
+                           else if (full && d2 == md2) { ties++; add(acc_eq, j, pa, d2); }
+                       }, vis, rows);
+                const int need = full ? K - less : 0;
+                if (ties == need) {
+                    acc.x += acc_eq.x; acc.y += acc_eq.y; acc.z += acc_eq.z;
+                } else {
+                    /* more photons at exactly r_k^2 than places: the lowest slots (rare) */
+                    uint32_t last = 0u;
+                    bool first = true;
+                    for (int t = 0; t < need; ++t) {
+                        uint32_t best = 0xffffffffu, bj = 0u;
+                        float4 ba = make_float4(0.f, 0.f, 0.f, 0.f);
+                        G.scan(P.cell_start, P.ph_a, p, [&]() { return md2; },
+                               [&](uint32_t j, const float4 &pa, float d2) {
+                                   if (d2 != md2) return;
+                                   const uint32_t sl = __float_as_uint(phb[8 * (size_t)j + 5]);
+                                   if ((first || sl > last) && sl <= best) { best = sl; bj = j; ba = pa; }
+                               }, vis, rows);
+                        add(acc, bj, ba, md2);
+                        last = best;
+                        first = false;
                     }
                 }
+                cnt = full ? K : less;
             }
             if (COUNT) { hits += (unsigned long long)cnt; act++; }
             const double inv = 1.0 / (double)sc;
@@ -442,7 +488,7 @@ hipError_t launch_gather_knn(const GatherParams &p, int count, hipStream_t s) {
     if (p.rec_end <= p.rec_begin) return hipSuccess;
     if (p.knn_k < 1 || p.knn_k > PM_KNN_MAX) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)((p.rec_end - p.rec_begin + KNN_BLOCK - 1) / KNN_BLOCK);
-    const uint32_t lds = (uint32_t)(2 * p.knn_k * KNN_BLOCK * sizeof(uint32_t));
+    const uint32_t lds = (uint32_t)(p.knn_k * KNN_BLOCK * sizeof(uint32_t));
     if (count) pm_launch(k_gather_knn<1>, dim3(grid), dim3(KNN_BLOCK), lds, s, p);
     else pm_launch(k_gather_knn<0>, dim3(grid), dim3(KNN_BLOCK), lds, s, p);
     return hipGetLastError();
