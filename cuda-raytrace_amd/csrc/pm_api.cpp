@@ -871,6 +871,13 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
     T.S = c->S;
     T.slots = c->d_slots.as<pm_photon>();
     halton_perm((uint32_t)pass, T.perm);
+    {
+        const uint32_t base[3] = {3u, 5u, 7u}, off[3] = {2u, 5u, 10u};
+        for (int k = 0; k < 3; ++k) {
+            T.perm_bits[k] = 0u;
+            for (uint32_t d = 0; d < base[k]; ++d) T.perm_bits[k] |= T.perm[off[k] + d] << (3u * d);
+        }
+    }
     T.path_begin = path_begin; T.path_count = path_count; T.slot_path_base = slot_path_base;
     T.per_block = c->trace_per_block;
     T.wave_paths = c->trace_wave_paths;

@@ -171,34 +171,62 @@ PMD float permuted_radical_inverse(uint32_t n, uint32_t base, const uint32_t *p)
 }
 
 /* The four dimensions (bases 2, 3, 5, 7; table offsets 0, 2, 5, 10) of
- * photontracing.cu:33-43 as four interleaved chains of one loop, so their
- * independent digit steps overlap instead of running as four serial loops.
- * Each chain is exactly permuted_radical_inverse; base 2 has the most digits
- * (every chain's n stays <= base 2's), so it bounds the loop. */
-PMD void permuted_halton4(uint32_t n, const uint32_t *p, float out[4]) {
-    const uint32_t base[4] = {2u, 3u, 5u, 7u}, off[4] = {0u, 2u, 5u, 10u};
-    float val[4], invBase[4], invBi[4];
-    uint32_t m[4];
+ * photontracing.cu:33-43, each exactly permuted_radical_inverse:
+ *  - base 2 in closed form for n < 2^24: there the quirk n *= 0.5f is an exact
+ *    shift, so the digits are the L = bitlength(n) bits of n, and every term
+ *    d_i * 2^-(i+1) and partial sum is an exact dyadic fraction (<= 24
+ *    significant bits): the loop's float sum equals rev = brev(n) / 2^32
+ *    (table (0,1)) or (1 - 2^-L) - rev (table (1,0)) bit for bit;
+ *  - bases 3, 5, 7 as three interleaved chains of one loop (independent
+ *    digit steps overlap), bounded by base 3, which has the most digits. The
+ *    permutation tables come packed, 3 bits per digit (pbits[k] >> 3r & 7:
+ *    no LDS load in the digit chain). Below 12,582,912 the quirk's
+ *    truncated product equals floor(m / base) for these bases (exhaustive
+ *    check over all m < 2^24: first mismatch at 12,582,912 for base 7 and
+ *    12,582,914 for base 3), so the digit is m - base * next instead of a
+ *    modulo; larger indices (C4/C5) take the modulo. */
+template <bool EXACT>
+PMD void halton_chains(uint32_t n, const uint32_t pbits[3], float out[3]) {
+    const uint32_t base[3] = {3u, 5u, 7u};
+    float val[3], invBase[3], invBi[3];
+    uint32_t m[3];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 3; ++k) {
         val[k] = 0.f;
         invBase[k] = 1.f / base[k];
         invBi[k] = invBase[k];
         m[k] = n;
     }
-    while ((m[0] | m[1] | m[2] | m[3]) != 0u) {
+    while ((m[0] | m[1] | m[2]) != 0u) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < 3; ++k) {
             if (m[k] > 0) {
-                const uint32_t d_i = p[off[k] + m[k] % base[k]];
+                const uint32_t next = (uint32_t)((float)m[k] * invBase[k]); /* reference quirk: n *= invBase */
+                const uint32_t r = EXACT ? m[k] - next * base[k] : m[k] % base[k];
+                const uint32_t d_i = (pbits[k] >> (3u * r)) & 7u;
                 val[k] += d_i * invBi[k];
-                m[k] = (uint32_t)((float)m[k] * invBase[k]); /* reference quirk: n *= invBase */
+                m[k] = next;
                 invBi[k] *= invBase[k];
             }
         }
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) out[k] = val[k];
+    for (int k = 0; k < 3; ++k) out[k] = val[k];
+}
+PMD void permuted_halton4(uint32_t n, const uint32_t *p, const uint32_t pbits[3], float out[4]) {
+#ifdef PM_EXP_HALTON_CHEAP /* cost experiment only (not bit-exact): make variant */
+    for (int k = 0; k < 4; ++k) out[k] = (float)((n * (2654435761u + 2u * k)) >> 8) * (1.0f / 16777216.0f);
+    return;
+#endif
+    if (n < (1u << 24)) {
+        const float rev = (float)__builtin_bitreverse32(n) * 0x1p-32f;
+        const int L = n ? 32 - __builtin_clz(n) : 0;
+        out[0] = p[0] == 0u ? rev : (1.0f - __builtin_ldexpf(1.0f, -L)) - rev;
+    } else {
+        out[0] = permuted_radical_inverse(n, 2u, p);
+    }
+    if (n < 12582912u) halton_chains<true>(n, pbits, out + 1);
+    else halton_chains<false>(n, pbits, out + 1);
 }
 
 /* ------------------------------------------------------------ intersect */

@@ -78,6 +78,7 @@ struct TraceParams {
     SceneDev S;
     pm_photon *slots;
     uint32_t perm[28];
+    uint32_t perm_bits[3]; /* the base 3, 5, 7 tables of perm, 3 bits per digit (permuted_halton4) */
     int64_t path_begin, path_count, slot_path_base;
     int64_t per_block;  /* > 0: block-compacting kernel, paths per block pool; 0: per-lane kernel */
     int64_t wave_paths; /* per-lane kernel: paths per wave pool (>= 64; 64 = no refills) */

@@ -293,7 +293,7 @@ struct TProf {
 PMD bool emit_path(const TraceParams &P, const SceneDev &S, const uint32_t *perm, uint32_t pid, PathState &st) {
     const uint32_t pm_index = pid * (uint32_t)P.mpc;
     float smp[4];
-    permuted_halton4(pm_index, perm, smp);
+    permuted_halton4(pm_index, perm, P.perm_bits, smp);
     const LightDev Lt = S.lights[P.light_index];
     v3 N1; float pdf;
     v3 Le = sample_le(Lt, smp[0], smp[1], smp[2], smp[3], P.eps, &st.ray, &N1, &pdf);
