@@ -73,6 +73,8 @@ struct Ctx {
     SceneDev S{};
     float bbox_lo[3] = {0, 0, 0}, bbox_hi[3] = {0, 0, 0};
     double emit_max = 1.0, kd_max = 1.0; /* bounds for the fixed-point flux scale */
+    bool scene_nonneg = true;  /* no negative emission / albedo component (fixed-point sums in double) */
+    bool slots_nonneg = true;  /* the slot buffer holds no negative flux (uploaded slots are checked) */
     int bvh_depth = 0;
     /* records */
     DevBuf d_pos, d_nrm, d_state, d_n, d_dl;
@@ -106,7 +108,8 @@ struct Ctx {
     int64_t trace_wave_paths = 64; /* per-lane kernel: paths per wave (env PM_TRACE_WAVE_PATHS) */
     int trace_refill_min = 32;     /* per-lane kernel: idle lanes that trigger a refill (env PM_TRACE_REFILL_MIN) */
     bool fuse_count = true;        /* bucket counting inside the trace kernel (env PM_FUSE_COUNT=0 disables) */
-    bool gather_wave = false;      /* wave-cooperative bucket gather (env PM_GATHER_WAVE=1; measured 2x slower) */
+    int gather_kernel = PM_GK_TILE; /* bucket gather kernel (env PM_GATHER_KERNEL=tile|lane|wave) */
+    bool gather_xcd = false;        /* tile gather: contiguous tile ranges per XCD (env PM_GATHER_XCD=1) */
     /* leading words of d_count known to be zero (the bucket scan clears the
      * counters it reads); valid while d_count.p == count_zero_ptr */
     size_t count_zero_words = 0;
@@ -310,7 +313,9 @@ GatherParams gather_params(Ctx *c, const pm_render_params *p) {
     G.ph_a = c->d_pha.as<float4>(); G.ph_b = c->d_phb.as<float4>();
     G.kd_nodes = c->d_kd.as<pm_photon>(); G.kd_count = c->kd_count;
     G.counters = c->d_counters.as<unsigned long long>();
-    G.wave = c->gather_wave ? 1 : 0;
+    G.kernel = c->gather_kernel;
+    G.fx_nonneg = c->scene_nonneg && c->slots_nonneg ? 1 : 0;
+    G.xcd = c->gather_xcd ? 1 : 0;
     if (c->view_active) { G.view_rank = c->d_vrank.as<uint32_t>(); G.view_list = c->d_vlist.as<uint32_t>(); }
     /* fixed-point scale 2^S: a single contribution is bounded by
      * alpha_max * Kd_max / pi with alpha_max = emission * Kd_max^mpc (Lambert
@@ -411,7 +416,10 @@ int pm_create(void **out, const pm_config *cfg) {
     if (const char *e = getenv("PM_TRACE_WAVE_PATHS")) c->trace_wave_paths = std::max(64LL, atoll(e));
     if (const char *e = getenv("PM_TRACE_REFILL_MIN")) c->trace_refill_min = std::max(1, std::min(64, atoi(e)));
     if (const char *e = getenv("PM_FUSE_COUNT")) c->fuse_count = atoi(e) != 0;
-    if (const char *e = getenv("PM_GATHER_WAVE")) c->gather_wave = atoi(e) != 0;
+    if (const char *e = getenv("PM_GATHER_KERNEL"))
+        c->gather_kernel = !strcmp(e, "lane") ? PM_GK_LANE : !strcmp(e, "wave") ? PM_GK_WAVE : PM_GK_TILE;
+    if (const char *e = getenv("PM_GATHER_WAVE")) if (atoi(e)) c->gather_kernel = PM_GK_WAVE;
+    if (const char *e = getenv("PM_GATHER_XCD")) c->gather_xcd = atoi(e) != 0;
     if (const char *e = getenv("PM_STAGE_TIMERS")) if (atoi(e) == 0) c->timed_stages.clear();
     (void)hipSetDevice(dev);
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -753,6 +761,11 @@ int pm_commit(void *ptr) {
         if (fbits_h(m.w) == PM_MATTE) kd = std::max({kd, (double)m.x, (double)m.y, (double)m.z});
     c->emit_max = std::max(em, 1e-30);
     c->kd_max = kd;
+    bool nn = true;
+    for (const LightDev &L : c->lights) nn = nn && L.le.x >= 0.f && L.le.y >= 0.f && L.le.z >= 0.f && L.n_area.w >= 0.f;
+    for (const float4 &m : c->materials)
+        if (fbits_h(m.w) == PM_MATTE) nn = nn && m.x >= 0.f && m.y >= 0.f && m.z >= 0.f;
+    c->scene_nonneg = nn;
     c->committed = true;
     return PM_OK;
 }
@@ -909,6 +922,7 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
     timer_end(c, "trace", s);
     if (fuse) { c->fused.valid = true; c->fused.n = end_slot; c->fused.grid = T.grid; c->count_zero_words = 0; }
     c->slots_used = std::max(c->slots_used, end_slot);
+    c->slots_nonneg = true; /* traced photons carry the scene's signs (scene_nonneg) */
     return PM_OK;
 }
 
@@ -1246,6 +1260,10 @@ int pm_upload_slots(void *ptr, const pm_photon *in, int64_t n) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(c->d_slots.p, in, n * sizeof(pm_photon), hipMemcpyHostToDevice));
     c->slots_used = n;
+    c->slots_nonneg = true;
+    for (int64_t i = 0; i < n && c->slots_nonneg; ++i)
+        if (in[i].bits & 1u) /* valid photon */
+            c->slots_nonneg = in[i].alpha[0] >= 0.f && in[i].alpha[1] >= 0.f && in[i].alpha[2] >= 0.f;
     return PM_OK;
 }
 

@@ -62,104 +62,358 @@ PMD void write_partial(const GatherParams &P, int64_t k, int M, Fx3 L) {
 /* Fixed-radius query over photon buckets. Every photon with
  * d^2 < r^2 is inside the visited cells because the cell range is taken
  * over [p - r', p + r'] with r' slightly larger than sqrt(r^2). */
+PMD void add_hit(Fx3 &Lf, v3 ns, v3 fv, float4 a, float4 b, float wz, float sc) {
+    const v3 wi = mk(a.w, b.w, wz);
+    const v3 c = fabsf(dot(ns, wi)) * fv * xyz(b); /* processPhoton, gathering.cu:17-23 */
+    Lf.x += to_fx(c.x, sc); Lf.y += to_fx(c.y, sc); Lf.z += to_fx(c.z, sc);
+}
+PMD bool in_radius(v3 p, float4 a, float r2) { /* gathering.cu:32-36 (DistanceSquared < maxDist2) */
+    const v3 diff = p - xyz(a);
+    return diff.x * diff.x + diff.y * diff.y + diff.z * diff.z < r2;
+}
+
+/* One lane scans its own cells [x0, x1] x [y0, y1] x [z0, z1] straight from
+ * global memory: the census launches (their photons-tested count is the
+ * per-record unit bench.py prices), lanes whose radius exceeds the grid's
+ * design radius (uploaded records), and tiles whose row union is too wide for
+ * k_gather_tile's LDS staging. Rows are read four photons at a time with all
+ * eight row bounds loaded first. */
+template <int COUNT>
+PMD void lane_scan(const GatherParams &P, v3 p, float r2, v3 ns, v3 fv, uint32_t x0, uint32_t x1, uint32_t y0,
+                   uint32_t y1, uint32_t z0, uint32_t z1, int &M, Fx3 &Lf, unsigned long long &vis,
+                   unsigned long long &rows) {
+    const GridDesc &g = P.grid;
+    const float sc = P.fx_scale;
+    const float *phb = reinterpret_cast<const float *>(P.ph_b);
+    auto photon = [&](const float4 a, uint32_t j) {
+        if (in_radius(p, a, r2)) {
+            M++;
+            add_hit(Lf, ns, fv, a, P.ph_b[2 * (size_t)j], phb[8 * (size_t)j + 4], sc);
+        }
+    };
+    auto range = [&](uint32_t j, const uint32_t e) {
+        for (; j + 4 <= e; j += 4) { /* 4 photon loads in flight */
+            const float4 a0 = P.ph_a[j], a1 = P.ph_a[j + 1], a2 = P.ph_a[j + 2], a3 = P.ph_a[j + 3];
+            photon(a0, j); photon(a1, j + 1); photon(a2, j + 2); photon(a3, j + 3);
+        }
+        for (; j < e; ++j) photon(P.ph_a[j], j);
+    };
+    if (y1 <= y0 + 1 && z1 <= z0 + 1) {
+        /* all row bounds first: 8 independent loads in flight */
+        uint32_t rb[4], re[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t cy = y0 + (k & 1), cz = z0 + (k >> 1);
+            const bool use = cy <= y1 && cz <= z1;
+            const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+            rb[k] = use ? P.cell_start[row + x0] : 0u;
+            re[k] = use ? P.cell_start[row + x1 + 1] : 0u;
+            if (COUNT) { vis += re[k] - rb[k]; rows += use; }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) range(rb[k], re[k]);
+    } else { /* radius above the grid's design radius (uploaded records) */
+        for (uint32_t cz = z0; cz <= z1; ++cz)
+            for (uint32_t cy = y0; cy <= y1; ++cy) {
+                const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+                const uint32_t b = P.cell_start[row + x0], e = P.cell_start[row + x1 + 1];
+                if (COUNT) { vis += e - b; rows++; }
+                range(b, e);
+            }
+    }
+}
+
+/* record prologue shared by the bucket kernels: flags, PPM state, BSDF, cell
+ * box of [p - r', p + r'] (small: at most 2 x 2 rows, the grid's design case) */
+struct GatherRec {
+    bool live = false, small = false, big = false;
+    float4 st = make_float4(0.f, 0.f, 0.f, 0.f);
+    v3 p = mk(0.f, 0.f, 0.f), ns = mk(0.f, 0.f, 0.f), fv = mk(0.f, 0.f, 0.f);
+    float r2 = 0.f;
+    uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0, z0 = 0, z1 = 0;
+    template <int PARTIAL>
+    PMD void load(const GatherParams &P, int64_t r) {
+        if (r >= P.rec_end) return;
+        const float4 pos = P.R.pos[r];
+        const uint32_t flags = (uint32_t)__float_as_int(pos.w);
+        if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) {
+            if (PARTIAL) write_partial(P, partial_index(P, r), 0, Fx3{0, 0, 0});
+            return;
+        }
+        live = true;
+        st = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : P.R.state[r];
+        const float4 nrm = P.R.nrm[r];
+        r2 = st.w;
+        const float4 m = P.materials[__float_as_int(nrm.w)];
+        fv = __float_as_int(m.w) == PM_MATTE ? xyz(m) * INV_PI : mk(0.f, 0.f, 0.f);
+        p = xyz(pos); ns = xyz(nrm);
+        if (r2 > 0.f) {
+            const GridDesc &g = P.grid;
+            const float rq = sqrtf(r2) * 1.0001f + 1e-4f;
+            /* cells overlapping [p - r', p + r']: cell edge >= 2 r_max, so at
+             * most 2 per axis -> at most 4 (y, z) rows of <= 2 cells in x */
+            x0 = cell_axis(p.x - rq, g.gx, g.inv_cs, g.dx); x1 = cell_axis(p.x + rq, g.gx, g.inv_cs, g.dx);
+            y0 = cell_axis(p.y - rq, g.gy, g.inv_cs, g.dy); y1 = cell_axis(p.y + rq, g.gy, g.inv_cs, g.dy);
+            z0 = cell_axis(p.z - rq, g.gz, g.inv_cs, g.dz); z1 = cell_axis(p.z + rq, g.gz, g.inv_cs, g.dz);
+            small = y1 <= y0 + 1 && z1 <= z0 + 1;
+            big = !small;
+        }
+    }
+    /* fused PPM update (gathering.cu:104-126) or the partial of the exchange */
+    template <int PARTIAL>
+    PMD void store(const GatherParams &P, int64_t r, int M, Fx3 Lf) {
+        if (!live) return;
+        if (PARTIAL) {
+            write_partial(P, partial_index(P, r), M, Lf);
+        } else {
+            const double inv = P.fx_inv;
+            v3 L = mk((float)((double)Lf.x * inv), (float)((double)Lf.y * inv), (float)((double)Lf.z * inv));
+            float N = P.fresh ? 0.f : P.R.n[r];
+            ppm_apply(st, N, M, L, P.ppm_alpha);
+            if (M > 0 || P.fresh) { P.R.state[r] = st; P.R.n[r] = N; }
+        }
+    }
+};
+
+/* Per-lane bucket gather: one lane per record, its own rows from global
+ * memory. Census launches (COUNT) and the PM_GATHER_KERNEL=lane experiment. */
 template <int PARTIAL, int COUNT>
 __global__ __launch_bounds__(GATHER_BLOCK, 8) void k_gather_grid(GatherParams P) { /* 8 waves/SIMD: latency bound */
     const int64_t r = P.rec_begin + (int64_t)blockIdx.x * GATHER_BLOCK + threadIdx.x;
     unsigned long long vis = 0, hits = 0, rows = 0, act = 0;
-    if (r < P.rec_end) {
-        float4 pos = P.R.pos[r];
-        uint32_t flags = (uint32_t)__float_as_int(pos.w);
-        if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) {
-            if (PARTIAL) write_partial(P, partial_index(P, r), 0, Fx3{0, 0, 0});
+    GatherRec R;
+    R.load<PARTIAL>(P, r);
+    int M = 0;
+    Fx3 Lf{0, 0, 0};
+    if (R.live && R.r2 > 0.f)
+        lane_scan<COUNT>(P, R.p, R.r2, R.ns, R.fv, R.x0, R.x1, R.y0, R.y1, R.z0, R.z1, M, Lf, vis, rows);
+    if (COUNT && R.live) { hits += (unsigned long long)M; act++; }
+    R.store<PARTIAL>(P, r, M, Lf);
+    if (COUNT) count4(P.counters, vis, hits, rows, act);
+}
+
+/* ---------------------------------------------------------------------- */
+/* Tile gather (default): the 64 records of a wave are one 8x8 pixel tile, so
+ * their cell boxes overlap almost entirely. The wave takes the union box of
+ * its lanes' boxes (X0..X1 x Y0..Y1 x Z0..Z1 cells), and when it has at most
+ * 64 (y, z) rows:
+ *   1. lane u loads the bounds of union row u (cells X0..X1: one contiguous
+ *      run of photons), a wave prefix sum concatenates the rows -> U photons;
+ *   2. the concatenation is staged into this wave's LDS window, TILE_CAP
+ *      photons at a time, with coalesced loads (positions lane and lane + 64:
+ *      1 KiB per load instruction): ph_a (p, wi.x) and the flux half of ph_b
+ *      (alpha, wi.y | wi.z); the row of each position comes from a wave
+ *      max-scan over the row-start markers;
+ *   3. every lane tests the whole union-x run of each of its <= 4 rows from
+ *      LDS (lanes sharing a row read the same address: broadcast), its rows
+ *      walked as one flattened sequence, two photons per step.
+ * A lane tests a superset of its own cells (the union's x-range); every
+ * photon with d^2 < r^2 still lies in exactly one visited run, and the sums
+ * are exact fixed point, so M and L are bit-identical to k_gather_grid's.
+ * Global memory sees one record read, one row-bounds load per union row and
+ * ~3 coalesced loads per 64 photons per tile, instead of ~2 scattered loads
+ * per photon per lane. Lanes with an oversized radius and
+ * tiles with more than 64 union rows fall back to lane_scan. */
+constexpr int TILE_CAP = 128; /* photons per LDS window (two per lane) */
+struct TileLds {
+    float4 a[TILE_CAP]; /* p.xyz, wi.x */
+    float4 b[TILE_CAP]; /* alpha.rgb, wi.y */
+    float c[TILE_CAP];  /* wi.z */
+    int mark[TILE_CAP]; /* union row starting at this position, -1 = none */
+};
+/* LDS traffic between lanes of one wave: ds_* of a wave execute in order, so
+ * a compiler-level ordering point is all the exchange needs */
+PMD void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+/* inclusive wave scans on DPP (row_shr 1/2/4/8 inside rows of 16 lanes,
+ * then row_bcast 15/31 into rows 1,3 / 2,3): VALU-rate cross-lane moves
+ * instead of an LDS round trip per step (__shfl = ds_bpermute). A lane
+ * whose DPP source is out of its row, or whose row the mask leaves out,
+ * receives `id`, the operation's identity, so no lane guards are needed.
+ * Every lane must be active. */
+template <class Op>
+PMD int wave_scan_dpp(int v, int id, Op op) {
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x111, 0xf, 0xf, false)); /* row_shr:1 */
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x112, 0xf, 0xf, false)); /* row_shr:2 */
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x114, 0xf, 0xf, false)); /* row_shr:4 */
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x118, 0xf, 0xf, false)); /* row_shr:8 */
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x142, 0xa, 0xf, false)); /* row_bcast:15 -> rows 1, 3 */
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x143, 0xc, 0xf, false)); /* row_bcast:31 -> rows 2, 3 */
+    return v;
+}
+PMD uint32_t wave_incl_sum_u32(uint32_t v) {
+    return (uint32_t)wave_scan_dpp((int)v, 0, [](int a, int b) { return (int)((uint32_t)a + (uint32_t)b); });
+}
+PMD int wave_incl_max_i32(int v) { return wave_scan_dpp(v, -1, [](int a, int b) { return max(a, b); }); }
+/* wave-uniform min / max (the scan's last lane) */
+PMD uint32_t wave_min_u32(uint32_t v) {
+    const int m = wave_scan_dpp((int)v, -1, [](int a, int b) { return (int)min((uint32_t)a, (uint32_t)b); });
+    return (uint32_t)__builtin_amdgcn_readlane(m, 63);
+}
+PMD uint32_t wave_max_u32(uint32_t v) {
+    const int m = wave_scan_dpp((int)v, 0, [](int a, int b) { return (int)max((uint32_t)a, (uint32_t)b); });
+    return (uint32_t)__builtin_amdgcn_readlane(m, 63);
+}
+/* two 16-bit minima at once (v_pk_min_u16) */
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+PMD uint32_t wave_min_2x16(uint32_t v) {
+    const int m = wave_scan_dpp((int)v, -1, [](int a, int b) {
+        return (int)__builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
+                                                                          __builtin_bit_cast(u16x2, b)));
+    });
+    return (uint32_t)__builtin_amdgcn_readlane(m, 63);
+}
+PMD uint32_t uniform_u32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+/* blockIdx -> block of tiles. Blocks are dispatched round-robin over the 8
+ * XCDs; with xcd set, XCD x processes one contiguous range of tiles, so the
+ * photon rows neighbouring tiles share stay in that XCD's own L2 */
+PMD int64_t gather_block(const GatherParams &P) {
+    const uint32_t b = blockIdx.x;
+    if (!P.xcd) return b;
+    const uint32_t nb = gridDim.x, q = nb / 8u, rm = nb % 8u, x = b % 8u, i = b / 8u;
+    return (int64_t)((x < rm ? x * (q + 1u) : rm * (q + 1u) + (x - rm) * q) + i);
+}
+
+template <int PARTIAL, int NN>
+__global__ __launch_bounds__(GATHER_BLOCK) void k_gather_tile(GatherParams P) {
+    __shared__ TileLds tiles[GATHER_BLOCK / 64];
+    TileLds &T = tiles[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63;
+    const int64_t r = P.rec_begin + gather_block(P) * GATHER_BLOCK + threadIdx.x;
+    const GridDesc &g = P.grid;
+    GatherRec R;
+    R.load<PARTIAL>(P, r);
+    int M = 0;
+    Fx3 Lf{0, 0, 0};
+    const float sc = P.fx_scale;
+    unsigned long long nv = 0, nr = 0; /* lane_scan census (unused) */
+    /* NN (no negative contribution possible, GatherParams::fx_nonneg): the
+     * integer-valued contributions rint(c * 2^S) are summed in double — exact
+     * while the sum stays below 2^53 (checked at the end; partial sums of
+     * non-negative terms never exceed it), and 4 instructions per channel
+     * instead of a float -> int64 conversion and a 64-bit add */
+    double dx = 0.0, dy = 0.0, dz = 0.0;
+    bool direct = R.big;               /* lanes that scan their own cells from global memory */
+    if (__ballot(R.small) != 0ull) {
+        uint32_t X0, X1, Y0, Y1, Z0, Z1;
+        if (g.dx < 65536 && g.dy < 65536 && g.dz < 65536) {
+            /* three packed 16-bit minima (maxima as minima of 0xffff - c) */
+            const uint32_t m0 = wave_min_2x16(R.small ? (R.x0 << 16) | R.y0 : 0xffffffffu);
+            const uint32_t m1 = wave_min_2x16(R.small ? ((0xffffu - R.x1) << 16) | (0xffffu - R.y1) : 0xffffffffu);
+            const uint32_t m2 = wave_min_2x16(R.small ? (R.z0 << 16) | (0xffffu - R.z1) : 0xffffffffu);
+            X0 = m0 >> 16; Y0 = m0 & 0xffffu; X1 = 0xffffu - (m1 >> 16); Y1 = 0xffffu - (m1 & 0xffffu);
+            Z0 = m2 >> 16; Z1 = 0xffffu - (m2 & 0xffffu);
         } else {
-            float4 st = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : P.R.state[r];
-            float4 nrm = P.R.nrm[r];
-            const float r2 = st.w;
-            float4 m = P.materials[__float_as_int(nrm.w)];
-            v3 fv = __float_as_int(m.w) == PM_MATTE ? xyz(m) * INV_PI : mk(0.f, 0.f, 0.f);
-            const v3 p = xyz(pos), ns = xyz(nrm);
-            int M = 0;
-            Fx3 Lf{0, 0, 0};
-            const float sc = P.fx_scale;
-            if (r2 > 0.f) {
-                const GridDesc &g = P.grid;
-                const float rq = sqrtf(r2) * 1.0001f + 1e-4f;
-                /* cells overlapping [p - r', p + r']: cell edge >= 2 r_max, so at
-                 * most 2 per axis -> at most 4 (y, z) rows of <= 2 cells in x */
-                uint32_t x0 = cell_axis(p.x - rq, g.gx, g.inv_cs, g.dx), x1 = cell_axis(p.x + rq, g.gx, g.inv_cs, g.dx);
-                uint32_t y0 = cell_axis(p.y - rq, g.gy, g.inv_cs, g.dy), y1 = cell_axis(p.y + rq, g.gy, g.inv_cs, g.dy);
-                uint32_t z0 = cell_axis(p.z - rq, g.gz, g.inv_cs, g.dz), z1 = cell_axis(p.z + rq, g.gz, g.inv_cs, g.dz);
-                auto photon = [&](const float4 a, uint32_t j) {
-                    v3 diff = p - xyz(a);
-                    float dist2 = diff.x * diff.x + diff.y * diff.y + diff.z * diff.z;
-                    if (dist2 < r2) {
-                        M++;
-                        const float4 bb = P.ph_b[2 * (size_t)j];
-                        const float wz = reinterpret_cast<const float *>(P.ph_b)[8 * (size_t)j + 4];
-                        v3 wi = mk(a.w, bb.w, wz);
-                        v3 c = fabsf(dot(ns, wi)) * fv * xyz(bb); /* processPhoton, gathering.cu:17-23 */
-                        Lf.x += to_fx(c.x, sc); Lf.y += to_fx(c.y, sc); Lf.z += to_fx(c.z, sc);
-                    }
-                };
-                auto range = [&](uint32_t j, const uint32_t e) {
-                    for (; j + 4 <= e; j += 4) { /* 4 photon loads in flight */
-                        const float4 a0 = P.ph_a[j], a1 = P.ph_a[j + 1], a2 = P.ph_a[j + 2], a3 = P.ph_a[j + 3];
-                        photon(a0, j); photon(a1, j + 1); photon(a2, j + 2); photon(a3, j + 3);
-                    }
-                    for (; j < e; ++j) photon(P.ph_a[j], j);
-                };
-                if (y1 <= y0 + 1 && z1 <= z0 + 1) {
-                    /* all row bounds first: 8 independent loads in flight */
-                    uint32_t rb[4], re[4];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const uint32_t cy = y0 + (k & 1), cz = z0 + (k >> 1);
-                        const bool use = cy <= y1 && cz <= z1;
-                        const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
-                        rb[k] = use ? P.cell_start[row + x0] : 0u;
-                        re[k] = use ? P.cell_start[row + x1 + 1] : 0u;
-                        if (COUNT) { vis += re[k] - rb[k]; rows += use; }
-                    }
-                    /* The lane's four rows as ONE sequence v = 0 .. tot-1 (photon
-                     * v lives at v + off(row of v)), four photons per step: the
-                     * wave steps max_lane(tot) / 4 times instead of summing each
-                     * row's lane maximum (C2 lane utilisation of the photon loads
-                     * 0.51 -> ~0.7, simulated on the oracle's photons). Sums are
-                     * fixed point: the visiting order changes no bit. */
-                    const uint32_t c1 = re[0] - rb[0], c2 = c1 + (re[1] - rb[1]), c3 = c2 + (re[2] - rb[2]);
-                    const uint32_t tot = c3 + (re[3] - rb[3]);
-                    const uint32_t o0 = rb[0], o1 = rb[1] - c1, o2 = rb[2] - c2, o3 = rb[3] - c3;
-                    auto at = [&](uint32_t v) { return v + (v < c1 ? o0 : v < c2 ? o1 : v < c3 ? o2 : o3); };
-                    uint32_t v = 0;
-                    for (; v + 2 <= tot; v += 2) {
-                        const uint32_t j0 = at(v), j1 = at(v + 1);
-                        const float4 a0 = P.ph_a[j0], a1 = P.ph_a[j1];
-                        photon(a0, j0); photon(a1, j1);
-                    }
-                    for (; v < tot; ++v) { const uint32_t j = at(v); photon(P.ph_a[j], j); }
-                } else { /* radius above the grid's design radius (uploaded records) */
-                    for (uint32_t cz = z0; cz <= z1; ++cz)
-                        for (uint32_t cy = y0; cy <= y1; ++cy) {
-                            const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
-                            const uint32_t b = P.cell_start[row + x0], e = P.cell_start[row + x1 + 1];
-                            if (COUNT) { vis += e - b; rows++; }
-                            range(b, e);
-                        }
+            X0 = wave_min_u32(R.small ? R.x0 : 0xffffffffu); X1 = wave_max_u32(R.small ? R.x1 : 0u);
+            Y0 = wave_min_u32(R.small ? R.y0 : 0xffffffffu); Y1 = wave_max_u32(R.small ? R.y1 : 0u);
+            Z0 = wave_min_u32(R.small ? R.z0 : 0xffffffffu); Z1 = wave_max_u32(R.small ? R.z1 : 0u);
+        }
+        const uint32_t NY = Y1 - Y0 + 1u, NZ = Z1 - Z0 + 1u;
+        if ((uint64_t)NY * NZ <= 64u) {
+            const uint32_t nu = NY * NZ;
+            /* 1. union row u = lane: photons [B, B + len) */
+            uint32_t B = 0u, len = 0u;
+            if ((uint32_t)lane < nu) {
+                const uint32_t cy = Y0 + (uint32_t)lane % NY, cz = Z0 + (uint32_t)lane / NY;
+                const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+                B = P.cell_start[row + X0];
+                len = P.cell_start[row + X1 + 1u] - B;
+            }
+            const uint32_t incl = wave_incl_sum_u32(len), pre = incl - len;
+            const uint32_t U = uniform_u32(__builtin_amdgcn_readlane(incl, 63));
+            const uint32_t gofs = B - pre; /* photon index of concatenated position t in row u: t + gofs_u */
+            /* this lane's rows as two runs of the concatenation: rows (y0, z)
+             * and (y0 + 1, z) are neighbours in the union, so each z-layer of
+             * the lane's box is one contiguous run [sA, eA) / [sB, eB) */
+            const uint32_t ny = R.small ? R.y1 - R.y0 + 1u : 1u;
+            const int uA = R.small ? (int)((R.z0 - Z0) * NY + (R.y0 - Y0)) : 0;
+            const int uB = R.small && R.z1 > R.z0 ? uA + (int)NY : uA;
+            /* every lane shuffles: a bpermute from a lane that is inactive at
+             * the shuffle reads 0 */
+            const uint32_t sA = (uint32_t)__shfl((int)pre, uA), eA = (uint32_t)__shfl((int)incl, uA + (int)ny - 1);
+            const uint32_t sB = (uint32_t)__shfl((int)pre, uB), eB0 = (uint32_t)__shfl((int)incl, uB + (int)ny - 1);
+            const uint32_t eB = R.small && R.z1 > R.z0 ? eB0 : sB;
+            for (uint32_t T0 = 0; T0 < U; T0 += TILE_CAP) {
+                const uint32_t n = min((uint32_t)TILE_CAP, U - T0);
+                /* 2. stage positions T0 + lane and T0 + 64 + lane */
+                T.mark[lane] = -1;
+                T.mark[lane + 64] = -1;
+                wave_lds_sync();
+                if (len > 0u) {
+                    if (pre >= T0 && pre < T0 + TILE_CAP) T.mark[pre - T0] = lane;
+                    else if (pre < T0 && pre + len > T0) T.mark[0] = lane; /* row running into the window */
                 }
+                wave_lds_sync();
+                const int ua = wave_incl_max_i32(T.mark[lane]);
+                const int ub = max(wave_incl_max_i32(T.mark[lane + 64]), __builtin_amdgcn_readlane(ua, 63));
+                const uint32_t ga = T0 + (uint32_t)lane + (uint32_t)__shfl((int)gofs, ua);
+                const uint32_t gb = T0 + 64u + (uint32_t)lane + (uint32_t)__shfl((int)gofs, ub);
+                /* all six loads in flight, then the LDS writes; positions at or
+                 * beyond n re-read position 0's photon (n >= 1) and are never read */
+                const float *phb = reinterpret_cast<const float *>(P.ph_b);
+                const uint32_t g0 = (uint32_t)__builtin_amdgcn_readlane((int)ga, 0);
+                const uint32_t ja = (uint32_t)lane < n ? ga : g0, jb = (uint32_t)lane + 64u < n ? gb : g0;
+                const float4 pa = P.ph_a[ja], pb = P.ph_a[jb];
+                const float4 qa = P.ph_b[2 * (size_t)ja], qb = P.ph_b[2 * (size_t)jb];
+                const float ca = phb[8 * (size_t)ja + 4], cb = phb[8 * (size_t)jb + 4];
+                T.a[lane] = pa; T.a[lane + 64] = pb;
+                T.b[lane] = qa; T.b[lane + 64] = qb;
+                T.c[lane] = ca; T.c[lane + 64] = cb;
+                wave_lds_sync();
+                /* 3. this lane's runs within the window as one sequence v =
+                 * 0 .. tot-1 (LDS position v + (v < c0 ? a0 : a1)). Tested 32
+                 * positions at a time into a hit mask; the hits are then summed
+                 * with every lane busy (max over lanes of its hits per chunk
+                 * instead of one masked pass per photon any lane hits). */
+                const uint32_t loA = max(sA, T0), hiA = min(eA, T0 + n);
+                const uint32_t loB = max(sB, T0), hiB = min(eB, T0 + n);
+                const uint32_t c0 = R.small && hiA > loA ? hiA - loA : 0u;
+                const uint32_t tot = c0 + (R.small && hiB > loB ? hiB - loB : 0u);
+                const uint32_t a0 = loA - T0, a1 = loB - T0 - c0;
+                auto at = [&](uint32_t v) { return (v + (v < c0 ? a0 : a1)) & (TILE_CAP - 1); };
+                const uint32_t vmax = wave_max_u32(tot);
+                for (uint32_t vb = 0; vb < vmax; vb += 32) {
+                    const uint32_t cnt = min(32u, vmax - vb);
+                    uint32_t bits = 0u;
+#pragma unroll 4
+                    for (uint32_t j = 0; j < cnt; ++j) {
+                        const uint32_t v = vb + j;
+                        const float4 a = T.a[at(v)];
+                        if (v < tot && in_radius(R.p, a, R.r2)) bits |= 1u << j;
+                    }
+                    M += __builtin_popcount(bits);
+                    while (bits) {
+                        const uint32_t j = (uint32_t)__builtin_ctz(bits);
+                        bits &= bits - 1u;
+                        const uint32_t t = at(vb + j);
+                        if (NN) {
+                            const float4 pa = T.a[t], pb = T.b[t];
+                            const v3 c = fabsf(dot(R.ns, mk(pa.w, pb.w, T.c[t]))) * R.fv * xyz(pb); /* processPhoton */
+                            dx += (double)rintf(c.x * sc); dy += (double)rintf(c.y * sc); dz += (double)rintf(c.z * sc);
+                        } else {
+                            add_hit(Lf, R.ns, R.fv, T.a[t], T.b[t], T.c[t], sc);
+                        }
+                    }
+                }
+                wave_lds_sync(); /* the window is read before the next one overwrites it */
             }
-            if (COUNT) { hits += (unsigned long long)M; act++; }
-            if (PARTIAL) {
-                write_partial(P, partial_index(P, r), M, Lf);
-            } else {
-                const double inv = P.fx_inv;
-                v3 L = mk((float)((double)Lf.x * inv), (float)((double)Lf.y * inv), (float)((double)Lf.z * inv));
-                float N = P.fresh ? 0.f : P.R.n[r];
-                ppm_apply(st, N, M, L, P.ppm_alpha);
-                if (M > 0 || P.fresh) { P.R.state[r] = st; P.R.n[r] = N; }
-            }
+        } else {
+            direct = direct || R.small;
         }
     }
-    if (COUNT) count4(P.counters, vis, hits, rows, act);
+    if (NN) {
+        if (fmax(fmax(dx, dy), dz) < 0x1p53) {
+            Lf.x = (long long)dx; Lf.y = (long long)dy; Lf.z = (long long)dz;
+        } else if (R.small) { /* inexact (or NaN): this record again in int64 */
+            M = 0;
+            direct = true;
+        }
+    }
+    if (direct) lane_scan<0>(P, R.p, R.r2, R.ns, R.fv, R.x0, R.x1, R.y0, R.y1, R.z0, R.z1, M, Lf, nv, nr);
+    R.store<PARTIAL>(P, r, M, Lf);
 }
 
 /* Wave-cooperative bucket gather. A wave's 64 records are one 8x8 pixel
@@ -180,17 +434,6 @@ __global__ __launch_bounds__(GATHER_BLOCK, 8) void k_gather_grid(GatherParams P)
  * 139 us vs 69 us for k_gather_grid — every photon costs two dependent
  * scalar-load round trips for the whole wave, and every participant tests
  * the union of the tile's x-ranges. */
-PMD uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off));
-    return v;
-}
-PMD uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
-    return v;
-}
-
 template <int PARTIAL>
 __global__ __launch_bounds__(GATHER_BLOCK, 8) void k_gather_wave(GatherParams P) {
     const int64_t r = P.rec_begin + (int64_t)blockIdx.x * GATHER_BLOCK + threadIdx.x;
@@ -589,8 +832,12 @@ static void launch_g(const GatherParams &p, hipStream_t s) {
     unsigned grid = (unsigned)((p.rec_end - p.rec_begin + GATHER_BLOCK - 1) / GATHER_BLOCK);
     /* a counting launch always runs the per-lane kernel: its census (rows and
      * photons per RECORD) is the algorithm's unit count bench.py prices; the
-     * wave kernel finds exactly the same photons (bit-identical records) */
-    if (STRUCT == PM_GATHER_GRID && p.wave && !COUNT)
+     * tile and wave kernels find exactly the same photons (bit-identical records) */
+    if (STRUCT == PM_GATHER_GRID && !COUNT && p.kernel == PM_GK_TILE && p.fx_nonneg)
+        pm_launch((k_gather_tile<PARTIAL, 1>), dim3(grid), dim3(GATHER_BLOCK), 0, s, p);
+    else if (STRUCT == PM_GATHER_GRID && !COUNT && p.kernel == PM_GK_TILE)
+        pm_launch((k_gather_tile<PARTIAL, 0>), dim3(grid), dim3(GATHER_BLOCK), 0, s, p);
+    else if (STRUCT == PM_GATHER_GRID && !COUNT && p.kernel == PM_GK_WAVE)
         pm_launch((k_gather_wave<PARTIAL>), dim3(grid), dim3(GATHER_BLOCK), 0, s, p);
     else if (STRUCT == PM_GATHER_GRID)
         pm_launch((k_gather_grid<PARTIAL, COUNT>), dim3(grid), dim3(GATHER_BLOCK), 0, s, p);

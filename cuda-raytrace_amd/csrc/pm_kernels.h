@@ -35,6 +35,7 @@ constexpr int EYE_BLOCK = 128;     /* traversal kernels: LDS stack column per la
 constexpr int TRACE_BLOCK = 256;    /* k_trace: 4 waves compact paths together */
 constexpr int BVH_STACK = BVH_STACK_DEPTH; /* >= max BVH depth (builder enforces it) */
 constexpr int GATHER_BLOCK = 256;
+enum { PM_GK_TILE = 0, PM_GK_LANE = 1, PM_GK_WAVE = 2 };
 constexpr int KD_STACK = 32;       /* >= pbrt median kd-tree depth for < 2^31 photons */
 constexpr int KNN_BLOCK = 64;      /* k_gather_knn: one wave per block, LDS heaps [K][64] */
 
@@ -111,6 +112,9 @@ struct GatherParams {
     /* fixed-point flux: contribution c -> rint(c * fx_scale), fx_inv = 1/fx_scale (2^-S) */
     float fx_scale;
     double fx_inv;
+    /* every contribution is >= 0 (scene emission and albedos and the photon
+     * fluxes are non-negative): the tile kernel may sum in double (exact) */
+    int fx_nonneg;
     /* partial mode: per record int64 (M, L.x, L.y, L.z) in fixed point, or
      * (count != null) split: int32 M in count[k], three int64 in flux[3k..] */
     long long *partial;
@@ -124,8 +128,11 @@ struct GatherParams {
      * view_list[i] = record of view position i (update); null = all records */
     const uint32_t *view_rank;
     const uint32_t *view_list;
-    /* grid gather kernel: 1 = wave-cooperative (k_gather_wave, experiment), 0 = per lane (k_gather_grid, default) */
-    int wave;
+    /* grid gather kernel (PM_GK_*): tile (k_gather_tile, LDS-staged, default),
+     * lane (k_gather_grid, per lane from global memory), wave (k_gather_wave,
+     * scalar-cache experiment); census launches always run k_gather_grid */
+    int kernel;
+    int xcd; /* tile kernel: contiguous tile ranges per XCD (gather_block) */
     /* kNN estimator (k_gather_knn): knn_k nearest photons with d^2 < knn_r2;
      * per-record fixed-point scale = power of two below knn_fx * r_k^2;
      * slots = the slot buffer the buckets were built from (ph_b carries the

@@ -171,19 +171,27 @@ def test_grid_gather_parity(cornell, radius2):
 
 
 @pytest.mark.parametrize("radius2", [4.0, 25.0, 400.0])
-def test_wave_gather_equals_lane_gather(radius2, oracle_mod, hip_mod, monkeypatch):
-    """The wave-cooperative bucket gather (PM_GATHER_WAVE=1, experiment) and
-    the per-lane kernel (default) find the same photons: fused records and split
-    partials bit-identical. radius2 400 exceeds the grid's design radius for
-    uploaded records -> the wave kernel's per-lane fallback."""
+@pytest.mark.parametrize("W,H,paths", [(64, 48, 16384), (320, 180, 131072)])
+def test_bucket_gather_kernels_agree(radius2, W, H, paths, oracle_mod, hip_mod, monkeypatch):
+    """The bucket gather kernels find the same photons: the LDS-staged tile
+    kernel (default, with and without the per-XCD tile ranges), the
+    wave-cooperative scalar-cache experiment and the per-lane kernel give
+    bit-identical fused records and split partials. radius2 25 makes the
+    unions of a tile exceed one LDS window (several windows); 400 exceeds the
+    grid's design radius for uploaded records -> the per-lane fallbacks."""
     torch = pytest.importorskip("torch")
-    sc = scenes.cornell_box(64, 48)
+    sc = scenes.cornell_box(W, H)
     orc = sc.load_into(oracle_mod.Oracle())
-    p, recs, slots = _gather_inputs(orc, radius2=radius2)
+    p, recs, slots = _gather_inputs(orc, radius2=radius2, paths=paths)
     p.gather_structure = PM_GATHER_GRID
-    outs = []
-    for wave in ("1", "0"):
-        monkeypatch.setenv("PM_GATHER_WAVE", wave)
+    outs = {}
+    for name, env in (("lane", {"PM_GATHER_KERNEL": "lane"}), ("tile", {"PM_GATHER_KERNEL": "tile"}),
+                      ("tile_xcd", {"PM_GATHER_KERNEL": "tile", "PM_GATHER_XCD": "1"}),
+                      ("wave", {"PM_GATHER_KERNEL": "wave"})):
+        for k in ("PM_GATHER_KERNEL", "PM_GATHER_XCD"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         ctx = sc.load_into(hip_mod.Context(0))
         try:
             ctx.upload_records(recs)
@@ -194,12 +202,14 @@ def test_wave_gather_equals_lane_gather(radius2, oracle_mod, hip_mod, monkeypatc
             ctx.gather_partial(p, part.data_ptr())
             ctx.synchronize()
             ctx.gather(p)
-            outs.append((ctx.download_records(), part.cpu().numpy()))
+            outs[name] = (ctx.download_records(), part.cpu().numpy())
         finally:
             ctx.close()
-    assert (outs[0][1][:, 0] > 0).sum() > 100
-    assert np.array_equal(outs[0][1], outs[1][1])
-    assert_bitexact(outs[0][0], outs[1][0], "wave vs per-lane gather")
+    ref_rec, ref_part = outs["lane"]
+    assert (ref_part[:, 0] > 0).sum() > 100
+    for name in ("tile", "tile_xcd", "wave"):
+        assert np.array_equal(outs[name][1], ref_part), name
+        assert_bitexact(outs[name][0], ref_rec, f"{name} vs per-lane gather")
 
 
 def test_partial_plus_update_equals_fused(cornell):
