@@ -131,22 +131,26 @@ struct GatherRec {
     v3 p = mk(0.f, 0.f, 0.f), ns = mk(0.f, 0.f, 0.f), fv = mk(0.f, 0.f, 0.f);
     float r2 = 0.f;
     uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0, z0 = 0, z1 = 0;
+    float4 nrm = make_float4(0.f, 0.f, 0.f, 0.f);
+    /* phase 1: position, PPM state and cell box. The state is read with the
+     * position (speculatively, also for inactive records) so that the cell
+     * box waits for one round trip only; the normal is requested here and
+     * consumed by shade() */
     template <int PARTIAL>
     PMD void load(const GatherParams &P, int64_t r) {
         if (r >= P.rec_end) return;
         const float4 pos = P.R.pos[r];
+        const float4 st0 = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : P.R.state[r];
         const uint32_t flags = (uint32_t)__float_as_int(pos.w);
         if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) {
             if (PARTIAL) write_partial(P, partial_index(P, r), 0, Fx3{0, 0, 0});
             return;
         }
         live = true;
-        st = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : P.R.state[r];
-        const float4 nrm = P.R.nrm[r];
+        st = st0;
+        nrm = P.R.nrm[r];
         r2 = st.w;
-        const float4 m = P.materials[__float_as_int(nrm.w)];
-        fv = __float_as_int(m.w) == PM_MATTE ? xyz(m) * INV_PI : mk(0.f, 0.f, 0.f);
-        p = xyz(pos); ns = xyz(nrm);
+        p = xyz(pos);
         if (r2 > 0.f) {
             const GridDesc &g = P.grid;
             const float rq = sqrtf(r2) * 1.0001f + 1e-4f;
@@ -158,6 +162,13 @@ struct GatherRec {
             small = y1 <= y0 + 1 && z1 <= z0 + 1;
             big = !small;
         }
+    }
+    /* phase 2: shading normal and BSDF (Kd / pi for matte, processPhoton) */
+    PMD void shade(const GatherParams &P) {
+        if (!live) return;
+        const float4 m = P.materials[__float_as_int(nrm.w)];
+        fv = __float_as_int(m.w) == PM_MATTE ? xyz(m) * INV_PI : mk(0.f, 0.f, 0.f);
+        ns = xyz(nrm);
     }
     /* fused PPM update (gathering.cu:104-126) or the partial of the exchange */
     template <int PARTIAL>
@@ -183,6 +194,7 @@ __global__ __launch_bounds__(GATHER_BLOCK, 8) void k_gather_grid(GatherParams P)
     unsigned long long vis = 0, hits = 0, rows = 0, act = 0;
     GatherRec R;
     R.load<PARTIAL>(P, r);
+    R.shade(P);
     int M = 0;
     Fx3 Lf{0, 0, 0};
     if (R.live && R.r2 > 0.f)
@@ -214,10 +226,17 @@ __global__ __launch_bounds__(GATHER_BLOCK, 8) void k_gather_grid(GatherParams P)
  * ~3 coalesced loads per 64 photons per tile, instead of ~2 scattered loads
  * per photon per lane. Lanes with an oversized radius and
  * tiles with more than 64 union rows fall back to lane_scan. */
-constexpr int TILE_CAP = 128; /* photons per LDS window (two per lane) */
+#ifndef PM_TILE_CAP
+#define PM_TILE_CAP 128
+#endif
+constexpr int TILE_CAP = PM_TILE_CAP; /* photons per LDS window (two per lane) */
 struct TileLds {
-    float4 a[TILE_CAP]; /* p.xyz, wi.x */
+    /* positions SoA, so that a pair of neighbouring photons is one ds_read2;
+     * 2 x TILE_CAP entries: the test loop reads up to TILE_CAP past a run's
+     * start (lanes beyond their run) without wrapping the index */
+    float x[2 * TILE_CAP], y[2 * TILE_CAP], z[2 * TILE_CAP];
     float4 b[TILE_CAP]; /* alpha.rgb, wi.y */
+    float w[TILE_CAP];  /* wi.x */
     float c[TILE_CAP];  /* wi.z */
     int mark[TILE_CAP]; /* union row starting at this position, -1 = none */
 };
@@ -277,8 +296,25 @@ PMD int64_t gather_block(const GatherParams &P) {
     return (int64_t)((x < rm ? x * (q + 1u) : rm * (q + 1u) + (x - rm) * q) + i);
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+/* PM_TILE_STATS builds (make variant VFLAGS=-DPM_TILE_STATS): per-wave event
+ * counts of k_gather_tile into counters[8..15] (read with pm_trace_profile):
+ * tile waves, windows, test pairs, hit iterations, direct lanes, chunks,
+ * wide (> 64 rows) waves, staged photons */
+#ifdef PM_TILE_STATS
+#define TILE_STAT(k, v) do { const unsigned long long tv_ = (unsigned long long)(v); \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&P.counters[8 + (k)], tv_); } while (0)
+#else
+#define TILE_STAT(k, v) do { } while (0)
+#endif
+
+#ifdef PM_TILE_WAVES
+#define TILE_OCC __attribute__((amdgpu_waves_per_eu(PM_TILE_WAVES, PM_TILE_WAVES)))
+#else
+#define TILE_OCC
+#endif
 template <int PARTIAL, int NN>
-__global__ __launch_bounds__(GATHER_BLOCK) void k_gather_tile(GatherParams P) {
+__global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherParams P) {
     __shared__ TileLds tiles[GATHER_BLOCK / 64];
     TileLds &T = tiles[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
@@ -296,7 +332,8 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_tile(GatherParams P) {
      * non-negative terms never exceed it), and 4 instructions per channel
      * instead of a float -> int64 conversion and a 64-bit add */
     double dx = 0.0, dy = 0.0, dz = 0.0;
-    bool direct = R.big;               /* lanes that scan their own cells from global memory */
+    bool direct = R.big; /* lanes that scan their own cells from global memory */
+    bool shaded = false;
     if (__ballot(R.small) != 0ull) {
         uint32_t X0, X1, Y0, Y1, Z0, Z1;
         if (g.dx < 65536 && g.dy < 65536 && g.dz < 65536) {
@@ -314,6 +351,7 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_tile(GatherParams P) {
         const uint32_t NY = Y1 - Y0 + 1u, NZ = Z1 - Z0 + 1u;
         if ((uint64_t)NY * NZ <= 64u) {
             const uint32_t nu = NY * NZ;
+            TILE_STAT(0, 1);
             /* 1. union row u = lane: photons [B, B + len) */
             uint32_t B = 0u, len = 0u;
             if ((uint32_t)lane < nu) {
@@ -322,6 +360,9 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_tile(GatherParams P) {
                 B = P.cell_start[row + X0];
                 len = P.cell_start[row + X1 + 1u] - B;
             }
+            R.shade(P); /* its material load overlaps the row bounds and the staging */
+            shaded = true;
+            const v3 fvs = R.fv * sc;
             const uint32_t incl = wave_incl_sum_u32(len), pre = incl - len;
             const uint32_t U = uniform_u32(__builtin_amdgcn_readlane(incl, 63));
             const uint32_t gofs = B - pre; /* photon index of concatenated position t in row u: t + gofs_u */
@@ -333,68 +374,104 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_tile(GatherParams P) {
             const int uB = R.small && R.z1 > R.z0 ? uA + (int)NY : uA;
             /* every lane shuffles: a bpermute from a lane that is inactive at
              * the shuffle reads 0 */
-            const uint32_t sA = (uint32_t)__shfl((int)pre, uA), eA = (uint32_t)__shfl((int)incl, uA + (int)ny - 1);
+            const uint32_t sA = (uint32_t)__shfl((int)pre, uA), eA0 = (uint32_t)__shfl((int)incl, uA + (int)ny - 1);
             const uint32_t sB = (uint32_t)__shfl((int)pre, uB), eB0 = (uint32_t)__shfl((int)incl, uB + (int)ny - 1);
+            const uint32_t eA = R.small ? eA0 : sA;
             const uint32_t eB = R.small && R.z1 > R.z0 ? eB0 : sB;
+            const f2 px2 = {R.p.x, R.p.x}, py2 = {R.p.y, R.p.y}, pz2 = {R.p.z, R.p.z};
             for (uint32_t T0 = 0; T0 < U; T0 += TILE_CAP) {
                 const uint32_t n = min((uint32_t)TILE_CAP, U - T0);
-                /* 2. stage positions T0 + lane and T0 + 64 + lane */
-                T.mark[lane] = -1;
-                T.mark[lane + 64] = -1;
+                TILE_STAT(1, 1);
+                TILE_STAT(7, n);
+                /* 2. stage positions T0 + lane (and T0 + 64 + lane) */
+                constexpr int H = TILE_CAP / 64;
+                static_assert(H == 1 || H == 2, "TILE_CAP is 64 or 128");
+#pragma unroll
+                for (int h = 0; h < H; ++h) T.mark[lane + 64 * h] = -1;
                 wave_lds_sync();
                 if (len > 0u) {
                     if (pre >= T0 && pre < T0 + TILE_CAP) T.mark[pre - T0] = lane;
                     else if (pre < T0 && pre + len > T0) T.mark[0] = lane; /* row running into the window */
                 }
                 wave_lds_sync();
-                const int ua = wave_incl_max_i32(T.mark[lane]);
-                const int ub = max(wave_incl_max_i32(T.mark[lane + 64]), __builtin_amdgcn_readlane(ua, 63));
-                const uint32_t ga = T0 + (uint32_t)lane + (uint32_t)__shfl((int)gofs, ua);
-                const uint32_t gb = T0 + 64u + (uint32_t)lane + (uint32_t)__shfl((int)gofs, ub);
-                /* all six loads in flight, then the LDS writes; positions at or
+                int u[H];
+                u[0] = wave_incl_max_i32(T.mark[lane]);
+                if (H == 2) u[H - 1] = max(wave_incl_max_i32(T.mark[lane + 64 * (H - 1)]), __builtin_amdgcn_readlane(u[0], 63));
+                uint32_t gi[H];
+#pragma unroll
+                for (int h = 0; h < H; ++h) gi[h] = T0 + 64u * h + (uint32_t)lane + (uint32_t)__shfl((int)gofs, u[h]);
+                /* every load in flight, then the LDS writes; positions at or
                  * beyond n re-read position 0's photon (n >= 1) and are never read */
                 const float *phb = reinterpret_cast<const float *>(P.ph_b);
-                const uint32_t g0 = (uint32_t)__builtin_amdgcn_readlane((int)ga, 0);
-                const uint32_t ja = (uint32_t)lane < n ? ga : g0, jb = (uint32_t)lane + 64u < n ? gb : g0;
-                const float4 pa = P.ph_a[ja], pb = P.ph_a[jb];
-                const float4 qa = P.ph_b[2 * (size_t)ja], qb = P.ph_b[2 * (size_t)jb];
-                const float ca = phb[8 * (size_t)ja + 4], cb = phb[8 * (size_t)jb + 4];
-                T.a[lane] = pa; T.a[lane + 64] = pb;
-                T.b[lane] = qa; T.b[lane + 64] = qb;
-                T.c[lane] = ca; T.c[lane + 64] = cb;
+                const uint32_t g0 = (uint32_t)__builtin_amdgcn_readlane((int)gi[0], 0);
+                float4 pa[H], qa[H];
+                float ca[H];
+#pragma unroll
+                for (int h = 0; h < H; ++h) {
+                    const uint32_t j = (uint32_t)lane + 64u * h < n ? gi[h] : g0;
+                    pa[h] = P.ph_a[j]; qa[h] = P.ph_b[2 * (size_t)j]; ca[h] = phb[8 * (size_t)j + 4];
+                }
+#pragma unroll
+                for (int h = 0; h < H; ++h) {
+                    const int q = lane + 64 * h;
+                    T.x[q] = pa[h].x; T.y[q] = pa[h].y; T.z[q] = pa[h].z; T.w[q] = pa[h].w;
+                    T.b[q] = qa[h]; T.c[q] = ca[h];
+                }
                 wave_lds_sync();
-                /* 3. this lane's runs within the window as one sequence v =
-                 * 0 .. tot-1 (LDS position v + (v < c0 ? a0 : a1)). Tested 32
-                 * positions at a time into a hit mask; the hits are then summed
-                 * with every lane busy (max over lanes of its hits per chunk
-                 * instead of one masked pass per photon any lane hits). */
-                const uint32_t loA = max(sA, T0), hiA = min(eA, T0 + n);
-                const uint32_t loB = max(sB, T0), hiB = min(eB, T0 + n);
-                const uint32_t c0 = R.small && hiA > loA ? hiA - loA : 0u;
-                const uint32_t tot = c0 + (R.small && hiB > loB ? hiB - loB : 0u);
-                const uint32_t a0 = loA - T0, a1 = loB - T0 - c0;
-                auto at = [&](uint32_t v) { return (v + (v < c0 ? a0 : a1)) & (TILE_CAP - 1); };
-                const uint32_t vmax = wave_max_u32(tot);
-                for (uint32_t vb = 0; vb < vmax; vb += 32) {
-                    const uint32_t cnt = min(32u, vmax - vb);
+                /* 3. each run of this lane within the window: positions [lo,
+                 * lo + cnt) of the LDS window. Tested two photons per packed
+                 * instruction, 32 positions at a time, into a hit mask; the hits
+                 * are then summed with every lane busy (max over lanes of its
+                 * hits per chunk, instead of one masked pass per photon that
+                 * any lane hits). */
+                const uint32_t loA = max(sA, T0), hiA = min(eA, T0 + n), mA = hiA > loA ? hiA - loA : 0u;
+                const uint32_t loB = max(sB, T0), hiB = min(eB, T0 + n), mB = hiB > loB ? hiB - loB : 0u;
+                const uint32_t baseA = mA ? loA - T0 : 0u, baseB = mB ? loB - T0 : 0u; /* < TILE_CAP */
+                const uint32_t vmaxA = wave_max_u32(mA), vmaxB = wave_max_u32(mB);
+                /* hit mask of positions [v0, v0 + 32) of a run starting at LDS
+                 * position base (cnt of them tested, wave-uniform) */
+                auto test32 = [&](uint32_t base, uint32_t v0, uint32_t cnt, uint32_t m) {
+                    const float *xs = T.x + base + v0, *ys = T.y + base + v0, *zs = T.z + base + v0;
                     uint32_t bits = 0u;
 #pragma unroll 4
-                    for (uint32_t j = 0; j < cnt; ++j) {
-                        const uint32_t v = vb + j;
-                        const float4 a = T.a[at(v)];
-                        if (v < tot && in_radius(R.p, a, R.r2)) bits |= 1u << j;
+                    for (uint32_t j = 0; j < cnt; j += 2) {
+                        /* in_radius for both photons: ((dx^2 + dy^2) + dz^2) < r^2 */
+                        const f2 ddx = px2 - f2{xs[j], xs[j + 1]}, ddy = py2 - f2{ys[j], ys[j + 1]},
+                                 ddz = pz2 - f2{zs[j], zs[j + 1]};
+                        const f2 d2 = (ddx * ddx + ddy * ddy) + ddz * ddz;
+                        if (d2.x < R.r2) bits |= 1u << j;
+                        if (d2.y < R.r2) bits |= 2u << j;
                     }
-                    M += __builtin_popcount(bits);
-                    while (bits) {
-                        const uint32_t j = (uint32_t)__builtin_ctz(bits);
-                        bits &= bits - 1u;
-                        const uint32_t t = at(vb + j);
+                    /* positions at or beyond m belong to the next run / window */
+                    const uint32_t left = m > v0 ? m - v0 : 0u;
+                    return bits & (left >= 32u ? 0xffffffffu : (1u << left) - 1u);
+                };
+                const uint32_t vmax = max(vmaxA, vmaxB);
+                for (uint32_t vb = 0; vb < vmax; vb += 32) {
+                    TILE_STAT(5, 1);
+                    TILE_STAT(2, (min(32u, vmaxA > vb ? vmaxA - vb : 0u) + 1) / 2 + (min(32u, vmaxB > vb ? vmaxB - vb : 0u) + 1) / 2);
+                    uint32_t bA = vmaxA > vb ? test32(baseA, vb, min(32u, vmaxA - vb), mA) : 0u;
+                    uint32_t bB = vmaxB > vb ? test32(baseB, vb, min(32u, vmaxB - vb), mB) : 0u;
+                    M += __builtin_popcount(bA) + __builtin_popcount(bB);
+                    TILE_STAT(3, wave_max_u32(__builtin_popcount(bA) + __builtin_popcount(bB)));
+                    /* both runs' hits in one loop: max over lanes of the sum,
+                     * not the sum of the two maxima */
+                    while (bA | bB) {
+                        const bool fromA = bA != 0u;
+                        const uint32_t bits = fromA ? bA : bB;
+                        const uint32_t t = (fromA ? baseA : baseB) + vb + (uint32_t)__builtin_ctz(bits);
+                        const uint32_t rest = bits & (bits - 1u);
+                        bA = fromA ? rest : bA;
+                        bB = fromA ? bB : rest;
+                        const float4 qb4 = T.b[t];
+                        const v3 wi = mk(T.w[t], qb4.w, T.c[t]);
                         if (NN) {
-                            const float4 pa = T.a[t], pb = T.b[t];
-                            const v3 c = fabsf(dot(R.ns, mk(pa.w, pb.w, T.c[t]))) * R.fv * xyz(pb); /* processPhoton */
-                            dx += (double)rintf(c.x * sc); dy += (double)rintf(c.y * sc); dz += (double)rintf(c.z * sc);
+                            /* fvs = fv * 2^S: the power-of-two scale commutes with the
+                             * rounding, so this is rint(c * 2^S) for c of processPhoton */
+                            const v3 c = fabsf(dot(R.ns, wi)) * fvs * xyz(qb4);
+                            dx += (double)rintf(c.x); dy += (double)rintf(c.y); dz += (double)rintf(c.z);
                         } else {
-                            add_hit(Lf, R.ns, R.fv, T.a[t], T.b[t], T.c[t], sc);
+                            add_hit(Lf, R.ns, R.fv, make_float4(0.f, 0.f, 0.f, wi.x), qb4, wi.z, sc);
                         }
                     }
                 }
@@ -402,8 +479,11 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_tile(GatherParams P) {
             }
         } else {
             direct = direct || R.small;
+            TILE_STAT(6, 1);
         }
     }
+    TILE_STAT(4, __builtin_popcountll(__ballot(direct)));
+    if (!shaded) R.shade(P);
     if (NN) {
         if (fmax(fmax(dx, dy), dz) < 0x1p53) {
             Lf.x = (long long)dx; Lf.y = (long long)dy; Lf.z = (long long)dz;

@@ -1,0 +1,23 @@
+"""k_gather_tile event counts at C2 (PM_TILE_STATS variant build):
+   make -C cuda-raytrace_amd variant NAME=tstats VFLAGS=-DPM_TILE_STATS
+   PMHIP_LIB=cuda-raytrace_amd/lib/variants/libpmhip_tstats.so python tools/tile_stats.py"""
+import os, sys
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(R, "cuda-raytrace_amd"))
+import torch  # noqa: F401
+from pmrender import hip, scenes
+from pmrender.abi import RenderParams
+sc = scenes.cornell_box(1920, 1080)
+ctx = sc.load_into(hip.Context(0))
+p = RenderParams.defaults(paths_per_pass=262144)
+ctx.eye_pass(p)
+ctx.trace_photons(p, 0, 0, 262144)
+ctx.build_photon_map(p, 262144 * 4)
+ctx.synchronize()
+ctx.trace_profile(reset=True)
+ctx.gather(p)
+ctx.synchronize()
+v = list(ctx.trace_profile().values())
+names = ["tile_waves", "windows", "test_pairs", "hit_iters", "direct_lanes", "chunks", "wide_waves", "staged"]
+for k, x in zip(names, v):
+    print(f"{k:14s} {x:12d}  per tile wave {x / max(v[0], 1):8.2f}")
