@@ -153,7 +153,8 @@ struct GatherRec {
         p = xyz(pos);
         if (r2 > 0.f) {
             const GridDesc &g = P.grid;
-            const float rq = sqrtf(r2) * 1.0001f + 1e-4f;
+            /* hardware sqrt (<= 1 ulp): the 1e-4 relative margin covers it */
+            const float rq = __builtin_amdgcn_sqrtf(r2) * 1.0001f + 1e-4f;
             /* cells overlapping [p - r', p + r']: cell edge >= 2 r_max, so at
              * most 2 per axis -> at most 4 (y, z) rows of <= 2 cells in x */
             x0 = cell_axis(p.x - rq, g.gx, g.inv_cs, g.dx); x1 = cell_axis(p.x + rq, g.gx, g.inv_cs, g.dx);
@@ -170,19 +171,22 @@ struct GatherRec {
         fv = __float_as_int(m.w) == PM_MATTE ? xyz(m) * INV_PI : mk(0.f, 0.f, 0.f);
         ns = xyz(nrm);
     }
-    /* fused PPM update (gathering.cu:104-126) or the partial of the exchange */
+    /* fused PPM update (gathering.cu:104-126) from the fixed-point sums as
+     * doubles (exact integers) */
+    PMD void store_sum(const GatherParams &P, int64_t r, int M, double sx, double sy, double sz) {
+        if (!live) return;
+        const double inv = P.fx_inv;
+        v3 L = mk((float)(sx * inv), (float)(sy * inv), (float)(sz * inv));
+        float N = P.fresh ? 0.f : P.R.n[r];
+        ppm_apply(st, N, M, L, P.ppm_alpha);
+        if (M > 0 || P.fresh) { P.R.state[r] = st; P.R.n[r] = N; }
+    }
+    /* fused PPM update or the partial of the exchange */
     template <int PARTIAL>
     PMD void store(const GatherParams &P, int64_t r, int M, Fx3 Lf) {
         if (!live) return;
-        if (PARTIAL) {
-            write_partial(P, partial_index(P, r), M, Lf);
-        } else {
-            const double inv = P.fx_inv;
-            v3 L = mk((float)((double)Lf.x * inv), (float)((double)Lf.y * inv), (float)((double)Lf.z * inv));
-            float N = P.fresh ? 0.f : P.R.n[r];
-            ppm_apply(st, N, M, L, P.ppm_alpha);
-            if (M > 0 || P.fresh) { P.R.state[r] = st; P.R.n[r] = N; }
-        }
+        if (PARTIAL) write_partial(P, partial_index(P, r), M, Lf);
+        else store_sum(P, r, M, (double)Lf.x, (double)Lf.y, (double)Lf.z);
     }
 };
 
@@ -297,6 +301,12 @@ PMD int64_t gather_block(const GatherParams &P) {
 }
 
 typedef float f2 __attribute__((ext_vector_type(2)));
+/* integer-valued double in [0, 2^53) -> int64, exactly (two 32-bit halves) */
+PMD long long d2ll(double d) {
+    const uint32_t hi = (uint32_t)(d * 0x1p-32);
+    const uint32_t lo = (uint32_t)fma((double)hi, -0x1p32, d);
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
 /* PM_TILE_STATS builds (make variant VFLAGS=-DPM_TILE_STATS): per-wave event
  * counts of k_gather_tile into counters[8..15] (read with pm_trace_profile):
  * tile waves, windows, test pairs, hit iterations, direct lanes, chunks,
@@ -313,6 +323,30 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #else
 #define TILE_OCC
 #endif
+/* the cell box [X0, X1] x [Y0, Y1] x [Z0, Z1] of the lanes with `in` set */
+PMD void union_box(const GridDesc &g, const GatherRec &R, bool in, uint32_t &X0, uint32_t &X1, uint32_t &Y0,
+                   uint32_t &Y1, uint32_t &Z0, uint32_t &Z1) {
+    if (g.dx < 65536 && g.dy < 65536 && g.dz < 65536) {
+        /* three packed 16-bit minima (maxima as minima of 0xffff - c) */
+        const uint32_t m0 = wave_min_2x16(in ? (R.x0 << 16) | R.y0 : 0xffffffffu);
+        const uint32_t m1 = wave_min_2x16(in ? ((0xffffu - R.x1) << 16) | (0xffffu - R.y1) : 0xffffffffu);
+        const uint32_t m2 = wave_min_2x16(in ? (R.z0 << 16) | (0xffffu - R.z1) : 0xffffffffu);
+        X0 = m0 >> 16; Y0 = m0 & 0xffffu; X1 = 0xffffu - (m1 >> 16); Y1 = 0xffffu - (m1 & 0xffffu);
+        Z0 = m2 >> 16; Z1 = 0xffffu - (m2 & 0xffffu);
+    } else {
+        X0 = wave_min_u32(in ? R.x0 : 0xffffffffu); X1 = wave_max_u32(in ? R.x1 : 0u);
+        Y0 = wave_min_u32(in ? R.y0 : 0xffffffffu); Y1 = wave_max_u32(in ? R.y1 : 0u);
+        Z0 = wave_min_u32(in ? R.z0 : 0xffffffffu); Z1 = wave_max_u32(in ? R.z1 : 0u);
+    }
+}
+#ifndef PM_GROUP_R
+#define PM_GROUP_R 3
+#endif
+/* a group takes the lanes whose box starts within GROUP_R cells of the
+ * leader's: y rows [ly - R, ly + R + 1] fit the row pitch 8, z layers x 8
+ * rows fit the 64 lanes */
+constexpr uint32_t GROUP_R = PM_GROUP_R;
+static_assert(2 * GROUP_R + 2 <= 8, "group rows exceed the 64-lane row map");
 template <int PARTIAL, int NN>
 __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherParams P) {
     __shared__ TileLds tiles[GATHER_BLOCK / 64];
@@ -332,161 +366,165 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
      * non-negative terms never exceed it), and 4 instructions per channel
      * instead of a float -> int64 conversion and a 64-bit add */
     double dx = 0.0, dy = 0.0, dz = 0.0;
-    bool direct = R.big; /* lanes that scan their own cells from global memory */
-    bool shaded = false;
-    if (__ballot(R.small) != 0ull) {
+    R.shade(P);
+    const v3 fvs = R.fv * sc;
+    const f2 px2 = {R.p.x, R.p.x}, py2 = {R.p.y, R.p.y}, pz2 = {R.p.z, R.p.z};
+    /* Groups: the first pending lane leads; every pending lane whose box
+     * starts within GROUP_R cells of the leader's on each axis joins. A
+     * group's union box is at most (2 GROUP_R + 2)^3 cells (<= 8 x 8 rows),
+     * so it always fits the 64-lane row map; a coherent tile is one group, a
+     * tile across a depth edge two or three, never one huge box. */
+    bool pend = R.small;
+    while (true) {
+        const unsigned long long pm = __ballot(pend);
+        if (pm == 0ull) break;
+        /* the box of all pending lanes when it fits the row map (the common,
+         * coherent tile: one group), else the leader's neighbourhood */
         uint32_t X0, X1, Y0, Y1, Z0, Z1;
-        if (g.dx < 65536 && g.dy < 65536 && g.dz < 65536) {
-            /* three packed 16-bit minima (maxima as minima of 0xffff - c) */
-            const uint32_t m0 = wave_min_2x16(R.small ? (R.x0 << 16) | R.y0 : 0xffffffffu);
-            const uint32_t m1 = wave_min_2x16(R.small ? ((0xffffu - R.x1) << 16) | (0xffffu - R.y1) : 0xffffffffu);
-            const uint32_t m2 = wave_min_2x16(R.small ? (R.z0 << 16) | (0xffffu - R.z1) : 0xffffffffu);
-            X0 = m0 >> 16; Y0 = m0 & 0xffffu; X1 = 0xffffu - (m1 >> 16); Y1 = 0xffffu - (m1 & 0xffffu);
-            Z0 = m2 >> 16; Z1 = 0xffffu - (m2 & 0xffffu);
-        } else {
-            X0 = wave_min_u32(R.small ? R.x0 : 0xffffffffu); X1 = wave_max_u32(R.small ? R.x1 : 0u);
-            Y0 = wave_min_u32(R.small ? R.y0 : 0xffffffffu); Y1 = wave_max_u32(R.small ? R.y1 : 0u);
-            Z0 = wave_min_u32(R.small ? R.z0 : 0xffffffffu); Z1 = wave_max_u32(R.small ? R.z1 : 0u);
+        bool mine = pend;
+        union_box(g, R, mine, X0, X1, Y0, Y1, Z0, Z1);
+        /* row pitch: NY rounded up to a power of two, 2^LY */
+        uint32_t LY = Y1 > Y0 ? 32u - (uint32_t)__builtin_clz(Y1 - Y0) : 0u;
+        if (LY > 6u || ((uint64_t)(Z1 - Z0 + 1u) << LY) > 64u) {
+            const int leader = __builtin_ctzll(pm);
+            const uint32_t lx = __builtin_amdgcn_readlane(R.x0, leader), ly = __builtin_amdgcn_readlane(R.y0, leader),
+                           lz = __builtin_amdgcn_readlane(R.z0, leader);
+            mine = pend && R.x0 + GROUP_R - lx <= 2u * GROUP_R && R.y0 + GROUP_R - ly <= 2u * GROUP_R &&
+                   R.z0 + GROUP_R - lz <= 2u * GROUP_R;
+            union_box(g, R, mine, X0, X1, Y0, Y1, Z0, Z1);
+            LY = 3u;
         }
-        const uint32_t NY = Y1 - Y0 + 1u, NZ = Z1 - Z0 + 1u;
-        if ((uint64_t)NY * NZ <= 64u) {
-            const uint32_t nu = NY * NZ;
-            TILE_STAT(0, 1);
-            /* 1. union row u = lane: photons [B, B + len) */
-            uint32_t B = 0u, len = 0u;
-            if ((uint32_t)lane < nu) {
-                const uint32_t cy = Y0 + (uint32_t)lane % NY, cz = Z0 + (uint32_t)lane / NY;
-                const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
-                B = P.cell_start[row + X0];
-                len = P.cell_start[row + X1 + 1u] - B;
+        pend = pend && !mine;
+        TILE_STAT(0, 1);
+        /* 1. union row u = lane: photons [B, B + len); u = (cz - Z0) * 2^LY +
+         * (cy - Y0) (no lane divides; padding rows are empty) */
+        uint32_t B = 0u, len = 0u;
+        const uint32_t cy = Y0 + ((uint32_t)lane & ((1u << LY) - 1u)), cz = Z0 + ((uint32_t)lane >> LY);
+        if (cy <= Y1 && cz <= Z1) {
+            const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+            B = P.cell_start[row + X0];
+            len = P.cell_start[row + X1 + 1u] - B;
+        }
+        const uint32_t incl = wave_incl_sum_u32(len), pre = incl - len;
+        const uint32_t U = uniform_u32(__builtin_amdgcn_readlane(incl, 63));
+        if (U == 0u) continue;
+        const uint32_t gofs = B - pre; /* photon index of concatenated position t in row u: t + gofs_u */
+        /* this lane's rows as two runs of the concatenation: rows (y0, z) and
+         * (y0 + 1, z) are neighbours in the union, so each z-layer of the
+         * lane's box is one contiguous run [sA, eA) / [sB, eB) */
+        const uint32_t ny = mine ? R.y1 - R.y0 + 1u : 1u;
+        const int uA = mine ? (int)(((R.z0 - Z0) << LY) + (R.y0 - Y0)) : 0;
+        const int uB = mine && R.z1 > R.z0 ? uA + (1 << LY) : uA;
+        /* every lane shuffles: a bpermute from a lane that is inactive at the
+         * shuffle reads 0 */
+        const uint32_t sA0 = (uint32_t)__shfl((int)pre, uA), eA0 = (uint32_t)__shfl((int)incl, uA + (int)ny - 1);
+        const uint32_t sB0 = (uint32_t)__shfl((int)pre, uB), eB0 = (uint32_t)__shfl((int)incl, uB + (int)ny - 1);
+        const uint32_t sA = mine ? sA0 : 0u, eA = mine ? eA0 : 0u;
+        const uint32_t sB = mine && R.z1 > R.z0 ? sB0 : 0u, eB = mine && R.z1 > R.z0 ? eB0 : 0u;
+        for (uint32_t T0 = 0; T0 < U; T0 += TILE_CAP) {
+            const uint32_t n = min((uint32_t)TILE_CAP, U - T0);
+            TILE_STAT(1, 1);
+            TILE_STAT(7, n);
+            /* 2. stage positions T0 + lane (and T0 + 64 + lane) */
+            constexpr int H = TILE_CAP / 64;
+            static_assert(H == 1 || H == 2, "TILE_CAP is 64 or 128");
+#pragma unroll
+            for (int h = 0; h < H; ++h) T.mark[lane + 64 * h] = -1;
+            wave_lds_sync();
+            if (len > 0u) {
+                if (pre >= T0 && pre < T0 + TILE_CAP) T.mark[pre - T0] = lane;
+                else if (pre < T0 && pre + len > T0) T.mark[0] = lane; /* row running into the window */
             }
-            R.shade(P); /* its material load overlaps the row bounds and the staging */
-            shaded = true;
-            const v3 fvs = R.fv * sc;
-            const uint32_t incl = wave_incl_sum_u32(len), pre = incl - len;
-            const uint32_t U = uniform_u32(__builtin_amdgcn_readlane(incl, 63));
-            const uint32_t gofs = B - pre; /* photon index of concatenated position t in row u: t + gofs_u */
-            /* this lane's rows as two runs of the concatenation: rows (y0, z)
-             * and (y0 + 1, z) are neighbours in the union, so each z-layer of
-             * the lane's box is one contiguous run [sA, eA) / [sB, eB) */
-            const uint32_t ny = R.small ? R.y1 - R.y0 + 1u : 1u;
-            const int uA = R.small ? (int)((R.z0 - Z0) * NY + (R.y0 - Y0)) : 0;
-            const int uB = R.small && R.z1 > R.z0 ? uA + (int)NY : uA;
-            /* every lane shuffles: a bpermute from a lane that is inactive at
-             * the shuffle reads 0 */
-            const uint32_t sA = (uint32_t)__shfl((int)pre, uA), eA0 = (uint32_t)__shfl((int)incl, uA + (int)ny - 1);
-            const uint32_t sB = (uint32_t)__shfl((int)pre, uB), eB0 = (uint32_t)__shfl((int)incl, uB + (int)ny - 1);
-            const uint32_t eA = R.small ? eA0 : sA;
-            const uint32_t eB = R.small && R.z1 > R.z0 ? eB0 : sB;
-            const f2 px2 = {R.p.x, R.p.x}, py2 = {R.p.y, R.p.y}, pz2 = {R.p.z, R.p.z};
-            for (uint32_t T0 = 0; T0 < U; T0 += TILE_CAP) {
-                const uint32_t n = min((uint32_t)TILE_CAP, U - T0);
-                TILE_STAT(1, 1);
-                TILE_STAT(7, n);
-                /* 2. stage positions T0 + lane (and T0 + 64 + lane) */
-                constexpr int H = TILE_CAP / 64;
-                static_assert(H == 1 || H == 2, "TILE_CAP is 64 or 128");
+            wave_lds_sync();
+            int u[H];
+            u[0] = wave_incl_max_i32(T.mark[lane]);
+            if (H == 2) u[H - 1] = max(wave_incl_max_i32(T.mark[lane + 64 * (H - 1)]), __builtin_amdgcn_readlane(u[0], 63));
+            uint32_t gi[H];
 #pragma unroll
-                for (int h = 0; h < H; ++h) T.mark[lane + 64 * h] = -1;
-                wave_lds_sync();
-                if (len > 0u) {
-                    if (pre >= T0 && pre < T0 + TILE_CAP) T.mark[pre - T0] = lane;
-                    else if (pre < T0 && pre + len > T0) T.mark[0] = lane; /* row running into the window */
-                }
-                wave_lds_sync();
-                int u[H];
-                u[0] = wave_incl_max_i32(T.mark[lane]);
-                if (H == 2) u[H - 1] = max(wave_incl_max_i32(T.mark[lane + 64 * (H - 1)]), __builtin_amdgcn_readlane(u[0], 63));
-                uint32_t gi[H];
+            for (int h = 0; h < H; ++h) gi[h] = T0 + 64u * h + (uint32_t)lane + (uint32_t)__shfl((int)gofs, u[h]);
+            /* every load in flight, then the LDS writes; positions at or beyond
+             * n re-read position 0's photon (n >= 1) and are never read */
+            const float *phb = reinterpret_cast<const float *>(P.ph_b);
+            const uint32_t g0 = (uint32_t)__builtin_amdgcn_readlane((int)gi[0], 0);
+            float4 pa[H], qa[H];
+            float ca[H];
 #pragma unroll
-                for (int h = 0; h < H; ++h) gi[h] = T0 + 64u * h + (uint32_t)lane + (uint32_t)__shfl((int)gofs, u[h]);
-                /* every load in flight, then the LDS writes; positions at or
-                 * beyond n re-read position 0's photon (n >= 1) and are never read */
-                const float *phb = reinterpret_cast<const float *>(P.ph_b);
-                const uint32_t g0 = (uint32_t)__builtin_amdgcn_readlane((int)gi[0], 0);
-                float4 pa[H], qa[H];
-                float ca[H];
+            for (int h = 0; h < H; ++h) {
+                const uint32_t j = (uint32_t)lane + 64u * h < n ? gi[h] : g0;
+                pa[h] = P.ph_a[j]; qa[h] = P.ph_b[2 * (size_t)j]; ca[h] = phb[8 * (size_t)j + 4];
+            }
 #pragma unroll
-                for (int h = 0; h < H; ++h) {
-                    const uint32_t j = (uint32_t)lane + 64u * h < n ? gi[h] : g0;
-                    pa[h] = P.ph_a[j]; qa[h] = P.ph_b[2 * (size_t)j]; ca[h] = phb[8 * (size_t)j + 4];
-                }
-#pragma unroll
-                for (int h = 0; h < H; ++h) {
-                    const int q = lane + 64 * h;
-                    T.x[q] = pa[h].x; T.y[q] = pa[h].y; T.z[q] = pa[h].z; T.w[q] = pa[h].w;
-                    T.b[q] = qa[h]; T.c[q] = ca[h];
-                }
-                wave_lds_sync();
-                /* 3. each run of this lane within the window: positions [lo,
-                 * lo + cnt) of the LDS window. Tested two photons per packed
-                 * instruction, 32 positions at a time, into a hit mask; the hits
-                 * are then summed with every lane busy (max over lanes of its
-                 * hits per chunk, instead of one masked pass per photon that
-                 * any lane hits). */
-                const uint32_t loA = max(sA, T0), hiA = min(eA, T0 + n), mA = hiA > loA ? hiA - loA : 0u;
-                const uint32_t loB = max(sB, T0), hiB = min(eB, T0 + n), mB = hiB > loB ? hiB - loB : 0u;
-                const uint32_t baseA = mA ? loA - T0 : 0u, baseB = mB ? loB - T0 : 0u; /* < TILE_CAP */
-                const uint32_t vmaxA = wave_max_u32(mA), vmaxB = wave_max_u32(mB);
-                /* hit mask of positions [v0, v0 + 32) of a run starting at LDS
-                 * position base (cnt of them tested, wave-uniform) */
-                auto test32 = [&](uint32_t base, uint32_t v0, uint32_t cnt, uint32_t m) {
-                    const float *xs = T.x + base + v0, *ys = T.y + base + v0, *zs = T.z + base + v0;
-                    uint32_t bits = 0u;
+            for (int h = 0; h < H; ++h) {
+                const int q = lane + 64 * h;
+                T.x[q] = pa[h].x; T.y[q] = pa[h].y; T.z[q] = pa[h].z; T.w[q] = pa[h].w;
+                T.b[q] = qa[h]; T.c[q] = ca[h];
+            }
+            wave_lds_sync();
+            /* 3. each run of this lane within the window: LDS positions [base,
+             * base + m). Tested two photons per packed instruction, 32
+             * positions at a time, into hit masks; the hits of both runs are
+             * then summed in one loop with every lane busy (max over lanes of
+             * its hits per chunk, not one masked pass per photon any lane hits). */
+            auto test32 = [&](uint32_t base, uint32_t v0, uint32_t cnt, uint32_t m) {
+                const float *xs = T.x + base + v0, *ys = T.y + base + v0, *zs = T.z + base + v0;
+                uint32_t bits = 0u;
 #pragma unroll 4
-                    for (uint32_t j = 0; j < cnt; j += 2) {
-                        /* in_radius for both photons: ((dx^2 + dy^2) + dz^2) < r^2 */
-                        const f2 ddx = px2 - f2{xs[j], xs[j + 1]}, ddy = py2 - f2{ys[j], ys[j + 1]},
-                                 ddz = pz2 - f2{zs[j], zs[j + 1]};
-                        const f2 d2 = (ddx * ddx + ddy * ddy) + ddz * ddz;
-                        if (d2.x < R.r2) bits |= 1u << j;
-                        if (d2.y < R.r2) bits |= 2u << j;
-                    }
-                    /* positions at or beyond m belong to the next run / window */
-                    const uint32_t left = m > v0 ? m - v0 : 0u;
-                    return bits & (left >= 32u ? 0xffffffffu : (1u << left) - 1u);
-                };
-                const uint32_t vmax = max(vmaxA, vmaxB);
-                for (uint32_t vb = 0; vb < vmax; vb += 32) {
-                    TILE_STAT(5, 1);
-                    TILE_STAT(2, (min(32u, vmaxA > vb ? vmaxA - vb : 0u) + 1) / 2 + (min(32u, vmaxB > vb ? vmaxB - vb : 0u) + 1) / 2);
-                    uint32_t bA = vmaxA > vb ? test32(baseA, vb, min(32u, vmaxA - vb), mA) : 0u;
-                    uint32_t bB = vmaxB > vb ? test32(baseB, vb, min(32u, vmaxB - vb), mB) : 0u;
-                    M += __builtin_popcount(bA) + __builtin_popcount(bB);
-                    TILE_STAT(3, wave_max_u32(__builtin_popcount(bA) + __builtin_popcount(bB)));
-                    /* both runs' hits in one loop: max over lanes of the sum,
-                     * not the sum of the two maxima */
-                    while (bA | bB) {
-                        const bool fromA = bA != 0u;
-                        const uint32_t bits = fromA ? bA : bB;
-                        const uint32_t t = (fromA ? baseA : baseB) + vb + (uint32_t)__builtin_ctz(bits);
-                        const uint32_t rest = bits & (bits - 1u);
-                        bA = fromA ? rest : bA;
-                        bB = fromA ? bB : rest;
-                        const float4 qb4 = T.b[t];
-                        const v3 wi = mk(T.w[t], qb4.w, T.c[t]);
-                        if (NN) {
-                            /* fvs = fv * 2^S: the power-of-two scale commutes with the
-                             * rounding, so this is rint(c * 2^S) for c of processPhoton */
-                            const v3 c = fabsf(dot(R.ns, wi)) * fvs * xyz(qb4);
-                            dx += (double)rintf(c.x); dy += (double)rintf(c.y); dz += (double)rintf(c.z);
-                        } else {
-                            add_hit(Lf, R.ns, R.fv, make_float4(0.f, 0.f, 0.f, wi.x), qb4, wi.z, sc);
-                        }
-                    }
+                for (uint32_t j = 0; j < cnt; j += 2) {
+                    /* in_radius for both photons: ((dx^2 + dy^2) + dz^2) < r^2 */
+                    const f2 ddx = px2 - f2{xs[j], xs[j + 1]}, ddy = py2 - f2{ys[j], ys[j + 1]},
+                             ddz = pz2 - f2{zs[j], zs[j + 1]};
+                    const f2 d2 = (ddx * ddx + ddy * ddy) + ddz * ddz;
+                    if (d2.x < R.r2) bits |= 1u << j;
+                    if (d2.y < R.r2) bits |= 2u << j;
                 }
-                wave_lds_sync(); /* the window is read before the next one overwrites it */
+                /* positions at or beyond m belong to the next run / window */
+                const uint32_t left = m > v0 ? m - v0 : 0u;
+                return bits & (left >= 32u ? 0xffffffffu : (1u << left) - 1u);
+            };
+            auto hit = [&](uint32_t t) {
+                const float4 qb4 = T.b[t];
+                const v3 wi = mk(T.w[t], qb4.w, T.c[t]);
+                if (NN) {
+                    /* fvs = fv * 2^S: the power-of-two scale commutes with the
+                     * rounding, so this is rint(c * 2^S) for c of processPhoton */
+                    const v3 c = fabsf(dot(R.ns, wi)) * fvs * xyz(qb4);
+                    dx += (double)rintf(c.x); dy += (double)rintf(c.y); dz += (double)rintf(c.z);
+                } else {
+                    add_hit(Lf, R.ns, R.fv, make_float4(0.f, 0.f, 0.f, wi.x), qb4, wi.z, sc);
+                }
+            };
+            const uint32_t loA = max(sA, T0), hiA = min(eA, T0 + n), mA = hiA > loA ? hiA - loA : 0u;
+            const uint32_t loB = max(sB, T0), hiB = min(eB, T0 + n), mB = hiB > loB ? hiB - loB : 0u;
+            const uint32_t baseA = mA ? loA - T0 : 0u, baseB = mB ? loB - T0 : 0u; /* < TILE_CAP */
+            const uint32_t vmaxA = wave_max_u32(mA), vmaxB = wave_max_u32(mB);
+            const uint32_t vmax = max(vmaxA, vmaxB);
+            for (uint32_t vb = 0; vb < vmax; vb += 32) {
+                TILE_STAT(5, 1);
+                TILE_STAT(2, (min(32u, vmaxA > vb ? vmaxA - vb : 0u) + 1) / 2 + (min(32u, vmaxB > vb ? vmaxB - vb : 0u) + 1) / 2);
+                uint32_t bA = vmaxA > vb ? test32(baseA, vb, min(32u, vmaxA - vb), mA) : 0u;
+                uint32_t bB = vmaxB > vb ? test32(baseB, vb, min(32u, vmaxB - vb), mB) : 0u;
+                M += __builtin_popcount(bA) + __builtin_popcount(bB);
+                TILE_STAT(3, wave_max_u32(__builtin_popcount(bA) + __builtin_popcount(bB)));
+                while (bA | bB) {
+                    const bool fromA = bA != 0u;
+                    const uint32_t bits = fromA ? bA : bB;
+                    const uint32_t t = (fromA ? baseA : baseB) + vb + (uint32_t)__builtin_ctz(bits);
+                    const uint32_t rest = bits & (bits - 1u);
+                    bA = fromA ? rest : bA;
+                    bB = fromA ? bB : rest;
+                    hit(t);
+                }
             }
-        } else {
-            direct = direct || R.small;
-            TILE_STAT(6, 1);
+            wave_lds_sync(); /* the window is read before the next one overwrites it */
         }
     }
+    /* lanes whose radius exceeds the grid's design radius scan their own
+     * cells from global memory */
+    bool direct = R.big;
     TILE_STAT(4, __builtin_popcountll(__ballot(direct)));
-    if (!shaded) R.shade(P);
     if (NN) {
         if (fmax(fmax(dx, dy), dz) < 0x1p53) {
-            Lf.x = (long long)dx; Lf.y = (long long)dy; Lf.z = (long long)dz;
+            Lf.x = d2ll(dx); Lf.y = d2ll(dy); Lf.z = d2ll(dz);
         } else if (R.small) { /* inexact (or NaN): this record again in int64 */
             M = 0;
             direct = true;
