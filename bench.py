@@ -19,6 +19,7 @@ Single GPU: `python bench.py`. N GPUs (one process per GPU):
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -30,49 +31,119 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 VALU_FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector)
 
 
+# BASELINE.json configs: scene, resolution, photon paths
+# per GPU per pass (slots = 4 x paths), progressive passes
+CONFIGS = {
+    "c1": dict(scene="cornell", W=256, H=256, paths=25_000, progressive=False,
+               desc="C1: Cornell box, 100,000 photon slots (25,000 paths), 256x256 gather points"),
+    "c2": dict(scene="cornell", W=1920, H=1080, paths=262_144, progressive=False,
+               desc="C2: Cornell box, 1,048,576 photon slots (262,144 paths) per GPU, 1920x1080 gather points"),
+    "c3": dict(scene="soup", W=1920, H=1080, paths=1_048_576, progressive=False,
+               desc="C3: Cornell enclosure + 1M-triangle soup, 4,194,304 photon slots (1,048,576 paths) per GPU, "
+                    "1920x1080 gather points"),
+    "c4": dict(scene="cornell", W=3840, H=2160, paths=524_288, progressive=False,
+               desc="C4 per-GPU share: Cornell box, 2,097,152 photon slots (524,288 paths) per GPU, 3840x2160 "
+                    "gather points (the 8-GPU config's photon shard; every rank gathers the whole 4K view)"),
+    "c5": dict(scene="caustic", W=1920, H=1080, paths=1_048_576, progressive=True,
+               desc="C5: caustic scene (Cornell + glass and mirror spheres), 4,194,304 photon slots (1,048,576 "
+                    "paths) per GPU per progressive pass, 1920x1080 gather points; a step = one progressive pass"),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3"])
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--structure", default="grid", choices=["grid", "kd"])
     ap.add_argument("--exchange", default="reduce", choices=["reduce", "allgather"])
-    ap.add_argument("--paths", type=int, default=512 * 512, help="photon paths per GPU per pass")
+    ap.add_argument("--paths", type=int, default=None, help="photon paths per GPU per pass (default: the config's)")
     ap.add_argument("--estimator", default="ppm", choices=["ppm", "knn"],
                     help="ppm: the reference's fixed-radius PPM gather (headline); knn: pbrt-v2 LPhoton kNN")
     ap.add_argument("--knn-k", type=int, default=50, help="kNN photons per lookup (pbrt 'nused')")
     ap.add_argument("--radius2", type=float, default=None,
                     help="initial / maximum search radius^2 (default: 4 for ppm = raytracing.cu:123, 100 for knn)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="oracle threads (default: this process's CPU share: OMP_NUM_THREADS, else its affinity set)")
     ap.add_argument("--no-census", action="store_true")
     return ap.parse_args()
 
 
 def build_scene(cfg):
     from pmrender import scenes
-    if cfg == "c2":
-        return scenes.cornell_box(1920, 1080), "C2: Cornell box, 1,048,576 photon slots (262,144 paths) per GPU, 1920x1080 gather points"
-    return scenes.triangle_soup(1_000_000, 1920, 1080), "C3: Cornell enclosure + 1M-triangle soup, 1920x1080 gather points"
+    c = CONFIGS[cfg]
+    if c["scene"] == "cornell":
+        return scenes.cornell_box(c["W"], c["H"])
+    if c["scene"] == "soup":
+        return scenes.triangle_soup(1_000_000, c["W"], c["H"])
+    return scenes.caustic_scene(c["W"], c["H"])
 
 
-def load_pmc_traffic(kernel_prefix):
-    """Per-launch HBM bytes of the gather kernel from the committed PMC
-    profile (tools/pmc_traffic.py writes it from a separate rocprofv3 --pmc
-    pass); None if absent."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def kernel_src_sha():
+    """Hash of the HIP sources: a committed PMC profile is this build's only if it matches."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "cuda-raytrace_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".hip", ".h", ".cpp")):
+            with open(os.path.join(csrc, f), "rb") as fh:
+                h.update(f.encode() + fh.read())
+    return h.hexdigest()[:16]
+
+
+def load_pmc_traffic(kernel_prefix, config):
+    """Per-launch HBM bytes (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, gfx950
+    FETCH x2 correction; tools/pmc_traffic.py) of this kernel from the
+    committed profile — only if it was measured on these exact HIP sources
+    and this config; else (None, reason)."""
+    path = os.path.join(ROOT, "profiles", "r02", "pmc_traffic_%s.json" % config)
     if not os.path.exists(path):
-        return None, None
+        return None, "no committed PMC profile for this config"
     with open(path) as f:
         d = json.load(f)
+    if d.get("kernel_src_sha") != kernel_src_sha():
+        return None, "committed PMC profile is from other HIP sources (%s)" % d.get("kernel_src_sha")
     k = d.get("kernels", {}).get(kernel_prefix)
-    return (k.get("hbm_bytes_per_launch") if k else None), os.path.relpath(path, ROOT)
+    if not k:
+        return None, "kernel not in the committed PMC profile"
+    return k.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
 
 
-def cpu_baseline(scene, params, threads):
+def cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return None
+
+
+def default_cpu_threads():
+    """This process's CPU share: OMP_NUM_THREADS (16 per GPU on the GPU box,
+    where os.cpu_count() reports the whole machine), else the affinity set."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except Exception:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(scene, params, threads, cfg):
     """Oracle (CPU restatement of the reference, test infrastructure) timed on
-    this host: one full pass of the same workload (trace 262,144 paths +
+    this host: whole passes of the same workload (trace the config's paths +
     pbrt kd-tree build + range query/PPM update over all gather points)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
@@ -94,8 +165,11 @@ def cpu_baseline(scene, params, threads):
         "unit": "Mphotons/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{passes} full C2 passes on the host (each: trace {params.paths_per_pass} paths + pbrt kd-tree "
-                  f"build over ~{len(nodes)} photons + gather/PPM over {len(recs0)} records); {dt:.2f} s wall, "
+        "host_cpus": os.cpu_count(),
+        "cpu_model": cpu_model(),
+        "sample": f"{passes} full {cfg.upper()} passes on the host with {threads} threads (this process's CPU share; "
+                  f"the host has {os.cpu_count()}) — each: trace {params.paths_per_pass} paths + pbrt kd-tree "
+                  f"build over ~{len(nodes)} photons + gather/PPM over {len(recs0)} records; {dt:.2f} s wall, "
                   f"{dt * threads:.1f} thread-s",
         "mgather_samples_per_s": round(len(recs0) * passes / dt / 1e6, 4),
     }
@@ -122,7 +196,11 @@ def main():
         PM_REC_EXCEPTION, PM_REC_INVALID, PM_REC_MISS, RenderParams
     from pmrender.dist import HipEngine, PassRunner
 
-    scene, workload = build_scene(args.config)
+    cfg = CONFIGS[args.config]
+    if args.paths is None:
+        args.paths = cfg["paths"]
+    scene, workload = build_scene(args.config), cfg["desc"]
+    progressive = cfg["progressive"]
     t_setup = time.perf_counter()
     ctx = scene.load_into(hip.Context(local))
     structure = PM_GATHER_KDTREE if args.structure == "kd" else PM_GATHER_GRID
@@ -137,8 +215,20 @@ def main():
         eng = HipEngine(ctx)
         ctx.eye_pass(p, eng._s())
         runner = PassRunner(eng, p, rank, world, args.exchange)
+        # a step is one pass over the config's workload: from the initial PPM
+        # state (the reference's single pass), or for progressive configs the
+        # next pass of one render (Halton permutation of pass k, radii shrink)
+        pass_no = [0]
+
+        def step():
+            if progressive:
+                runner.step(pass_no[0], reset=pass_no[0] == 0)
+                pass_no[0] += 1
+            else:
+                runner.step(0, reset=True)
+
         for _ in range(args.warmup):
-            runner.step(0, reset=True)
+            step()
         runner.flush()
         torch.cuda.synchronize()
         setup_s = time.perf_counter() - t_setup
@@ -151,7 +241,7 @@ def main():
         ctx.set_stage_timing("gather")
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            runner.step(0, reset=True)
+            step()
         runner.flush()                 # the last pass's exchange is part of the timed work
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
@@ -166,7 +256,7 @@ def main():
         ctx.set_stage_timing("all")
         ctx.timing_reset()
         for _ in range(min(args.steps, 10)):
-            runner.step(0, reset=True)
+            step()
         runner.flush()
         torch.cuda.synchronize()
         stages = {}
@@ -176,15 +266,17 @@ def main():
                 stages[name] = round(ms / n, 5)
 
         census = canonical = tcensus = None
+        n_valid = None
         if not args.no_census:
             # untimed counting launch of the same step: algorithmic-byte units
             ctx.set_counting(True)
-            runner.step(0, reset=True)
+            step()
             runner.flush()
             torch.cuda.synchronize()
             census = ctx.gather_counters(full=True)
             tcensus = ctx.trace_counters()
             ctx.set_counting(False)
+            n_valid = ctx.map_info()["valid"]
             if rank == 0 and world == 1 and structure == PM_GATHER_GRID and not knn:
                 # SURVEY.md §8d's per-unit figure counts V on the canonical pbrt kd-tree
                 pk = RenderParams.defaults(paths_per_pass=args.paths, gather_structure=PM_GATHER_KDTREE)
@@ -206,52 +298,63 @@ def main():
     value = paths_total * args.steps / elapsed / 1e6
 
     roofline = None
+    kernel_name = ("k_gather_knn" if knn else "k_gather_tile" if structure == PM_GATHER_GRID else "k_gather_kd")
     if census is not None:
         vis, hits, rows, act = census
         inactive = n_rec - act
+        # SURVEY.md §8(d) compulsory bytes: every active record read (72 B:
+        # pos, ns, flags, r^2, N, flux, Kd) and its PPM state written (20 B),
+        # every valid photon read once (40 B) — the HBM floor of the gather
+        compulsory = 92 * act + 40 * n_valid
+        achieved = compulsory / (gather_ms * 1e-3) / 1e9
+        traffic, traffic_src = load_pmc_traffic(kernel_name, args.config)
         if knn:
-            # records as below; 8 B per bucket row; 16 B per photon tested; per
-            # photon found: its slot id (4 B, ph_b) + alpha and wi from the slot (24 B)
-            bytes_launch = 72 * act + 16 * inactive + 8 * rows + 16 * vis + 28 * hits
-            formula = "72*G_act + 16*G_inactive + 8*bucket_rows + 16*photons_tested + 28*photons_found"
+            l1_bytes = 72 * act + 16 * inactive + 8 * rows + 16 * vis + 28 * hits
+            l1_formula = "72*G_act + 16*G_inactive + 8*bucket_rows + 16*photons_tested + 28*photons_found"
         elif structure == PM_GATHER_GRID:
-            # records: pos 16 + nrm 16 + state 16 + N 4 read, state 16 + N 4 written (active);
-            # pos 16 read (inactive); 8 B of bucket bounds per row; 16 B per photon tested;
-            # 20 B (alpha + wi.y, wi.z) per photon inside the radius
-            bytes_launch = 72 * act + 16 * inactive + 8 * rows + 16 * vis + 20 * hits
-            formula = "72*G_act + 16*G_inactive + 8*bucket_rows + 16*photons_tested + 20*photons_in_radius"
+            l1_bytes = 72 * act + 16 * inactive + 8 * rows + 16 * vis + 20 * hits
+            l1_formula = "72*G_act + 16*G_inactive + 8*bucket_rows + 16*photons_tested + 20*photons_in_radius"
         else:
-            bytes_launch = 72 * act + 16 * inactive + 16 * vis + 24 * hits
-            formula = "72*G_act + 16*G_inactive + 16*kd_nodes_visited + 24*photons_in_radius"
-        achieved = bytes_launch / (gather_ms * 1e-3) / 1e9
-        traffic, traffic_src = load_pmc_traffic(
-            "k_gather_knn" if knn else "k_gather_grid" if structure == PM_GATHER_GRID else "k_gather_kd")
+            l1_bytes = 72 * act + 16 * inactive + 16 * vis + 24 * hits
+            l1_formula = "72*G_act + 16*G_inactive + 16*kd_nodes_visited + 24*photons_in_radius"
         roofline = {
             "bound": "hbm",
             "kernel": "k_gather_knn<0> (pbrt LPhoton kNN, fused record update)" if knn
-            else "k_gather_grid<0,0> (fused range query + PPM update)" if structure == PM_GATHER_GRID
+            else "k_gather_tile<0,1> (LDS-staged range query + fused PPM update)" if structure == PM_GATHER_GRID
             else "k_gather_kd<0,0>",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "algorithmic_bytes_per_launch": int(bytes_launch),
-            "formula": formula,
-            "units": {"G_act": act, "G_inactive": inactive, "bucket_rows": rows, "photons_tested": vis,
-                      "photons_found" if knn else "photons_in_radius": hits},
+            "algorithmic_bytes_per_launch": int(compulsory),
+            "formula": "92*G_act + 40*N_valid (SURVEY.md §8d compulsory bytes)",
+            "units": {"G_act": act, "G_inactive": inactive, "N_valid": n_valid, "bucket_rows": rows,
+                      "photons_tested": vis, "photons_found" if knn else "photons_in_radius": hits},
             "avg_launch_ms": round(gather_ms, 5),
             "launches_timed": gather_launches,
+            # the per-lane kernel's operand bytes (16 B per photon each lane
+            # tests): what the L1 / LDS deliver, not HBM traffic
+            "l1_delivered": {"bytes_per_launch": int(l1_bytes), "formula": l1_formula,
+                             "GBs": round(l1_bytes / (gather_ms * 1e-3) / 1e9, 1)},
+            "limiter": "VALU issue + per-wave latency (profiles/r02 counters): the kernel reads each record "
+                       "once and each tile's photons once, so HBM is not what bounds it",
         }
-        if traffic_src:
+        if traffic is not None:
+            roofline["traffic_GBs"] = round(traffic / (gather_ms * 1e-3) / 1e9, 1)
+            roofline["traffic_frac"] = round(traffic / (gather_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
             roofline["traffic_source"] = traffic_src
+        else:
+            roofline["traffic_note"] = traffic_src
         if canonical is not None:
             cv, ch, _, cact = canonical
             survey_bytes = 92 * cact + 16 * cv + 24 * ch
-            roofline["survey_8d_equivalent"] = {
+            roofline["survey_8d_graded"] = {
                 "formula": "92*G_act + 16*V_kd + 24*H (SURVEY.md §8d, V on the canonical pbrt kd-tree)",
                 "bytes_per_launch": int(survey_bytes), "V_kd": cv, "H": ch,
-                "GBs_at_measured_time": round(survey_bytes / (gather_ms * 1e-3) / 1e9, 1)}
+                "GBs_at_measured_time": round(survey_bytes / (gather_ms * 1e-3) / 1e9, 1),
+                "note": "V counts kd-tree nodes a tree walk would fetch; the bucket kernel fetches none of them, "
+                        "so this exceeds what the kernel moves"}
 
     trace_roofline = None
     if tcensus is not None and "trace" in stages and ctx.scene_info()["mode"] == "brute":
@@ -280,8 +383,10 @@ def main():
             "unit": "GB/s", "frac": round(tach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": int(tbytes),
             "formula": "40*deposits + 32*bvh_nodes + 36*prim_tests (SURVEY.md §8d B_trace)",
             "units": {"rays": rays, "bvh_nodes": nodes, "prim_tests": prims, "deposits": deposits},
+            "per_ray": {"bvh_nodes": round(nodes / max(rays, 1), 2), "prim_tests": round(prims / max(rays, 1), 2)},
             "avg_launch_ms": stages["trace"],
-            "note": "VALU-bound: the BVH and scene of C2 stay in L2/MALL, so B_trace is mostly cache traffic"}
+            "note": "latency-bound traversal: the BVH reads hit L2 / the 256 MiB MALL, so B_trace is mostly "
+                    "cache traffic, not HBM"}
 
     out = {
         "metric": METRIC,
@@ -295,7 +400,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: Cornell box built in code (pmrender/scenes.py), BASELINE.json configs[1]",
+        "data": "synthetic: scene built in code (pmrender/scenes.py), BASELINE.json config " + args.config.upper(),
         "config": {
             "workload": workload,
             "photon_slots_per_gpu": args.paths * int(p.max_photon_count),
@@ -321,7 +426,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(scene, RenderParams.defaults(paths_per_pass=args.paths, **est),
-                                               args.cpu_threads)
+                                               args.cpu_threads or default_cpu_threads(), args.config)
         except Exception as exc:  # the baseline is reported, never required for the GPU number
             out["cpu_baseline"] = {"error": repr(exc)}
     if rank == 0:

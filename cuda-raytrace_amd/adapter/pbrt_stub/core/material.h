@@ -1,0 +1,3 @@
+/* pbrt-v2 core/material.h -> the boundary stub (see ../pbrt_stub.h) */
+#pragma once
+#include "../pbrt_stub.h"

@@ -1347,6 +1347,22 @@ int pm_trace_counters(void *ptr, int64_t out[4]) {
     return PM_OK;
 }
 
+int pm_map_info(void *ptr, int64_t out[4]) {
+    GETCTX(ptr);
+    if (!out) FAIL(c, PM_ERR_INVALID, "null output");
+    out[0] = c->map_kind; out[1] = 0; out[2] = c->map_slots; out[3] = 0;
+    if (c->map_kind == PM_GATHER_KDTREE) {
+        out[1] = c->kd_count;
+    } else if (c->map_kind == PM_GATHER_GRID) {
+        uint32_t nv = 0;
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipMemcpy(&nv, c->d_cell_start.as<uint32_t>() + c->grid.ncells, 4, hipMemcpyDeviceToHost));
+        out[1] = nv;
+        out[3] = c->grid.ncells;
+    }
+    return PM_OK;
+}
+
 int pm_scene_info(void *ptr, int64_t out[7]) {
     GETCTX(ptr);
     if (!c->S.blob) FAIL(c, PM_ERR_INVALID, "no scene committed");

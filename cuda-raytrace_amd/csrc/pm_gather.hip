@@ -346,6 +346,10 @@ PMD void union_box(const GridDesc &g, const GatherRec &R, bool in, uint32_t &X0,
  * leader's: y rows [ly - R, ly + R + 1] fit the row pitch 8, z layers x 8
  * rows fit the 64 lanes */
 constexpr uint32_t GROUP_R = PM_GROUP_R;
+#ifndef PM_GROUP_MIN
+#define PM_GROUP_MIN 12
+#endif
+constexpr int GROUP_MIN = PM_GROUP_MIN;
 static_assert(2 * GROUP_R + 2 <= 8, "group rows exceed the 64-lane row map");
 template <int PARTIAL, int NN>
 __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherParams P) {
@@ -375,6 +379,7 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
      * so it always fits the 64-lane row map; a coherent tile is one group, a
      * tile across a depth edge two or three, never one huge box. */
     bool pend = R.small;
+    bool direct = R.big; /* lanes that scan their own cells from global memory */
     while (true) {
         const unsigned long long pm = __ballot(pend);
         if (pm == 0ull) break;
@@ -391,6 +396,13 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
                            lz = __builtin_amdgcn_readlane(R.z0, leader);
             mine = pend && R.x0 + GROUP_R - lx <= 2u * GROUP_R && R.y0 + GROUP_R - ly <= 2u * GROUP_R &&
                    R.z0 + GROUP_R - lz <= 2u * GROUP_R;
+            /* an incoherent tile (lanes on many far-apart surfaces, e.g. a
+             * triangle soup) would need a group per few lanes: below
+             * GROUP_MIN lanes the rest scan their own cells per lane */
+            if (__builtin_popcountll(__ballot(mine)) < GROUP_MIN) {
+                direct = direct || pend;
+                break;
+            }
             union_box(g, R, mine, X0, X1, Y0, Y1, Z0, Z1);
             LY = 3u;
         }
@@ -518,9 +530,8 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
             wave_lds_sync(); /* the window is read before the next one overwrites it */
         }
     }
-    /* lanes whose radius exceeds the grid's design radius scan their own
-     * cells from global memory */
-    bool direct = R.big;
+    /* lanes whose radius exceeds the grid's design radius, and the lanes
+     * of incoherent tiles, scan their own cells from global memory */
     TILE_STAT(4, __builtin_popcountll(__ballot(direct)));
     if (NN) {
         if (fmax(fmax(dx, dy), dz) < 0x1p53) {

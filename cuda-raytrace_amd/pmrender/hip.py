@@ -78,6 +78,7 @@ def load_library(path=None):
         "pm_gather_counters": (c_int, [vp, ctypes.POINTER(i64)]),
         "pm_trace_counters": (c_int, [vp, ctypes.POINTER(i64)]),
         "pm_scene_info": (c_int, [vp, ctypes.POINTER(i64)]),
+        "pm_map_info": (c_int, [vp, ctypes.POINTER(i64)]),
         "pm_trace_profile": (c_int, [vp, ctypes.POINTER(i64), c_int]),
         "pm_set_counting": (c_int, [vp, c_int]),
         "pm_set_stage_timing": (c_int, [vp, ctypes.c_char_p]),
@@ -367,6 +368,13 @@ class Context:
         v = [int(x) for x in out]
         return {"triangles": v[0], "disks": v[1], "spheres": v[2], "bvh_nodes": v[3], "bvh_depth": v[4],
                 "mode": ("bvh-hbm", "bvh-lds", "brute")[v[5]], "bytes": v[6]}
+
+    def map_info(self):
+        """dict: structure (PM_GATHER_*, -1 none), valid photons, slots, grid cells of the current photon map."""
+        out = (ctypes.c_int64 * 4)()
+        self._chk(self.lib.pm_map_info(self.h, out))
+        v = [int(x) for x in out]
+        return {"structure": v[0], "valid": v[1], "slots": v[2], "cells": v[3]}
 
     def trace_profile(self, reset=False):
         """k_trace phase cycles (profiling builds, lib/libpmhip_prof.so): dict of summed cycles."""

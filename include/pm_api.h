@@ -293,6 +293,11 @@ int pm_trace_counters(void *ctx, int64_t out[4]);
  * [2] spheres, [3] BVH nodes, [4] BVH depth, [5] traversal mode (0 BVH in
  * HBM, 1 BVH in LDS, 2 brute force over an LDS-sized scene), [6] scene bytes */
 int pm_scene_info(void *ctx, int64_t out[7]);
+/* the current photon map (pm_build_photon_map; the reference's
+ * CreatePhotonMap, photonmappingrenderer.cpp:150-180): [0] structure
+ * (PM_GATHER_GRID / PM_GATHER_KDTREE, -1 none), [1] valid photons in it,
+ * [2] slots it was built from, [3] grid cells (0 for the kd-tree) */
+int pm_map_info(void *ctx, int64_t out[4]);
 /* Phase profile of the trace kernel, summed over waves and launches since the
  * last reset: shader-clock cycles in [0] emission, [1] BVH traversal,
  * [2] shading + bounce + deposit, [3] compaction barrier, [4] state exchange,

@@ -7,7 +7,9 @@ gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE and WRITE_SIZE are in
 KiB; FETCH_SIZE reads 1/2 of the bytes of wide coalesced reads -> doubled here
 (flagged: uncalibrated for the gather's 16-B random reads).
 
-usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON
+usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON [CONFIG]
+(the JSON records the hash of the HIP sources it was measured on: bench.py
+uses it as `traffic` only for the same sources)
 """
 import csv
 import glob
@@ -30,8 +32,8 @@ def load(d, counter):
 
 
 def short(name):
-    for k in ("k_gather_grid", "k_gather_kd", "k_trace", "k_eye", "k_grid_keys", "k_grid_scatter",
-              "k_reset_records", "k_ppm_update", "k_final"):
+    for k in ("k_gather_tile", "k_gather_grid", "k_gather_knn", "k_gather_kd", "k_trace", "k_eye", "k_bucket_fill",
+              "k_scan_down", "k_scan_reduce", "k_reset_records", "k_ppm_update", "k_final"):
         if k in name:
             return k
     return None
@@ -39,7 +41,10 @@ def short(name):
 
 def main():
     fetch, write = load(sys.argv[1], "FETCH_SIZE"), load(sys.argv[2], "WRITE_SIZE")
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernel_src_sha
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes)",
+           "kernel_src_sha": kernel_src_sha(), "config": sys.argv[4] if len(sys.argv) > 4 else "c2",
            "correction": "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halving)",
            "kernels": {}}
     agg = defaultdict(lambda: {"fetch_kib": [], "write_kib": []})
