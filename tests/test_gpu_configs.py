@@ -1,0 +1,174 @@
+"""BASELINE.json configurations and index ranges beyond the small parity
+cases, HIP path vs the CPU oracle (oracle/pm_oracle.cpp, parity unpinned —
+see DESIGN.md §4):
+
+* Halton index ranges of C4/C5 (photontracing.cu:19-31): path ranges whose
+  pm_index = 4 * path crosses 2^20, 12,582,912 (where the reference's
+  `n *= invBase` quirk stops equalling n / base) and 2^24 (where base 2
+  leaves its closed form), traced with global path ids exactly as a rank of
+  a multi-GPU run traces them — slots bit-exact;
+* point-light photon emission (cudalight.cu.h:78-88) as light 0;
+* C1 (256x256, 25,000 paths), C2 per-record PPM state at full size, C3 (1M
+  triangles, 1,048,576 paths, 1080p) and C5 (caustic scene, 4 progressive
+  passes of 1,048,576 paths at 1080p) at full size: slots / photon counts /
+  N' / r^2 exact, flux within fp32 summation order, radiance RMSE < 1e-3,
+  plus determinism and conservation properties of the full workloads."""
+import numpy as np
+import pytest
+
+from parity_util import assert_bitexact, compare_gathered_records, rmse
+from pmrender import scenes
+from pmrender.abi import PM_GATHER_GRID, PM_GATHER_KDTREE, RenderParams
+
+pytestmark = pytest.mark.gpu
+
+
+def make_pair(scene, oracle_mod, hip_mod, threads=None):
+    return scene.load_into(hip_mod.Context(0)), scene.load_into(oracle_mod.Oracle(nthreads=threads))
+
+
+@pytest.fixture(scope="module")
+def cornell_small(oracle_mod, hip_mod):
+    ctx, orc = make_pair(scenes.cornell_box(32, 32), oracle_mod, hip_mod)
+    yield ctx, orc
+    ctx.close()
+
+
+@pytest.mark.parametrize("path_begin", [262_100, 3_145_700, 4_194_270, 8_388_000])
+@pytest.mark.parametrize("pass_index", [0, 3])
+def test_halton_index_ranges(cornell_small, path_begin, pass_index):
+    """pm_index = 4 * path across 2^20 (262,144), 12,582,912 (3,145,728),
+    2^24 (4,194,304) and C5's last paths (8,388,607): GPU slots of the range
+    == oracle slots of the same global paths."""
+    ctx, orc = cornell_small
+    n = 4096
+    p = RenderParams.defaults(paths_per_pass=n)
+    ctx.trace_photons(p, pass_index, path_begin, n, slot_path_base=path_begin)
+    got = ctx.download_slots(n * 4)
+    ref = orc.trace_photons(p, pass_index, path_begin, n)
+    assert (ref["bits"] & 1).sum() > n // 2
+    assert_bitexact(got, ref, f"slots of paths [{path_begin}, {path_begin + n}) pass {pass_index}")
+
+
+def point_light_scene(W, H):
+    """The Cornell box lit by a point light (light 0) instead of the disk."""
+    s = scenes.cornell_box(W, H)
+    s.lights = [("point", np.float32([278.0, 500.0, 279.5]), np.float32([150000.0, 150000.0, 150000.0]))]
+    s.disks = []
+    return s
+
+
+@pytest.mark.parametrize("structure", [PM_GATHER_KDTREE, PM_GATHER_GRID])
+def test_point_light_emission(structure, oracle_mod, hip_mod):
+    sc = point_light_scene(64, 48)
+    ctx, orc = make_pair(sc, oracle_mod, hip_mod)
+    try:
+        p = RenderParams.defaults(paths_per_pass=16384, gather_structure=structure, initial_radius2=25.0)
+        img, st = ctx.render(p)
+        slots = ctx.download_slots(16384 * 4)
+        ref_slots = orc.trace_photons(p, 0, 0, 16384)
+        assert (ref_slots["bits"] & 1).sum() > 10000
+        assert_bitexact(slots, ref_slots, "point-light slots")
+        ref, st_ref = orc.render(p)
+        assert st["photons_valid"] == st_ref["photons_valid"]
+        assert rmse(img, ref) < 1e-3
+        if structure == PM_GATHER_KDTREE:
+            assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+    finally:
+        ctx.close()
+
+
+def stage_records(ctx, orc, p, passes=1):
+    """Per-record PPM state after `passes` passes: GPU stage API (grid) vs the
+    oracle's pbrt kd-tree passes."""
+    ctx.eye_pass(p)
+    recs = orc.eye_pass(p)
+    for k in range(passes):
+        ctx.trace_photons(p, k, 0, p.paths_per_pass)
+        ctx.build_photon_map(p, p.paths_per_pass * 4)
+        ctx.gather(p)
+        slots = orc.trace_photons(p, k, 0, p.paths_per_pass)
+        orc.gather(orc.build_kdtree(slots), recs, p)
+    return ctx.download_records(), recs
+
+
+def test_c1_full(oracle_mod, hip_mod):
+    """C1: Cornell 256x256, 100,000 slots (25,000 paths)."""
+    sc = scenes.cornell_box(256, 256)
+    ctx, orc = make_pair(sc, oracle_mod, hip_mod)
+    try:
+        p = RenderParams.defaults(paths_per_pass=25_000)
+        got, ref = stage_records(ctx, orc, p)
+        compare_gathered_records(got, ref)
+        img, st = ctx.render(p)
+        ref_img, st_ref = orc.render(p)
+        assert st["photons_valid"] == st_ref["photons_valid"] > 50_000
+        assert rmse(img, ref_img) < 1e-3
+        pk = RenderParams.defaults(paths_per_pass=25_000, gather_structure=PM_GATHER_KDTREE)
+        img_kd, _ = ctx.render(pk)
+        ref_kd, _ = orc.render(pk)
+        assert np.array_equal(img_kd.view(np.uint32), ref_kd.view(np.uint32))
+    finally:
+        ctx.close()
+
+
+def test_c2_full_records(oracle_mod, hip_mod):
+    """C2 at full size: per-record M -> N', r^2 exact, flux <= 2e-5 relative."""
+    sc = scenes.cornell_box(1920, 1080)
+    ctx, orc = make_pair(sc, oracle_mod, hip_mod)
+    try:
+        p = RenderParams.defaults()
+        got, ref = stage_records(ctx, orc, p)
+        active = (ref["photon_count"] > 0).sum()
+        assert active > 500_000
+        compare_gathered_records(got, ref)
+    finally:
+        ctx.close()
+
+
+def test_c3_full_workload(oracle_mod, hip_mod):
+    """C3: Cornell enclosure + 1M-triangle soup, 1,048,576 paths, 1080p.
+    Oracle: eye records and every photon slot bit-exact, per-record PPM
+    state after the gather; properties: two runs bit-identical, valid slots
+    == photons in the map == cell_start[ncells]."""
+    sc = scenes.triangle_soup(1_000_000, 1920, 1080)
+    ctx, orc = make_pair(sc, oracle_mod, hip_mod)
+    try:
+        assert ctx.scene_info()["mode"] == "bvh-hbm"
+        paths = 1_048_576
+        p = RenderParams.defaults(paths_per_pass=paths)
+        got, ref = stage_records(ctx, orc, p)
+        compare_gathered_records(got, ref)
+        slots = ctx.download_slots(paths * 4)
+        ref_slots = orc.trace_photons(p, 0, 0, paths)
+        assert_bitexact(slots, ref_slots, "C3 slots")
+        nvalid = int((slots["bits"] & 1).sum())
+        assert nvalid > 3_000_000
+        assert ctx.map_info()["valid"] == nvalid
+        img1, st1 = ctx.render(p)
+        img2, st2 = ctx.render(p)
+        assert st1["photons_valid"] == st2["photons_valid"] == nvalid
+        assert np.array_equal(img1.view(np.uint32), img2.view(np.uint32)), "C3 render not deterministic"
+    finally:
+        ctx.close()
+
+
+def test_c5_progressive(oracle_mod, hip_mod):
+    """C5 substitute: caustic scene (glass + mirror spheres), 1080p, 4
+    progressive passes of 1,048,576 paths (shrinking radii, PPM state carried):
+    per-record N', r^2 exact after the passes, flux within tolerance, image
+    RMSE < 1e-3."""
+    sc = scenes.caustic_scene(1920, 1080)
+    ctx, orc = make_pair(sc, oracle_mod, hip_mod)
+    try:
+        paths, passes = 1_048_576, 4
+        p = RenderParams.defaults(paths_per_pass=paths)
+        got, ref = stage_records(ctx, orc, p, passes=passes)
+        compare_gathered_records(got, ref, flux_rtol=5e-5)
+        assert (ref["photon_count"] > 0).sum() > 500_000
+        pp = RenderParams.defaults(paths_per_pass=paths, passes=passes)
+        img, st = ctx.render(pp)
+        ref_img = orc.final(ref, float(paths * passes))
+        assert rmse(img, ref_img) < 1e-3
+    finally:
+        ctx.close()
