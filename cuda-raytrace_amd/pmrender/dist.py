@@ -25,8 +25,14 @@ Two exchange strategies:
     build (which do not read records), so they overlap them; flush()
     completes the last one.
   * "allgather": the reference-style exchange: all-gather the
-    40-B photon slots into a replicated map, gather locally owned chunks.
-    Bytes per pass: 40 B x slots x (N-1)/N per rank.
+    40-B photon slots into a replicated map, gather the locally owned records:
+    the image's 8-row bands, dealt round-robin in runs (about four per rank)
+    so that every rank gets a mix of bright and dark image regions. Bytes per
+    pass: 40 B x slots x (N-1)/N per rank.
+
+Records: in "reduce" mode every rank gathers EVERY active record against its
+own photons (the gather is replicated, the photon map is not); in
+"allgather" mode the map is replicated and the records are split.
 
 The engine protocol (implemented by HipEngine below for the GPU and by the
 CPU oracle engine in tests/) works on torch tensors so that the collective
@@ -46,6 +52,61 @@ def _chunk(n, world, rank):
     return b, min(n, b + per) - b, per
 
 
+def _bands(n, unit, world, per_rank=4):
+    """Record ranges of each rank in the all-gather mode: the image's 8-row
+    bands (`unit` records each) in runs of equal size dealt round-robin, about
+    `per_rank` runs per rank — Cornell photon density is non-uniform over the
+    image, interleaving balances the gather."""
+    units = (n + unit - 1) // unit
+    runs = max(1, -(-units // (world * per_rank)))      # bands per run
+    owned = [[] for _ in range(world)]
+    k = 0
+    for u in range(0, units, runs):
+        b = u * unit
+        owned[k % world].append((b, min(n, (u + runs) * unit) - b))
+        k += 1
+    return owned
+
+
+class _AsyncExchange:
+    """The reduce exchange of one pass, one contract for every backend:
+    start() issues the count all-reduce and the flux reduce-scatter
+    asynchronously, wait() joins them — afterwards `count` holds the global
+    photon counts of every view record and `flux_chunk` this rank's slice of
+    the summed flux. The backend enters in one place: RCCL runs
+    reduce_scatter_tensor on the device tensors; gloo (the CPU tests, and
+    several ranks sharing one GPU) has no reduce-scatter, so it all-reduces
+    the flux (on host copies for device tensors) and slices at wait()."""
+
+    def __init__(self, count, flux, flux_chunk, rank, v_per):
+        self.count, self.flux, self.flux_chunk = count, flux, flux_chunk
+        self.rank, self.v_per = rank, v_per
+        self.gloo = dist.get_backend() == "gloo"
+        self.works = []
+        self.host = None
+
+    def start(self):
+        if not self.gloo:
+            self.works = [dist.all_reduce(self.count, async_op=True),
+                          dist.reduce_scatter_tensor(self.flux_chunk, self.flux, async_op=True)]
+            return self
+        count, flux = self.count, self.flux
+        if count.is_cuda:                      # gloo works on host tensors
+            count, flux = count.cpu(), flux.cpu()
+            self.host = (count, flux)
+        self.works = [dist.all_reduce(count, async_op=True), dist.all_reduce(flux, async_op=True)]
+        return self
+
+    def wait(self):
+        for w in self.works:
+            w.wait()                           # RCCL: the compute stream waits for the collectives
+        if self.gloo:
+            count, flux = self.host if self.host is not None else (self.count, self.flux)
+            if self.host is not None:
+                self.count.copy_(count)
+            self.flux_chunk.copy_(flux[self.rank * self.v_per:(self.rank + 1) * self.v_per])
+
+
 class HipEngine:
     """Adapter of hip.Context onto torch tensors; all stages run on torch's
     current stream so they are ordered with the RCCL collectives."""
@@ -59,6 +120,13 @@ class HipEngine:
 
     def num_records(self):
         return self.ctx.num_records()
+
+    def band_records(self):
+        """Records of one 8-pixel-row band: records are stored in 8x8 tiles
+        (one wave each), so a tile row is a contiguous record range."""
+        if self.ctx.pinhole:
+            return ((self.ctx.width + 7) // 8) * 64
+        return 8 * 64
 
     def alloc(self, shape, dtype):
         return torch.zeros(shape, dtype=dtype, device=self.device)
@@ -142,13 +210,16 @@ class PassRunner:
         if world > 1 and exchange == "allgather":
             self.slot_buf = engine.alloc((world * self.slots_per_rank * PHOTON_DTYPE.itemsize,), torch.uint8)
             engine.use_slot_buffer(self.slot_buf)
+            unit = engine.band_records() if hasattr(engine, "band_records") else 512
+            self.bands = _bands(n, unit, world)            # interleaved 8-row bands per rank
+            self.band_max = max(sum(c for _, c in b) for b in self.bands)
 
     @property
     def emitted_per_pass(self):
         return self.paths * self.world
 
-    # gloo (CPU tests, or several ranks sharing one GPU) has no reduce_scatter
-    # and works on host tensors: device tensors are staged through host memory
+    # gloo (CPU tests, or several ranks sharing one GPU) works on host tensors:
+    # device tensors are staged through host memory
     @staticmethod
     def _gloo():
         return dist.get_backend() == "gloo"
@@ -162,27 +233,14 @@ class PassRunner:
             dist.all_gather_into_tensor(out, mine)
 
     def _start_exchange(self):
-        if self._gloo():
-            self._pending = ("gloo", None)   # done synchronously in _finish_exchange
-        else:
-            self._pending = ("rccl", [dist.all_reduce(self.count, async_op=True),
-                                      dist.reduce_scatter_tensor(self.flux_chunk, self.flux, async_op=True)])
+        self._pending = _AsyncExchange(self.count, self.flux, self.flux_chunk, self.rank, self.v_per).start()
 
     def _finish_exchange(self):
         """Complete the previous pass: global counts -> every radius; summed flux -> owner's chunk."""
         if self._pending is None:
             return
-        kind, works = self._pending
+        self._pending.wait()
         self._pending = None
-        if kind == "gloo":                   # gloo has no reduce_scatter: all-reduce + slice, via host
-            for t in (self.count, self.flux):
-                host = t.cpu()
-                dist.all_reduce(host)
-                t.copy_(host)
-            self.flux_chunk.copy_(self.flux[self.rank * self.v_per:(self.rank + 1) * self.v_per])
-        else:
-            for w in works:
-                w.wait()                     # the compute stream waits for the collectives
         self.e.ppm_update_split(self.p, self.count, self.flux_chunk, self.v_begin, self.v_count)
 
     def flush(self):
@@ -216,7 +274,8 @@ class PassRunner:
                                  (self.rank + 1) * self.slots_per_rank * PHOTON_DTYPE.itemsize]
             self._all_gather(self.slot_buf, mine)
             e.build_photon_map(p, self.world * self.slots_per_rank)
-            e.gather_range(p, self.rec_begin, self.rec_count)   # replicated map, owned records
+            for b, c in self.bands[self.rank]:                  # replicated map, owned bands
+                e.gather_range(p, b, c)
 
     def final_gather(self, emitted, out_full):
         """Final radiance of all records (record order) on every rank."""
@@ -236,9 +295,18 @@ class PassRunner:
             out_full.zero_()
             out_full[view.long()] = gathered[: self.n_view]
             return out_full
-        mine = self.e.alloc((self.rec_per, 3), torch.float32)
-        self.e.final(emitted, self.rec_begin, self.rec_count, mine)
-        gathered = self.e.alloc((self.padded, 3), torch.float32)
+        # all-gather: each rank renders its bands; equal-size (padded) buffers
+        # are all-gathered and every rank scatters them back to record order
+        mine = self.e.alloc((self.band_max, 3), torch.float32)
+        o = 0
+        for b, c in self.bands[self.rank]:
+            self.e.final(emitted, b, c, mine[o:o + c])
+            o += c
+        gathered = self.e.alloc((self.band_max * self.world, 3), torch.float32)
         self._all_gather(gathered, mine)
-        out_full.copy_(gathered[: self.n_records])
+        for q in range(self.world):
+            o = q * self.band_max
+            for b, c in self.bands[q]:
+                out_full[b:b + c] = gathered[o:o + c]
+                o += c
         return out_full

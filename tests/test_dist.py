@@ -176,8 +176,8 @@ def _worker(rank, world, port, exchange, outdir):
     runner.final_gather(float(runner.emitted_per_pass * 2), out)
     if exchange == "reduce":   # PPM state is owned per chunk of the active-record view
         owned = eng.view[runner.v_begin:runner.v_begin + runner.v_count]
-    else:                      # per contiguous record chunk
-        owned = np.arange(runner.rec_begin, runner.rec_begin + runner.rec_count)
+    else:                      # the rank's interleaved 8-row bands
+        owned = np.concatenate([np.arange(b, b + c) for b, c in runner.bands[rank]])
     np.save(os.path.join(outdir, f"idx{rank}.npy"), owned)
     np.save(os.path.join(outdir, f"recs{rank}.npy"), eng.recs[owned])
     np.save(os.path.join(outdir, f"img{rank}.npy"), out.numpy())
@@ -226,3 +226,20 @@ def test_two_rank_pass_matches_single_process(exchange, tmp_path):
         # per-rank partial sums: exact M, flux within the fixed-point/fp32 rounding
         np.testing.assert_allclose(recs["flux"], ref_recs["flux"], rtol=1e-5, atol=1e-3)
         np.testing.assert_allclose(img, ref_img, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("n,unit,world", [(2_073_600, 240 * 64, 8), (3072, 8 * 64, 2), (100, 64, 4), (1, 512, 2)])
+def test_allgather_bands_cover_every_record_once(n, unit, world):
+    """All-gather mode ownership: 8-row bands dealt
+    round-robin in runs, about four runs per rank, every record exactly once."""
+    from pmrender.dist import _bands
+    owned = _bands(n, unit, world)
+    idx = np.concatenate([np.arange(b, b + c) for r in owned for b, c in r]) if n else np.zeros(0)
+    assert np.array_equal(np.sort(idx), np.arange(n))
+    runs = [b for r in owned for b, _ in r]
+    assert all(b % unit == 0 for b in runs)
+    if n >= unit * world * 4:
+        assert all(3 <= len(r) <= 5 for r in owned)
+        # interleaved: consecutive runs belong to consecutive ranks
+        order = sorted((b, q) for q, r in enumerate(owned) for b, _ in r)
+        assert [q for _, q in order[:world]] == list(range(world))
