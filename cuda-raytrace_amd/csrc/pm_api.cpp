@@ -108,6 +108,7 @@ struct Ctx {
     int64_t trace_wave_paths = 64; /* per-lane kernel: paths per wave (env PM_TRACE_WAVE_PATHS) */
     int trace_refill_min = 32;     /* per-lane kernel: idle lanes that trigger a refill (env PM_TRACE_REFILL_MIN) */
     bool fuse_count = true;        /* bucket counting inside the trace kernel (env PM_FUSE_COUNT=0 disables) */
+    int kd_stack = KD_STACK;        /* kd gather stack entries (env PM_KD_STACK, tests only) */
     int gather_kernel = PM_GK_TILE; /* bucket gather kernel (env PM_GATHER_KERNEL=tile|lane|wave) */
     bool gather_xcd = false;        /* tile gather: contiguous tile ranges per XCD (env PM_GATHER_XCD=1) */
     /* leading words of d_count known to be zero (the bucket scan clears the
@@ -314,6 +315,8 @@ GatherParams gather_params(Ctx *c, const pm_render_params *p) {
     G.kd_nodes = c->d_kd.as<pm_photon>(); G.kd_count = c->kd_count;
     G.counters = c->d_counters.as<unsigned long long>();
     G.kernel = c->gather_kernel;
+    G.kd_stack = c->kd_stack;
+    G.error = reinterpret_cast<unsigned int *>(c->d_counters.as<unsigned long long>() + 16);
     G.fx_nonneg = c->scene_nonneg && c->slots_nonneg ? 1 : 0;
     G.xcd = c->gather_xcd ? 1 : 0;
     if (c->view_active) { G.view_rank = c->d_vrank.as<uint32_t>(); G.view_list = c->d_vlist.as<uint32_t>(); }
@@ -420,6 +423,7 @@ int pm_create(void **out, const pm_config *cfg) {
         c->gather_kernel = !strcmp(e, "lane") ? PM_GK_LANE : !strcmp(e, "wave") ? PM_GK_WAVE : PM_GK_TILE;
     if (const char *e = getenv("PM_GATHER_WAVE")) if (atoi(e)) c->gather_kernel = PM_GK_WAVE;
     if (const char *e = getenv("PM_GATHER_XCD")) c->gather_xcd = atoi(e) != 0;
+    if (const char *e = getenv("PM_KD_STACK")) c->kd_stack = std::max(1, std::min(KD_STACK, atoi(e)));
     if (const char *e = getenv("PM_STAGE_TIMERS")) if (atoi(e) == 0) c->timed_stages.clear();
     (void)hipSetDevice(dev);
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -427,7 +431,7 @@ int pm_create(void **out, const pm_config *cfg) {
         delete c;
         FAIL((Ctx *)nullptr, PM_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
     }
-    e = c->d_counters.ensure(16 * sizeof(unsigned long long)); /* [gather x4][trace x4][trace profile x8] */
+    e = c->d_counters.ensure(17 * sizeof(unsigned long long)); /* [gather x4][trace x4][trace profile x8][gather error] */
     if (e != hipSuccess) {
         delete c;
         FAIL((Ctx *)nullptr, PM_ERR_HIP, "hipMalloc: %s", hipGetErrorString(e));
@@ -1013,9 +1017,19 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
         G.slots = c->d_slots.as<pm_photon>();
         HIPCHK(c, launch_gather_knn(G, c->counting, s));
     } else {
+        if (p->gather_structure == PM_GATHER_KDTREE) HIPCHK(c, hipMemsetAsync(G.error, 0, 4, s));
         HIPCHK(c, launch_gather(G, p->gather_structure, partial != nullptr || split, c->counting, s));
     }
     timer_end(c, "gather", s);
+    if (p->estimator != PM_ESTIMATOR_KNN && p->gather_structure == PM_GATHER_KDTREE) {
+        /* the reference's path (host kd-tree, synchronous like CreatePhotonMap):
+         * a truncated traversal is an error, not a silently darker pixel */
+        unsigned int err = 0;
+        HIPCHK(c, hipMemcpyAsync(&err, G.error, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        if (err & PM_GATHER_ERR_STACK) FAIL(c, PM_ERR_INVALID, "kd-tree gather: traversal stack of %d entries overflowed", G.kd_stack);
+        if (err & PM_GATHER_ERR_TREE) FAIL(c, PM_ERR_INVALID, "kd-tree gather: node links do not form a pbrt kd-tree");
+    }
     c->rec_estimator = p->estimator;
     if (consume) c->rec_fresh = false;
     return PM_OK;

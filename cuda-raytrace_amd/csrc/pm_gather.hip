@@ -909,8 +909,13 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_kd(GatherParams P) {
                 uint32_t nodeNum = 0;
                 stack[0] = 0; sp = 1;
                 int64_t guard = 0; /* each node is visited at most once */
+                const int stack_max = P.kd_stack < KD_STACK ? P.kd_stack : KD_STACK;
+                bool overflow = false;
                 do {
-                    if (++guard > P.kd_count || nodeNum >= (uint64_t)P.kd_count) break;
+                    if (++guard > P.kd_count || nodeNum >= (uint64_t)P.kd_count) { /* not a pbrt kd-tree */
+                        atomicOr(P.error, PM_GATHER_ERR_TREE);
+                        break;
+                    }
                     const float2 *q = reinterpret_cast<const float2 *>(P.kd_nodes + nodeNum);
                     float2 q0 = q[0], q1 = q[1];
                     uint32_t bits = (uint32_t)__float_as_int(q0.x);
@@ -929,10 +934,14 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_kd(GatherParams P) {
                         float pa = comp(p, (int)axis), na = comp(np, (int)axis);
                         float d2 = (pa - na) * (pa - na);
                         if (pa <= na) {
-                            if (d2 < maxDist2 && right < PM_PHOTON_MAX_RIGHT_CHILD && sp < KD_STACK) { stack[sp * GATHER_BLOCK] = right; ++sp; }
+                            if (d2 < maxDist2 && right < PM_PHOTON_MAX_RIGHT_CHILD) {
+                                if (sp < stack_max) { stack[sp * GATHER_BLOCK] = right; ++sp; } else overflow = true;
+                            }
                             if (hasLeft) nodeNum = nodeNum + 1; else { --sp; nodeNum = stack[sp * GATHER_BLOCK]; }
                         } else {
-                            if (d2 < maxDist2 && hasLeft && sp < KD_STACK) { stack[sp * GATHER_BLOCK] = nodeNum + 1; ++sp; }
+                            if (d2 < maxDist2 && hasLeft) {
+                                if (sp < stack_max) { stack[sp * GATHER_BLOCK] = nodeNum + 1; ++sp; } else overflow = true;
+                            }
                             if (right < PM_PHOTON_MAX_RIGHT_CHILD) nodeNum = right;
                             else { --sp; nodeNum = stack[sp * GATHER_BLOCK]; }
                         }
@@ -941,6 +950,8 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_kd(GatherParams P) {
                         nodeNum = stack[sp * GATHER_BLOCK];
                     }
                 } while (nodeNum);
+                /* a dropped subtree would silently lose photons: the launch reports it */
+                if (overflow) atomicOr(P.error, PM_GATHER_ERR_STACK);
             }
             if (COUNT) { hits += (unsigned long long)M; act++; }
             if (PARTIAL) {

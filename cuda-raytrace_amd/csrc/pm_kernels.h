@@ -36,6 +36,9 @@ constexpr int TRACE_BLOCK = 256;    /* k_trace: 4 waves compact paths together *
 constexpr int BVH_STACK = BVH_STACK_DEPTH; /* >= max BVH depth (builder enforces it) */
 constexpr int GATHER_BLOCK = 256;
 enum { PM_GK_TILE = 0, PM_GK_LANE = 1, PM_GK_WAVE = 2 };
+/* error word of a kd-tree gather: a record's traversal stack overflowed (a
+ * subtree would have been dropped), or the node links are not a pbrt tree */
+enum { PM_GATHER_ERR_STACK = 1u, PM_GATHER_ERR_TREE = 2u };
 constexpr int KD_STACK = 32;       /* >= pbrt median kd-tree depth for < 2^31 photons */
 constexpr int KNN_BLOCK = 64;      /* k_gather_knn: one wave per block, LDS heaps [K][64] */
 
@@ -109,6 +112,8 @@ struct GatherParams {
     /* kd-tree (reference layout) */
     const pm_photon *kd_nodes;
     int64_t kd_count;
+    int kd_stack;         /* traversal stack entries (<= KD_STACK; smaller only to test the overflow report) */
+    unsigned int *error;  /* PM_GATHER_ERR_* of the launch (device word, OR-ed) */
     /* fixed-point flux: contribution c -> rint(c * fx_scale), fx_inv = 1/fx_scale (2^-S) */
     float fx_scale;
     double fx_inv;

@@ -508,3 +508,30 @@ def test_knn_rejects_partial_gathers(cornell, hip_mod):
     with pytest.raises(hip_mod.PMError):
         ctx.gather(RenderParams.defaults(paths_per_pass=4096, estimator=PM_ESTIMATOR_KNN,
                                          gather_structure=PM_GATHER_KDTREE))
+
+
+def test_kd_gather_reports_stack_overflow(oracle_mod, hip_mod, monkeypatch):
+    """k_gather_kd drops no subtree silently: with a 2-entry traversal stack
+    (PM_KD_STACK, test knob) the gather fails with PM_ERR_INVALID; with the
+    default stack the same gather succeeds and matches the oracle."""
+    sc = scenes.cornell_box(32, 32)
+    orc = sc.load_into(oracle_mod.Oracle())
+    p, recs, slots = _gather_inputs(orc)
+    p.gather_structure = PM_GATHER_KDTREE
+    for stack, ok in (("2", False), ("32", True)):
+        monkeypatch.setenv("PM_KD_STACK", stack)
+        ctx = sc.load_into(hip_mod.Context(0))
+        try:
+            ctx.upload_records(recs)
+            ctx.upload_slots(slots)
+            ctx.build_photon_map(p, len(slots))
+            if ok:
+                ctx.gather(p)
+                ref = recs.copy()
+                orc.gather(oracle_mod.Oracle.build_kdtree(slots), ref, p)
+                assert_bitexact(ctx.download_records(), ref, "kd gather, default stack")
+            else:
+                with pytest.raises(hip_mod.PMError, match="stack"):
+                    ctx.gather(p)
+        finally:
+            ctx.close()
