@@ -86,6 +86,8 @@ struct Ctx {
     DevBuf d_count, d_cell_start, d_scratch, d_pha, d_phb;
     struct { bool valid = false; int64_t n = 0; GridDesc grid{}; } fused; /* counts made by the last trace */
     GridDesc grid{};
+    int64_t bvh4_nodes = 0; /* 4-wide BVH of an HBM scene (0: binary traversal) */
+    int bvh4_depth = 0;
     int map_kind = -1;
     int64_t map_slots = 0;
     /* kd-tree */
@@ -109,6 +111,8 @@ struct Ctx {
     int trace_refill_min = 32;     /* per-lane kernel: idle lanes that trigger a refill (env PM_TRACE_REFILL_MIN) */
     bool fuse_count = true;        /* bucket counting inside the trace kernel (env PM_FUSE_COUNT=0 disables) */
     int kd_stack = KD_STACK;        /* kd gather stack entries (env PM_KD_STACK, tests only) */
+    bool trace_pool = true;         /* pooled trace kernel for 4-wide BVH scenes (env PM_TRACE_POOL=0 disables) */
+    int64_t pool_waves = 8192;      /* pooled kernel: waves per launch (env PM_POOL_WAVES) */
     int gather_kernel = PM_GK_TILE; /* bucket gather kernel (env PM_GATHER_KERNEL=tile|lane|wave) */
     bool gather_xcd = false;        /* tile gather: contiguous tile ranges per XCD (env PM_GATHER_XCD=1) */
     /* leading words of d_count known to be zero (the bucket scan clears the
@@ -423,6 +427,8 @@ int pm_create(void **out, const pm_config *cfg) {
         c->gather_kernel = !strcmp(e, "lane") ? PM_GK_LANE : !strcmp(e, "wave") ? PM_GK_WAVE : PM_GK_TILE;
     if (const char *e = getenv("PM_GATHER_WAVE")) if (atoi(e)) c->gather_kernel = PM_GK_WAVE;
     if (const char *e = getenv("PM_GATHER_XCD")) c->gather_xcd = atoi(e) != 0;
+    if (const char *e = getenv("PM_TRACE_POOL")) c->trace_pool = atoi(e) != 0;
+    if (const char *e = getenv("PM_POOL_WAVES")) c->pool_waves = std::max(1LL, atoll(e));
     if (const char *e = getenv("PM_KD_STACK")) c->kd_stack = std::max(1, std::min(KD_STACK, atoi(e)));
     if (const char *e = getenv("PM_STAGE_TIMERS")) if (atoi(e) == 0) c->timed_stages.clear();
     (void)hipSetDevice(dev);
@@ -732,6 +738,26 @@ int pm_commit(void *ptr) {
     const size_t o_spheres = put(c->spheres.data(), c->spheres.size() * sizeof(float4));
     const size_t o_mats = put(c->materials.data(), c->materials.size() * sizeof(float4));
     const size_t o_lights = put(c->lights.data(), c->lights.size() * sizeof(LightDev));
+    /* scenes traversed from HBM also get the 4-wide BVH (half the dependent
+     * node fetches per ray); env PM_BVH_WIDE=0 keeps the binary traversal,
+     * PM_BVH4_LEAF sets the largest subtree folded into one leaf */
+    size_t o_wnodes = 0;
+    int wide = 0, wide_stack = 0;
+    if (blob.size() > LDS_SCENE_MAX) {
+        const char *we = getenv("PM_BVH_WIDE");
+        if (!we || atoi(we) != 0) {
+            const char *le = getenv("PM_BVH4_LEAF");
+            Bvh4Out w;
+            collapse_bvh4(bvh, le ? atoi(le) : 1, w);
+            if (w.max_stack <= BVH_STACK) {
+                o_wnodes = put(w.nodes.data(), w.nodes.size() * sizeof(float));
+                wide = 1;
+                wide_stack = w.max_stack;
+                c->bvh4_nodes = (int64_t)(w.nodes.size() / 32);
+                c->bvh4_depth = w.depth;
+            }
+        }
+    }
     blob.resize(std::max<size_t>((blob.size() + 15) & ~(size_t)15, 16), 0);
     int rc;
     if ((rc = upload(c, c->d_scene, blob))) return rc;
@@ -755,6 +781,9 @@ int pm_commit(void *ptr) {
     /* a push happens only when descending a level, so depth + 1 entries suffice;
      * sizing the LDS stack by the actual tree keeps occupancy VGPR-bound */
     S.stack_depth = std::min(BVH_STACK, std::max(2, c->bvh_depth + 2));
+    S.wide = wide;
+    S.wnodes = wide ? (const float4 *)(base + o_wnodes) : nullptr;
+    if (wide) S.stack_depth = std::min(BVH_STACK, std::max(S.stack_depth, wide_stack + 1));
     for (int a = 0; a < 3; ++a) { c->bbox_lo[a] = blo[a]; c->bbox_hi[a] = bhi[a]; }
     double em = 0.0, kd = 1.0;
     for (const LightDev &L : c->lights) {
@@ -898,6 +927,13 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
     T.path_begin = path_begin; T.path_count = path_count; T.slot_path_base = slot_path_base;
     T.per_block = c->trace_per_block;
     T.wave_paths = c->trace_wave_paths;
+    if (c->trace_pool && T.per_block == 0) {
+        /* pooled kernel: about 8192 waves (two rounds of four per SIMD), each
+         * with a contiguous pool of a multiple of 64 paths */
+        int64_t per = (path_count + c->pool_waves - 1) / c->pool_waves;
+        per = std::max<int64_t>(64, (per + 63) / 64 * 64);
+        T.pool_paths = per;
+    }
     T.refill_min = c->trace_refill_min;
     T.pass = pass; T.mpc = (int)mpc; T.max_spec = p->max_specular_depth; T.light_index = p->light_source_index;
     T.eps = p->scene_epsilon; T.seed = p->rng_seed;

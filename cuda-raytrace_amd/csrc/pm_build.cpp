@@ -135,6 +135,123 @@ struct BvhBuilder {
 
 } // namespace
 
+namespace {
+struct Bin { /* a binary-tree child: leaf (start, count) or internal node */
+    float lo[3], hi[3];
+    int code, count; /* count > 0 leaf with refs [~code, ~code + count); 0 internal */
+    float area() const {
+        const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        return dx < 0 || dy < 0 || dz < 0 ? 0.f : dx * dy + dy * dz + dz * dx;
+    }
+};
+
+struct Collapse {
+    const BvhOut &bin;
+    int leaf_prims;
+    std::vector<float> &out;
+    std::vector<int> first, total; /* per binary node: first ref, number of prims below */
+    int depth = 0;
+
+    Bin child_of(int node, int k) const {
+        const float *n = &bin.nodes[(size_t)node * 16];
+        Bin b;
+        for (int a = 0; a < 3; ++a) { b.lo[a] = n[6 * k + a]; b.hi[a] = n[6 * k + 3 + a]; }
+        int ints[4];
+        std::memcpy(ints, &n[12], sizeof(ints));
+        b.code = ints[k]; b.count = ints[2 + k];
+        return b;
+    }
+    /* prims below a binary child, and its first ref (subtrees are contiguous) */
+    void range(const Bin &b, int &f, int &t) const {
+        if (b.count > 0) { f = ~b.code; t = b.count; }
+        else if (b.count < 0) { f = 0; t = 0; }
+        else { f = first[b.code]; t = total[b.code]; }
+    }
+    void ranges(int node) {
+        int f0, t0, f1, t1;
+        for (int k = 0; k < 2; ++k) {
+            const Bin c = child_of(node, k);
+            if (c.count == 0) ranges(c.code);
+        }
+        range(child_of(node, 0), f0, t0);
+        range(child_of(node, 1), f1, t1);
+        first[node] = t0 ? (t1 ? std::min(f0, f1) : f0) : f1;
+        total[node] = t0 + t1;
+    }
+    /* a small internal subtree becomes one leaf over its contiguous refs */
+    Bin as_leaf(const Bin &b) const {
+        if (b.count != 0) return b;
+        int f, t;
+        range(b, f, t);
+        if (t > leaf_prims) return b;
+        Bin l = b;
+        l.code = ~f; l.count = t;
+        return l;
+    }
+    /* emits the 4-wide node of binary node `node`; returns (its index, stack need) */
+    int emit(int node, int level, int &need) {
+        depth = std::max(depth, level + 1);
+        std::vector<Bin> ch;
+        for (int k = 0; k < 2; ++k) {
+            Bin c = child_of(node, k);
+            if (c.count >= 0) ch.push_back(as_leaf(c));
+        }
+        while (ch.size() < 4) { /* open the largest internal child */
+            int best = -1;
+            for (size_t i = 0; i < ch.size(); ++i)
+                if (ch[i].count == 0 && (best < 0 || ch[i].area() > ch[best].area())) best = (int)i;
+            if (best < 0) break;
+            const int inner = ch[best].code;
+            ch.erase(ch.begin() + best);
+            for (int k = 0; k < 2; ++k) {
+                Bin c = child_of(inner, k);
+                if (c.count >= 0) ch.push_back(as_leaf(c));
+            }
+        }
+        const int id = (int)(out.size() / 32);
+        out.resize(out.size() + 32, 0.f);
+        int internal = 0, sub = 0;
+        int codes[4], counts[4];
+        float box[6][4];
+        for (int k = 0; k < 4; ++k) {
+            if (k < (int)ch.size()) {
+                for (int a = 0; a < 3; ++a) { box[a][k] = ch[k].lo[a]; box[3 + a][k] = ch[k].hi[a]; }
+                codes[k] = ch[k].code; counts[k] = ch[k].count;
+            } else {
+                for (int a = 0; a < 3; ++a) { box[a][k] = INFINITY; box[3 + a][k] = -INFINITY; }
+                codes[k] = 0; counts[k] = -1;
+            }
+        }
+        for (int k = 0; k < (int)ch.size(); ++k)
+            if (counts[k] == 0) {
+                int cn = 0;
+                codes[k] = emit(codes[k], level + 1, cn);
+                ++internal;
+                sub = std::max(sub, cn);
+            }
+        float *n = &out[(size_t)id * 32];
+        for (int r = 0; r < 6; ++r)
+            for (int k = 0; k < 4; ++k) n[4 * r + k] = box[r][k];
+        std::memcpy(&n[24], codes, sizeof(codes));
+        std::memcpy(&n[28], counts, sizeof(counts));
+        /* entering this node pushes all hit internal children but one */
+        need = (internal > 0 ? internal - 1 : 0) + sub;
+        return id;
+    }
+};
+} // namespace
+
+void collapse_bvh4(const BvhOut &bin, int leaf_prims, Bvh4Out &out) {
+    out.nodes.clear();
+    const size_t nn = bin.nodes.size() / 16;
+    Collapse C{bin, std::max(1, leaf_prims), out.nodes, std::vector<int>(nn, 0), std::vector<int>(nn, 0)};
+    C.ranges(0);
+    int need = 0;
+    C.emit(0, 0, need);
+    out.depth = C.depth;
+    out.max_stack = need + 1;
+}
+
 void build_bvh(std::vector<BuildPrim> &prims, int max_depth, BvhOut &out, const BvhCost &cost) {
     out.nodes.clear();
     out.refs.clear();

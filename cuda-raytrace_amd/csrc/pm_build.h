@@ -39,6 +39,22 @@ struct BvhCost {
 };
 void build_bvh(std::vector<BuildPrim> &prims, int max_depth, BvhOut &out, const BvhCost &cost = BvhCost());
 
+/* 4-wide BVH collapsed from the binary one (each node takes its binary
+ * node's children and opens the largest internal child until it has four):
+ * 32 floats = 128 B per node, one L2 line, SoA child boxes
+ *   lox[4] loy[4] loz[4] hix[4] hiy[4] hiz[4] child[4] count[4]
+ * child >= 0: internal node; child < 0: leaf, refs [~child, ~child + count);
+ * count -1: empty slot (box lo = +inf, hi = -inf). Binary subtrees of at
+ * most leaf_prims primitives become one leaf (their refs are contiguous).
+ * max_stack: entries a traversal stack needs (pushes all hit children but
+ * the nearest), so a kernel can size its LDS stack exactly. */
+struct Bvh4Out {
+    std::vector<float> nodes;
+    int depth = 0;
+    int max_stack = 0;
+};
+void collapse_bvh4(const BvhOut &bin, int leaf_prims, Bvh4Out &out);
+
 /* returns the number of nodes (= valid photons); nodes sized >= that */
 int64_t build_kdtree_pbrt(const pm_photon *slots, int64_t nslots, std::vector<pm_photon> &nodes);
 

@@ -93,6 +93,11 @@ struct SceneDev {
      * them with wave-uniform indices through the scalar cache into SGPRs */
     const float4 *tri_geo_g;
     const uint32_t *tri_id_g;
+    /* 4-wide BVH (8 float4 per node, pm_build.h collapse_bvh4) for scenes
+     * traversed from HBM (MODE_GLOBAL) when wide != 0; the binary nodes stay
+     * for the LDS modes */
+    const float4 *wnodes;
+    int wide;
     /* all arrays above are 16-B aligned sections of one blob in HBM */
     const char *blob;
     uint32_t blob_bytes;
@@ -495,6 +500,9 @@ PMD bool leaf_isect(const SceneDev &S, uint32_t start, uint32_t count, const Ray
  * Closest hit (ANY=false) or occlusion (ANY=true). Node = 4 float4:
  * (l.lo, l.hi.x) (l.hi.yz, r.lo.xy) (r.lo.z, r.hi) (left, right, lcount, rcount);
  * child >= 0 internal node, child < 0 leaf with refs start ~child. */
+template <bool ANY, class C>
+PMD bool traverse4(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int stride, C &cen);
+
 template <bool ANY, int MODE, class C>
 PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int stride, C &cen) {
     best.t = ray.tmax;
@@ -513,6 +521,9 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
         cen.node();
         if (brute_isect<ANY>(S, ray, best, cen)) return true;
         return ANY ? false : best.ref != 0xffffffffu;
+    }
+    if constexpr (MODE == MODE_GLOBAL) {
+        if (S.wide) return traverse4<ANY>(S, ray, best, stack, stride, cen);
     }
     uint32_t l0s = 0, l0n = 0, l1s = 0, l1n = 0; /* pending leaves: first ref, count (0 = none) */
     int guard = 0; /* every node is entered at most once per ray: a bound every lane reaches */
@@ -558,6 +569,134 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
     }
     return ANY ? false : best.ref != 0xffffffffu;
 }
+/* 4-wide traversal (MODE_GLOBAL scenes with S.wide): one 128-B node per
+ * visit, its four boxes tested at once; hit internal children are ordered
+ * near to far with a sorting network, the nearest entered next and the rest
+ * pushed (the stack is sized by the builder's max_stack); hit leaves are
+ * postponed and tested together as in traverse() (at most four per node). */
+template <bool ANY, class C>
+PMD bool traverse4(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int stride, C &cen) {
+    best.t = ray.tmax;
+    best.gid = 0xffffffffu;
+    best.ref = 0xffffffffu;
+    const v3 inv = safe_inv(ray.d);
+    const v3 oinv = mk(ray.o.x * inv.x, ray.o.y * inv.y, ray.o.z * inv.z);
+    int sp = 0;
+    int cur = 0;
+    uint32_t l0s = 0, l0n = 0, l1s = 0, l1n = 0, l2s = 0, l2n = 0, l3s = 0, l3n = 0;
+    int guard = 0;
+    const float INF = __int_as_float(0x7f800000);
+    while (true) {
+        while (cur >= 0 && l0n == 0 && guard <= S.n_nodes) {
+            ++guard;
+            cen.node();
+            const float4 *nd = S.wnodes + 8 * cur;
+            const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
+            const int4 ch = *reinterpret_cast<const int4 *>(nd + 6), cn = *reinterpret_cast<const int4 *>(nd + 7);
+            float t[4] = {box_near(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, oinv, inv, ray.tmin, best.t),
+                          box_near(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, oinv, inv, ray.tmin, best.t),
+                          box_near(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, oinv, inv, ray.tmin, best.t),
+                          box_near(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, oinv, inv, ray.tmin, best.t)};
+            int c[4] = {ch.x, ch.y, ch.z, ch.w};
+            const int n[4] = {cn.x, cn.y, cn.z, cn.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (t[k] != INF && n[k] > 0) { /* leaf: postpone */
+                    const uint32_t s0 = (uint32_t)~c[k], n0 = (uint32_t)n[k];
+                    if (l0n == 0) { l0s = s0; l0n = n0; }
+                    else if (l1n == 0) { l1s = s0; l1n = n0; }
+                    else if (l2n == 0) { l2s = s0; l2n = n0; }
+                    else { l3s = s0; l3n = n0; }
+                }
+                if (n[k] != 0) t[k] = INF; /* only internal children stay */
+            }
+            /* near to far: (0,1) (2,3) (0,2) (1,3) (1,2) */
+            auto cs = [&](int a, int b) {
+                if (t[b] < t[a]) { const float tt = t[a]; t[a] = t[b]; t[b] = tt; const int cc = c[a]; c[a] = c[b]; c[b] = cc; }
+            };
+            cs(0, 1); cs(2, 3); cs(0, 2); cs(1, 3); cs(1, 2);
+            if (t[3] != INF) { stack[sp * stride] = c[3]; ++sp; }
+            if (t[2] != INF) { stack[sp * stride] = c[2]; ++sp; }
+            if (t[1] != INF) { stack[sp * stride] = c[1]; ++sp; }
+            if (t[0] != INF) cur = c[0];
+            else if (sp > 0) { --sp; cur = stack[sp * stride]; }
+            else cur = -1;
+        }
+        while (l0n != 0) {
+            if (leaf_isect<ANY>(S, l0s, l0n, ray, best, cen)) return true;
+            l0s = l1s; l0n = l1n; l1s = l2s; l1n = l2n; l2s = l3s; l2n = l3n; l3n = 0;
+        }
+        if (cur < 0 || guard > S.n_nodes) break;
+    }
+    return ANY ? false : best.ref != 0xffffffffu;
+}
+
+/* Resumable closest-hit traversal of the 4-wide BVH for kernels that keep a
+ * ray's traversal alive across iterations of an outer loop (k_trace_pool):
+ * trav_step advances by one node visit or one leaf; the result equals
+ * traverse4's (same culling, same leaf tests, same tie-break). */
+struct TravState {
+    v3 inv, oinv;
+    Hit best;
+    int cur, sp, guard;
+    uint32_t l0s, l0n, l1s, l1n, l2s, l2n, l3s, l3n;
+};
+PMD void trav_begin(const Ray &ray, TravState &t) {
+    t.best.t = ray.tmax;
+    t.best.gid = 0xffffffffu;
+    t.best.ref = 0xffffffffu;
+    t.best.beta = t.best.gamma = 0.f;
+    t.inv = safe_inv(ray.d);
+    t.oinv = mk(ray.o.x * t.inv.x, ray.o.y * t.inv.y, ray.o.z * t.inv.z);
+    t.cur = 0; t.sp = 0; t.guard = 0;
+    t.l0n = t.l1n = t.l2n = t.l3n = 0;
+    t.l0s = t.l1s = t.l2s = t.l3s = 0;
+}
+/* false once the ray is done (best holds its closest hit, if any) */
+template <class C>
+PMD bool trav_step(const SceneDev &S, const Ray &ray, TravState &T, int *stack, int stride, C &cen) {
+    if (T.l0n != 0) {
+        leaf_isect<false>(S, T.l0s, T.l0n, ray, T.best, cen);
+        T.l0s = T.l1s; T.l0n = T.l1n; T.l1s = T.l2s; T.l1n = T.l2n; T.l2s = T.l3s; T.l2n = T.l3n; T.l3n = 0;
+        return T.l0n != 0 || T.cur >= 0;
+    }
+    if (T.cur < 0 || T.guard > S.n_nodes) return false;
+    ++T.guard;
+    cen.node();
+    const float INF = __int_as_float(0x7f800000);
+    const float4 *nd = S.wnodes + 8 * T.cur;
+    const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
+    const int4 ch = *reinterpret_cast<const int4 *>(nd + 6), cn = *reinterpret_cast<const int4 *>(nd + 7);
+    float t[4] = {box_near(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, T.oinv, T.inv, ray.tmin, T.best.t),
+                  box_near(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, T.oinv, T.inv, ray.tmin, T.best.t),
+                  box_near(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, T.oinv, T.inv, ray.tmin, T.best.t),
+                  box_near(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, T.oinv, T.inv, ray.tmin, T.best.t)};
+    int c[4] = {ch.x, ch.y, ch.z, ch.w};
+    const int n[4] = {cn.x, cn.y, cn.z, cn.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (t[k] != INF && n[k] > 0) {
+            const uint32_t s0 = (uint32_t)~c[k], n0 = (uint32_t)n[k];
+            if (T.l0n == 0) { T.l0s = s0; T.l0n = n0; }
+            else if (T.l1n == 0) { T.l1s = s0; T.l1n = n0; }
+            else if (T.l2n == 0) { T.l2s = s0; T.l2n = n0; }
+            else { T.l3s = s0; T.l3n = n0; }
+        }
+        if (n[k] != 0) t[k] = INF;
+    }
+    auto cs = [&](int a, int b) {
+        if (t[b] < t[a]) { const float tt = t[a]; t[a] = t[b]; t[b] = tt; const int cc = c[a]; c[a] = c[b]; c[b] = cc; }
+    };
+    cs(0, 1); cs(2, 3); cs(0, 2); cs(1, 3); cs(1, 2);
+    if (t[3] != INF) { stack[T.sp * stride] = c[3]; ++T.sp; }
+    if (t[2] != INF) { stack[T.sp * stride] = c[2]; ++T.sp; }
+    if (t[1] != INF) { stack[T.sp * stride] = c[1]; ++T.sp; }
+    if (t[0] != INF) T.cur = c[0];
+    else if (T.sp > 0) { --T.sp; T.cur = stack[T.sp * stride]; }
+    else T.cur = -1;
+    return T.l0n != 0 || T.cur >= 0;
+}
+
 template <bool ANY, int MODE>
 PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int stride) {
     NoCensus none;

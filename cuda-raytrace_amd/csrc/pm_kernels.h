@@ -87,6 +87,7 @@ struct TraceParams {
     int64_t per_block;  /* > 0: block-compacting kernel, paths per block pool; 0: per-lane kernel */
     int64_t wave_paths; /* per-lane kernel: paths per wave pool (>= 64; 64 = no refills) */
     int refill_min;     /* per-lane kernel: refill when at least this many lanes are idle */
+    int64_t pool_paths; /* > 0: pooled kernel (k_trace_pool, 4-wide BVH scenes), paths per wave */
     int pass, mpc, max_spec, light_index;
     float eps;
     uint32_t seed;

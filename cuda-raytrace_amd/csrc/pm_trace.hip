@@ -306,13 +306,21 @@ PMD bool emit_path(const TraceParams &P, const SceneDev &S, const uint32_t *perm
 
 /* one ray of a path: trace, then specular continuation or diffuse deposit +
  * Lambert bounce (photontracing.cu:119-183); false when the path ends */
+PMD bool path_shade(const TraceParams &P, const SceneDev &S, PathState &st, const Hit &h, TProf &prof);
+
 template <int MODE, class C>
 PMD bool path_step(const TraceParams &P, const SceneDev &S, int *stack, PathState &st, C &cen, TProf &prof) {
-    const uint32_t mpc = (uint32_t)P.mpc;
     Hit h;
     const bool hit = traverse<false, MODE>(S, st.ray, h, stack, TRACE_BLOCK, cen);
     prof.mark(1);
     if (!hit) return false;
+    return path_shade(P, S, st, h, prof);
+}
+
+/* the hit of a path's ray: specular continuation, or diffuse deposit +
+ * Lambert bounce (photontracing.cu:119-183); false when the path ends */
+PMD bool path_shade(const TraceParams &P, const SceneDev &S, PathState &st, const Hit &h, TProf &prof) {
+    const uint32_t mpc = (uint32_t)P.mpc;
     Geo g = shade(S, st.ray, h);
     v3 hit_point = st.ray.o + h.t * st.ray.d;
     float4 m = S.materials[g.material];
@@ -539,6 +547,91 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
     }
 }
 
+/* Pooled photon tracer for scenes traversed from HBM with the 4-wide BVH
+ * (C3). A ray's traversal lives across iterations of the wave's loop
+ * (TravState: node, stack in LDS, pending leaves, best hit), so lanes whose
+ * ray ended do not idle until the wave's longest ray ends: they wait until
+ * at least POOL_SHADE_MIN lanes are ready (or nothing traverses), then those
+ * lanes shade their hits together (deposit / bounce -> next ray) and lanes
+ * without a path take the next ones of the wave's pool [wbegin, wend). The
+ * rest of the time every iteration runs POOL_STEPS traversal steps for the
+ * traversing lanes. Paths, slots and bucket counts are the per-lane
+ * kernel's (owner-writes; the fused bucket ranks' order is immaterial). */
+#ifndef PM_POOL_SHADE_MIN
+#define PM_POOL_SHADE_MIN 16
+#endif
+constexpr int POOL_STEPS = 4, POOL_SHADE_MIN = PM_POOL_SHADE_MIN;
+enum { PHASE_DEAD = 0, PHASE_TRAV = 1, PHASE_SHADE = 2 };
+
+template <int COUNT>
+#ifdef PM_POOL_WAVES_EU
+__global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(PM_POOL_WAVES_EU))) void k_trace_pool(TraceParams P) {
+#else
+__global__ __launch_bounds__(TRACE_BLOCK) void k_trace_pool(TraceParams P) {
+#endif
+    extern __shared__ __attribute__((aligned(16))) int stk[];
+    __shared__ uint32_t perm[28];
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (tid < 28) perm[tid] = P.perm[tid];
+    const SceneDev &S = P.S;
+    __syncthreads();
+    int *stack = stk + tid;
+    typename std::conditional<COUNT != 0, Census, NoCensus>::type cen;
+    TProf prof;
+    uint32_t rays = 0, deposits = 0;
+    const int64_t wave_id = ((int64_t)blockIdx.x * TRACE_BLOCK + tid) >> 6;
+    const int64_t wbegin = wave_id * P.wave_paths;
+    const int64_t wend = wbegin + P.wave_paths < P.path_count ? wbegin + P.wave_paths : P.path_count;
+    int64_t cursor = wbegin; /* wave-uniform: next unassigned path of the pool */
+    PathState st;
+    TravState tr;
+    int phase = PHASE_DEAD;
+    while (true) {
+        const unsigned long long travm = __ballot(phase == PHASE_TRAV);
+        const unsigned long long shadem = __ballot(phase == PHASE_SHADE);
+        const unsigned long long deadm = __ballot(phase == PHASE_DEAD);
+        const bool pool_left = cursor < wend;
+        if (travm == 0ull && shadem == 0ull && !pool_left) break; /* every lane reaches it together */
+        const int waiting = __popcll(shadem) + (pool_left ? __popcll(deadm) : 0);
+        if (travm == 0ull || waiting >= POOL_SHADE_MIN) {
+            if (phase == PHASE_SHADE) {
+                ++rays;
+                bool alive = tr.best.ref != 0xffffffffu && path_shade(P, S, st, tr.best, prof);
+                if (alive) {
+                    trav_begin(st.ray, tr);
+                    phase = PHASE_TRAV;
+                } else {
+                    if (COUNT) deposits += st.stored;
+                    finish_path(P, st);
+                    phase = PHASE_DEAD;
+                }
+            }
+            const unsigned long long dm = __ballot(phase == PHASE_DEAD);
+            if (cursor < wend) {
+                const int64_t mine = cursor + __popcll(dm & ((1ull << lane) - 1ull));
+                if (phase == PHASE_DEAD && mine < wend) {
+                    if (emit_path(P, S, perm, (uint32_t)(P.path_begin + mine), st)) {
+                        trav_begin(st.ray, tr);
+                        phase = PHASE_TRAV;
+                    } else {
+                        finish_path(P, st);
+                    }
+                }
+                cursor = cursor + __popcll(dm) < wend ? cursor + __popcll(dm) : wend;
+            }
+            continue;
+        }
+#pragma unroll 1
+        for (int k = 0; k < POOL_STEPS; ++k)
+            if (phase == PHASE_TRAV && !trav_step(S, st.ray, tr, stack, TRACE_BLOCK, cen)) phase = PHASE_SHADE;
+    }
+    if (COUNT) {
+        uint32_t nodes = 0, prims = 0;
+        if constexpr (COUNT != 0) { nodes = cen.nodes; prims = cen.prims; }
+        count4(P.counters, rays, nodes, prims, deposits);
+    }
+}
+
 #define PM_LAUNCH_MODES(KERNEL, GRID, BLOCK, LDS, STREAM, PARAMS, COUNT)                                        \
     switch (scene_mode((PARAMS).S)) {                                                                            \
     case MODE_BRUTE:                                                                                             \
@@ -558,6 +651,15 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
 hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s) {
     if (p.path_count <= 0) return hipSuccess;
     const size_t lds = (size_t)p.S.stack_depth * TRACE_BLOCK * 4 + p.S.lds_bytes;
+    if (p.pool_paths > 0 && scene_mode(p.S) == MODE_GLOBAL && p.S.wide) {
+        TraceParams q = p;
+        q.wave_paths = p.pool_paths;
+        const int64_t waves = (p.path_count + q.wave_paths - 1) / q.wave_paths;
+        const unsigned grid = (unsigned)((waves + TRACE_BLOCK / 64 - 1) / (TRACE_BLOCK / 64));
+        if (count) pm_launch(k_trace_pool<1>, dim3(grid), dim3(TRACE_BLOCK), lds, s, q);
+        else pm_launch(k_trace_pool<0>, dim3(grid), dim3(TRACE_BLOCK), lds, s, q);
+        return hipGetLastError();
+    }
     if (p.per_block == 0) {
         if (p.wave_paths < 64 || p.refill_min < 1) return hipErrorInvalidValue;
         const int64_t waves = (p.path_count + p.wave_paths - 1) / p.wave_paths;
