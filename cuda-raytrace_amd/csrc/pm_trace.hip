@@ -564,11 +564,7 @@ constexpr int POOL_STEPS = 4, POOL_SHADE_MIN = PM_POOL_SHADE_MIN;
 enum { PHASE_DEAD = 0, PHASE_TRAV = 1, PHASE_SHADE = 2 };
 
 template <int COUNT>
-#ifdef PM_POOL_WAVES_EU
-__global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(PM_POOL_WAVES_EU))) void k_trace_pool(TraceParams P) {
-#else
-__global__ __launch_bounds__(TRACE_BLOCK) void k_trace_pool(TraceParams P) {
-#endif
+__global__ __launch_bounds__(TRACE_BLOCK) void k_trace_pool(TraceParams P) { /* 122 VGPRs: 4 waves/SIMD (5 spill: slower) */
     extern __shared__ __attribute__((aligned(16))) int stk[];
     __shared__ uint32_t perm[28];
     const int tid = threadIdx.x, lane = tid & 63;
