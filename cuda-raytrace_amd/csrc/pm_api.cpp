@@ -112,7 +112,7 @@ struct Ctx {
     bool fuse_count = true;        /* bucket counting inside the trace kernel (env PM_FUSE_COUNT=0 disables) */
     int kd_stack = KD_STACK;        /* kd gather stack entries (env PM_KD_STACK, tests only) */
     bool trace_pool = true;         /* pooled trace kernel for 4-wide BVH scenes (env PM_TRACE_POOL=0 disables) */
-    int64_t pool_waves = 8192;      /* pooled kernel: waves per launch (env PM_POOL_WAVES) */
+    int64_t pool_waves = 0;         /* pooled kernel: waves per launch (env PM_POOL_WAVES; 0 = one occupancy round) */
     int gather_kernel = PM_GK_TILE; /* bucket gather kernel (env PM_GATHER_KERNEL=tile|lane|wave) */
     bool gather_xcd = false;        /* tile gather: contiguous tile ranges per XCD (env PM_GATHER_XCD=1) */
     /* leading words of d_count known to be zero (the bucket scan clears the
@@ -928,9 +928,17 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
     T.per_block = c->trace_per_block;
     T.wave_paths = c->trace_wave_paths;
     if (c->trace_pool && T.per_block == 0) {
-        /* pooled kernel: about 8192 waves (two rounds of four per SIMD), each
-         * with a contiguous pool of a multiple of 64 paths */
-        int64_t per = (path_count + c->pool_waves - 1) / c->pool_waves;
+        /* pooled kernel: one occupancy round — 4 waves per SIMD (122 VGPRs),
+         * 4 SIMDs per CU — each wave with a contiguous pool of a multiple of
+         * 64 paths. C3 sweep (1M paths, 256 CUs): 4096 waves 5.25 ms, 8192
+         * (two rounds) 5.81, 5462 (1.33 rounds) 6.73, 2048 7.22 */
+        int64_t waves = c->pool_waves;
+        if (waves <= 0) {
+            int cus = 0;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0) cus = 256;
+            waves = (int64_t)cus * 16;
+        }
+        int64_t per = (path_count + waves - 1) / waves;
         per = std::max<int64_t>(64, (per + 63) / 64 * 64);
         T.pool_paths = per;
     }
@@ -1046,10 +1054,11 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
     if (p->estimator == PM_ESTIMATOR_KNN) {
         G.knn_k = p->knn_lookup;
         G.knn_r2 = p->initial_radius2; /* pbrt's maxDistSquared: the buckets cover it */
-        /* every term (kernel <= 3/pi < 1) is <= alpha_max / r_k^2: 2^50 of the
-         * per-record scale per term, 64 terms fit an int64 */
+        /* every term (kernel <= 3/pi < 1) is <= alpha_max / r_k^2: 2^47 of the
+         * per-record scale per term, and <= PM_KNN_MAX = 2^6 terms sum below
+         * 2^53 — exact in double */
         const double amax = c->emit_max * std::pow(c->kd_max, (double)p->max_photon_count) * 4.0;
-        G.knn_fx = (float)(std::ldexp(1.0, 50) / std::max(amax, 1e-30));
+        G.knn_fx = (float)(std::ldexp(1.0, 47) / std::max(amax, 1e-30));
         G.slots = c->d_slots.as<pm_photon>();
         HIPCHK(c, launch_gather_knn(G, c->counting, s));
     } else {

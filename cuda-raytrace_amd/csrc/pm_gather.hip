@@ -9,6 +9,8 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "pm_kernels.h"
 
 #pragma clang fp contract(off)
@@ -324,20 +326,24 @@ PMD long long d2ll(double d) {
 #define TILE_OCC
 #endif
 /* the cell box [X0, X1] x [Y0, Y1] x [Z0, Z1] of the lanes with `in` set */
-PMD void union_box(const GridDesc &g, const GatherRec &R, bool in, uint32_t &X0, uint32_t &X1, uint32_t &Y0,
-                   uint32_t &Y1, uint32_t &Z0, uint32_t &Z1) {
+PMD void union_box6(const GridDesc &g, bool in, uint32_t x0, uint32_t x1, uint32_t y0, uint32_t y1, uint32_t z0,
+                    uint32_t z1, uint32_t &X0, uint32_t &X1, uint32_t &Y0, uint32_t &Y1, uint32_t &Z0, uint32_t &Z1) {
     if (g.dx < 65536 && g.dy < 65536 && g.dz < 65536) {
         /* three packed 16-bit minima (maxima as minima of 0xffff - c) */
-        const uint32_t m0 = wave_min_2x16(in ? (R.x0 << 16) | R.y0 : 0xffffffffu);
-        const uint32_t m1 = wave_min_2x16(in ? ((0xffffu - R.x1) << 16) | (0xffffu - R.y1) : 0xffffffffu);
-        const uint32_t m2 = wave_min_2x16(in ? (R.z0 << 16) | (0xffffu - R.z1) : 0xffffffffu);
+        const uint32_t m0 = wave_min_2x16(in ? (x0 << 16) | y0 : 0xffffffffu);
+        const uint32_t m1 = wave_min_2x16(in ? ((0xffffu - x1) << 16) | (0xffffu - y1) : 0xffffffffu);
+        const uint32_t m2 = wave_min_2x16(in ? (z0 << 16) | (0xffffu - z1) : 0xffffffffu);
         X0 = m0 >> 16; Y0 = m0 & 0xffffu; X1 = 0xffffu - (m1 >> 16); Y1 = 0xffffu - (m1 & 0xffffu);
         Z0 = m2 >> 16; Z1 = 0xffffu - (m2 & 0xffffu);
     } else {
-        X0 = wave_min_u32(in ? R.x0 : 0xffffffffu); X1 = wave_max_u32(in ? R.x1 : 0u);
-        Y0 = wave_min_u32(in ? R.y0 : 0xffffffffu); Y1 = wave_max_u32(in ? R.y1 : 0u);
-        Z0 = wave_min_u32(in ? R.z0 : 0xffffffffu); Z1 = wave_max_u32(in ? R.z1 : 0u);
+        X0 = wave_min_u32(in ? x0 : 0xffffffffu); X1 = wave_max_u32(in ? x1 : 0u);
+        Y0 = wave_min_u32(in ? y0 : 0xffffffffu); Y1 = wave_max_u32(in ? y1 : 0u);
+        Z0 = wave_min_u32(in ? z0 : 0xffffffffu); Z1 = wave_max_u32(in ? z1 : 0u);
     }
+}
+PMD void union_box(const GridDesc &g, const GatherRec &R, bool in, uint32_t &X0, uint32_t &X1, uint32_t &Y0,
+                   uint32_t &Y1, uint32_t &Z0, uint32_t &Z1) {
+    union_box6(g, in, R.x0, R.x1, R.y0, R.y1, R.z0, R.z1, X0, X1, Y0, Y1, Z0, Z1);
 }
 #ifndef PM_GROUP_R
 #define PM_GROUP_R 3
@@ -683,13 +689,32 @@ __global__ __launch_bounds__(GATHER_BLOCK, 8) void k_gather_wave(GatherParams P)
  * entry, LDS columns [K][64]) finds r_k^2; (2) a rescan bounded by r_k^2 sums
  * the photons with d^2 < r_k^2 and, of those at exactly r_k^2, the lowest
  * slots (slot ids ride in ph_b; a third scan runs only when more ties than
- * places exist). The sum is exact and order-free in int64 fixed point
- * (scale: the power of two below knn_fx * r_k^2, every term being
- * <= alpha_max / r_k^2). Fused record update: flux += S, radius2 = r_k^2,
+ * places exist). The sum is exact and order-free: integer-valued terms
+ * in the record's fixed point (scale: the power of two below knn_fx * r_k^2,
+ * every term <= 2^47) added in double (Dx3). Fused record update: flux += S, radius2 = r_k^2,
  * photon_count = found; the final pass applies 1/paths and rho/pi = Kd/pi
  * (k_final). Both passes visit rows in rings around the query's row,
  * nearest first, and skip rows / cells beyond the current bound. */
 PMD float sq(float x) { return x * x; }
+/* kNN sums: each term rint(c * sc) is an integer-valued float <= 2^47
+ * (knn_fx), at most PM_KNN_MAX = 2^6 of them per record, so their double sum
+ * is exact (< 2^53): order-free like the PPM gather's int64 fixed point, at
+ * one conversion and one add per channel */
+struct Dx3 { double x, y, z; };
+/* Dot(Faceforward(ns, wo), wi) > 0 for the photon's wi = (wx, b.w, wz) */
+PMD bool knn_facing(v3 ns, bool back, const float4 &b, float wx, float wz) {
+    float dn = dot(ns, mk(wx, b.w, wz));
+    if (back) dn = -dn;
+    return dn > 0.f;
+}
+/* pbrt kernel() 3/pi (1 - d^2/r_k^2)^2 / r_k^2 times alpha, inv = 1/r_k^2,
+ * in the record's fixed point sc */
+PMD void knn_add(Dx3 &a, float d2, float inv, float sc, const float4 &b) {
+    const float s = 1.f - d2 * inv;
+    const float kk = 3.f * INV_PI * s * s;
+    const v3 c = (kk * inv) * xyz(b);
+    a.x += (double)rintf(c.x * sc); a.y += (double)rintf(c.y * sc); a.z += (double)rintf(c.z * sc);
+}
 /* distance, in cell units, from coordinate u (cell units) to cell c of an
  * axis with dim cells — the border cells extend to infinity (cell_axis
  * clamps) — less a 1e-3 margin that covers the float rounding of u and of the
@@ -731,12 +756,12 @@ PMD void heap_replace_top(uint32_t *h, int n, uint32_t d) {
  * (in world units^2) is re-read per row; visit(j, d2) per photon of the kept
  * cells. Returns nothing; COUNT census through vis / rows. */
 struct KnnGrid {
-    const GridDesc *g;
+    GridDesc g; /* a copy: a pointer into the kernel arguments would force them into scratch */
     uint32_t x0, x1, y0, y1, z0, z1;
     int cyc, czc, rings;
     float ux, uy, uz, inv2;
     PMD void init(const GridDesc &G, v3 p, float maxd2) {
-        g = &G;
+        g = G;
         const float rq = sqrtf(maxd2) * 1.0001f + 1e-4f;
         x0 = cell_axis(p.x - rq, G.gx, G.inv_cs, G.dx); x1 = cell_axis(p.x + rq, G.gx, G.inv_cs, G.dx);
         y0 = cell_axis(p.y - rq, G.gy, G.inv_cs, G.dy); y1 = cell_axis(p.y + rq, G.gy, G.inv_cs, G.dy);
@@ -754,14 +779,14 @@ struct KnnGrid {
             for (uint32_t cz = z0; cz <= z1; ++cz)
                 for (uint32_t cy = y0; cy <= y1; ++cy) {
                     if (max(abs((int)cy - cyc), abs((int)cz - czc)) != ring) continue;
-                    const float gy = cell_gap(uy, cy, g->dy), gz = cell_gap(uz, cz, g->dz);
+                    const float gy = cell_gap(uy, cy, g.dy), gz = cell_gap(uz, cz, g.dz);
                     const float lim = bound() * inv2 - (gy * gy + gz * gz);
                     if (lim < 0.f) continue;
                     uint32_t xa = x0, xb = x1;
-                    while (xa <= xb && sq(cell_gap(ux, xa, g->dx)) > lim) ++xa;
-                    while (xb > xa && sq(cell_gap(ux, xb, g->dx)) > lim) --xb;
+                    while (xa <= xb && sq(cell_gap(ux, xa, g.dx)) > lim) ++xa;
+                    while (xb > xa && sq(cell_gap(ux, xb, g.dx)) > lim) --xb;
                     if (xa > xb) continue;
-                    const uint32_t row = (cz * (uint32_t)g->dy + cy) * (uint32_t)g->dx;
+                    const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
                     const uint32_t b = cell_start[row + xa], e = cell_start[row + xb + 1];
                     vis += e - b; rows++;
                     for (uint32_t j = b; j < e; ++j) {
@@ -791,7 +816,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn(GatherParams P) {
             const v3 p = xyz(pos), ns = xyz(nrm);
             int cnt = 0;
             float md2 = maxd2;
-            Fx3 acc{0, 0, 0};
+            Dx3 acc{0, 0, 0};
             float sc = 1.f;
             bool nan = false;
             if (__float_as_int(m.w) == PM_MATTE) { /* non-specular BSDF components only */
@@ -817,21 +842,17 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn(GatherParams P) {
                 const bool back = (flags & PM_REC_BACKFACE) != 0;
                 const float *phb = reinterpret_cast<const float *>(P.ph_b);
                 /* contribution of photon j (LPhoton term) into a */
-                auto add = [&](Fx3 &a, uint32_t j, const float4 &pa, float d2) {
+                const float inv = 1.f / md2;
+                auto add = [&](Dx3 &a, uint32_t j, const float4 &pa, float d2) {
                     const float4 b0 = P.ph_b[2 * (size_t)j];
-                    float dn = dot(ns, mk(pa.w, b0.w, phb[8 * (size_t)j + 4]));
-                    if (back) dn = -dn; /* Dot(Faceforward(ns, wo), wi) */
-                    if (!(dn > 0.f)) return;
+                    if (!knn_facing(ns, back, b0, pa.w, phb[8 * (size_t)j + 4])) return;
                     if (md2 == 0.f) { nan = true; return; } /* K photons at distance 0: kernel() is 0/0 */
-                    const float s = 1.f - d2 / md2;
-                    const float kk = 3.f * INV_PI * s * s;
-                    const v3 c = (kk / md2) * xyz(b0);
-                    a.x += to_fx(c.x, sc); a.y += to_fx(c.y, sc); a.z += to_fx(c.z, sc);
+                    knn_add(a, d2, inv, sc, b0);
                 };
                 /* pass 2: every photon below r_k^2 (all below maxD2 when not full);
                  * ties at r_k^2 aside */
                 int less = 0, ties = 0;
-                Fx3 acc_eq{0, 0, 0};
+                Dx3 acc_eq{0, 0, 0};
                 G.scan(P.cell_start, P.ph_a, p, [&]() { return md2; },
                        [&](uint32_t j, const float4 &pa, float d2) {
                            if (d2 < md2) { less++; add(acc, j, pa, d2); }
@@ -861,8 +882,8 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn(GatherParams P) {
                 cnt = full ? K : less;
             }
             if (COUNT) { hits += (unsigned long long)cnt; act++; }
-            const double inv = 1.0 / (double)sc;
-            v3 L = mk((float)((double)acc.x * inv), (float)((double)acc.y * inv), (float)((double)acc.z * inv));
+            const double isc = 1.0 / (double)sc;
+            v3 L = mk((float)(acc.x * isc), (float)(acc.y * isc), (float)(acc.z * isc));
             if (nan) L = mk(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
             const v3 flux = xyz(st) + L;
             P.R.state[r] = make_float4(flux.x, flux.y, flux.z, md2);
@@ -872,10 +893,485 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn(GatherParams P) {
     if (COUNT) count4(P.counters, vis, hits, rows, act);
 }
 
+/* ---------------------------------------------------------------------- */
+/* kNN tile kernel (default kNN path): k_gather_knn's estimate, bit for bit
+ * (same found set, r_k^2, per-record scale and exact sums), for the 64
+ * records of an 8x8 tile at once.
+ *  - Photon source: the wave stages the union of its lanes' bucket rows (each
+ *    lane's box [p - maxD, p + maxD]) into LDS windows of KT_CAP photons with
+ *    coalesced loads, as k_gather_tile does; every lane tests every staged
+ *    photon against its own d^2 interval. The union is a superset of each
+ *    lane's cells and anything at d^2 >= maxD^2 is dropped, so the found set
+ *    is unchanged, and the scan loop is wave-uniform instead of 64 lanes
+ *    walking their own rows with a divergent heap.
+ *  - r_k^2 without a heap: the K-th smallest d^2 is selected exactly by
+ *    passes over the same photons. HIST counts each lane's photons of its
+ *    interval into 32 bins of a monotone bin function (float subtract,
+ *    multiply, clamp, truncate: every step is monotone, so a bin is an
+ *    interval of d^2 values) with one LDS add per photon; a prefix walk finds
+ *    the bin holding the K-th. COLLECT then keeps that bin's values (<= 8, in
+ *    LDS) with their min and max: <= 8 values are ranked directly, equal
+ *    values are the answer, otherwise [min, max] is re-binned (the extremes
+ *    land in bins 0 and 31, so every level shrinks the set). A deep or
+ *    overflowing (>= 2^16 photons) search extracts minima one by one instead.
+ *    A record with < K photons inside maxD (r_k^2 = maxD^2) goes from level
+ *    0's HIST straight to its SUM pass.
+ *  - HIST counts inline in the test loop (no per-hit loop); COLLECT, MIN and
+ *    SUM lanes take their hits one per lane per iteration, COLLECT over the
+ *    chosen bin's d^2 range only (conservative float bounds, exact bin test).
+ *  - Incoherent tiles: k_gather_tile's groups (leader neighbourhoods); lanes
+ *    left over in groups of < KT_GROUP_MIN run the same passes over their own
+ *    rows from global memory. */
+#ifndef PM_KT_CAP
+#define PM_KT_CAP 64
+#endif
+#ifndef PM_KT_GROUP_MIN
+#define PM_KT_GROUP_MIN 12
+#endif
+constexpr int KT_CAP = PM_KT_CAP;  /* photons per LDS window (one per lane) */
+#ifndef PM_KT_BINS
+#define PM_KT_BINS 64
+#endif
+constexpr int KT_BINS = PM_KT_BINS; /* histogram bins per pass */
+constexpr int KT_LIST = 8;         /* values a COLLECT pass keeps per lane */
+constexpr int KT_LEVELS = 4;       /* re-binning levels before minimum extraction */
+constexpr uint32_t KT_GROUP_R = 1; /* lane boxes span <= 5 cells: a group's union <= 7 per axis */
+constexpr int KT_GROUP_MIN = PM_KT_GROUP_MIN;
+struct KnnLds {
+    float x[KT_CAP + 4], y[KT_CAP + 4], z[KT_CAP + 4]; /* +4: the pair test reads one past the window */
+    float4 b[KT_CAP];                                   /* alpha.rgb, wi.y */
+    float w[KT_CAP], c[KT_CAP];                         /* wi.x, wi.z */
+    int mark[KT_CAP];
+    uint32_t hist[KT_BINS / 2][64]; /* two 16-bit counters per word, a column per lane */
+    uint32_t list[KT_LIST][64];
+};
+#define PM_INLINE __attribute__((always_inline))
+enum { KP_DONE = 0, KP_HIST = 1, KP_COLLECT = 2, KP_MIN = 3, KP_SUM = 4 };
+PMD float next_up(float x) { return __uint_as_float(__float_as_uint(x) + 1u); } /* x >= 0, finite */
+/* per-record fixed-point scale: the power of two below knn_fx * r_k^2 */
+PMD float knn_scale(float fx, float md2) {
+    return md2 == 0.f ? 1.f : __uint_as_float(__float_as_uint(fx * md2) & 0xff800000u);
+}
+/* one lane's selection state */
+struct KnnSel {
+    int phase = KP_DONE, level = 0, need = 0, kbin = 0;
+    float blo = INFINITY, bhi = 0.f; /* this pass's hit interval [blo, bhi) */
+    float lo = 0.f, s = 0.f;         /* bin function of HIST / COLLECT */
+    uint32_t cntf = 0, cc = 0, tcnt = 0;
+    float mn = INFINITY, mx = 0.f, tmin = INFINITY;
+    float md2 = 0.f, sc = 1.f;
+    int less = 0, ties = 0, cnt = 0;
+    bool full = true, tiefix = false, nan = false, nan_eq = false;
+    float inv = 0.f; /* 1 / r_k^2 */
+    Dx3 acc{0, 0, 0};
+    PMD int bin(float d2) const { return (int)fminf((d2 - lo) * s, (float)(KT_BINS - 1)); }
+};
+
+__global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
+    __shared__ KnnLds L;
+    const int lane = threadIdx.x & 63;
+    const int64_t r = P.rec_begin + (int64_t)blockIdx.x * KNN_BLOCK + threadIdx.x;
+    const GridDesc &g = P.grid;
+    const int K = P.knn_k;
+    const float maxd2 = P.knn_r2;
+#pragma unroll
+    for (int w = 0; w < KT_BINS / 2; ++w) L.hist[w][lane] = 0u;
+    /* record */
+    bool active = false, live = false, back = false;
+    float4 pos = make_float4(0.f, 0.f, 0.f, 0.f), nrm = pos;
+    if (r < P.rec_end) {
+        pos = P.R.pos[r];
+        const uint32_t flags = (uint32_t)__float_as_int(pos.w);
+        active = !(flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID));
+        back = (flags & PM_REC_BACKFACE) != 0;
+        if (active) {
+            nrm = P.R.nrm[r];
+            live = __float_as_int(P.materials[__float_as_int(nrm.w)].w) == PM_MATTE; /* non-specular BSDF only */
+        }
+    }
+    const v3 p = xyz(pos), ns = xyz(nrm);
+    uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0, z0 = 0, z1 = 0;
+    if (live) { /* KnnGrid::init's cells */
+        const float rq = sqrtf(maxd2) * 1.0001f + 1e-4f;
+        x0 = cell_axis(p.x - rq, g.gx, g.inv_cs, g.dx); x1 = cell_axis(p.x + rq, g.gx, g.inv_cs, g.dx);
+        y0 = cell_axis(p.y - rq, g.gy, g.inv_cs, g.dy); y1 = cell_axis(p.y + rq, g.gy, g.inv_cs, g.dy);
+        z0 = cell_axis(p.z - rq, g.gz, g.inv_cs, g.dz); z1 = cell_axis(p.z + rq, g.gz, g.inv_cs, g.dz);
+    }
+    KnnSel S;
+    if (live) { S.phase = KP_HIST; S.need = K; S.blo = 0.f; S.bhi = maxd2; S.s = (float)KT_BINS / maxd2; }
+    if (live && !(S.s <= 3.402823466e38f)) S.s = 3.402823466e38f;
+
+    /* contribution of a found photon (pbrt kernel(), LPhoton diffuse term) into
+     * a; returns true when it is pbrt's 0/0 (K photons at distance 0) */
+    auto contrib = [&](Dx3 &a, float d2, const float4 &b, float wx, float wz) PM_INLINE {
+        if (!knn_facing(ns, back, b, wx, wz)) return false;
+        if (S.md2 == 0.f) return true;
+        knn_add(a, d2, S.inv, S.sc, b);
+        return false;
+    };
+    /* a photon inside this pass's interval; fl() -> its (b, wi.x, wi.z) */
+    auto on_hit = [&](float d2, auto fl) PM_INLINE {
+        switch (S.phase) {
+        case KP_HIST: { /* per-lane passes only: the tile passes count inline */
+            const int b = S.bin(d2);
+            atomicAdd(&L.hist[b >> 1][lane], 1u << ((b & 1) * 16));
+            S.cntf++;
+            break;
+        }
+        case KP_COLLECT:
+            if (S.bin(d2) == S.kbin) {
+                if (S.cc < (uint32_t)KT_LIST) L.list[S.cc][lane] = __float_as_uint(d2);
+                S.cc++;
+                S.mn = fminf(S.mn, d2);
+                S.mx = fmaxf(S.mx, d2);
+            }
+            break;
+        case KP_MIN:
+            if (d2 < S.tmin) { S.tmin = d2; S.tcnt = 1u; }
+            else if (d2 == S.tmin) S.tcnt++;
+            break;
+        case KP_SUM: {
+            float4 fb; float wx, wz;
+            fl(fb, wx, wz);
+            if (d2 < S.md2) { S.less++; S.nan |= contrib(S.acc, d2, fb, wx, wz); }
+            else { /* d2 == r_k^2 (full lookups): the kernel is 0 there; only pbrt's 0/0 matters */
+                S.ties++;
+                if (S.md2 == 0.f) S.nan_eq |= knn_facing(ns, back, fb, wx, wz);
+            }
+            break;
+        }
+        default: break;
+        }
+    };
+    auto begin_sum = [&]() PM_INLINE {
+        S.sc = knn_scale(P.knn_fx, S.md2);
+        S.inv = 1.f / S.md2;
+        S.acc = Dx3{0, 0, 0};
+        S.less = S.ties = 0;
+        S.nan = S.nan_eq = false;
+        S.blo = 0.f; S.bhi = S.full ? next_up(S.md2) : S.md2; /* not full: every d^2 < maxD^2 */
+        S.phase = KP_SUM;
+    };
+    auto begin_min = [&](float lo_incl, float hi_excl) PM_INLINE {
+        S.blo = lo_incl; S.bhi = hi_excl;
+        S.tmin = INFINITY; S.tcnt = 0u;
+        S.phase = KP_MIN;
+    };
+    /* end of a pass: the next phase */
+    auto finish = [&]() PM_INLINE {
+        switch (S.phase) {
+        case KP_HIST: {
+            if (S.level == 0) {
+                if (S.cntf < (uint32_t)K) { /* fewer than K inside maxD: r_k^2 = maxD^2 */
+                    S.full = false;
+                    S.md2 = maxd2;
+                    begin_sum();
+                    break;
+                }
+                if (S.cntf >= 65536u) { begin_min(0.f, maxd2); break; } /* 16-bit bins may have wrapped */
+            }
+            uint32_t cum = 0u;
+            bool found = false;
+#pragma unroll
+            for (int w = 0; w < KT_BINS / 2; ++w) {
+                const uint32_t hw = L.hist[w][lane];
+                L.hist[w][lane] = 0u;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t c = (hw >> (16 * h)) & 0xffffu;
+                    if (!found && cum + c >= (uint32_t)S.need) { found = true; S.kbin = 2 * w + h; }
+                    else if (!found) cum += c;
+                }
+            }
+            S.need -= (int)cum;
+            S.cc = 0u; S.mn = INFINITY; S.mx = 0.f;
+            /* the bin's d^2 range, widened: (d2 - lo) * s is within 2^-23
+             * relative of exact, so bin k lies in lo + [k - 0.01, k + 1.01) / s,
+             * and two ulps cover the rounding of that bound */
+            if (S.kbin > 0) {
+                const float cl = S.lo + ((float)S.kbin - 0.01f) / S.s;
+                S.blo = fmaxf(S.blo, __uint_as_float(max((int)__float_as_uint(cl) - 2, 0)));
+            }
+            if (S.kbin < KT_BINS - 1) {
+                const float ch = S.lo + ((float)S.kbin + 1.01f) / S.s;
+                if (ch < 3.0e38f) S.bhi = fminf(S.bhi, next_up(next_up(ch)));
+            }
+            S.phase = KP_COLLECT; /* same bin function, exact bin test per hit */
+            break;
+        }
+        case KP_COLLECT:
+            if (S.cc <= (uint32_t)KT_LIST) { /* rank the kept values: the need-th smallest */
+                uint32_t v[KT_LIST];
+#pragma unroll
+                for (int a = 0; a < KT_LIST; ++a) v[a] = (uint32_t)a < S.cc ? L.list[a][lane] : 0xffffffffu;
+                uint32_t ans = v[0];
+#pragma unroll
+                for (int a = 0; a < KT_LIST; ++a) {
+                    int lt = 0, le = 0;
+#pragma unroll
+                    for (int b = 0; b < KT_LIST; ++b) { lt += v[b] < v[a]; le += v[b] <= v[a]; }
+                    if ((uint32_t)a < S.cc && lt < S.need && S.need <= le) ans = v[a];
+                }
+                S.md2 = __uint_as_float(ans);
+                begin_sum();
+            } else if (S.mn == S.mx) {
+                S.md2 = S.mn;
+                begin_sum();
+            } else if (S.level >= KT_LEVELS) {
+                begin_min(S.mn, next_up(S.mx));
+            } else { /* re-bin [mn, mx] */
+                S.level++;
+                S.lo = S.mn;
+                S.s = (float)KT_BINS / (S.mx - S.mn);
+                if (!(S.s <= 3.402823466e38f)) S.s = 3.402823466e38f;
+                S.blo = S.mn; S.bhi = next_up(S.mx);
+                S.cntf = 0u;
+                S.phase = KP_HIST;
+            }
+            break;
+        case KP_MIN:
+            if (S.tcnt == 0u || S.tcnt >= (uint32_t)S.need) { S.md2 = S.tcnt ? S.tmin : maxd2; begin_sum(); }
+            else { S.need -= (int)S.tcnt; begin_min(next_up(S.tmin), S.bhi); }
+            break;
+        case KP_SUM:
+            if (S.full) {
+                /* K found: those below r_k^2 and K - less of the ties; the ties
+                 * add 0 unless r_k^2 = 0, where the selected ones decide the NaN */
+                if (S.ties == K - S.less) S.nan |= S.nan_eq;
+                else if (S.md2 == 0.f) S.tiefix = true;
+                S.cnt = K;
+            } else {
+                S.cnt = S.less;
+            }
+            S.phase = KP_DONE;
+            break;
+        default: break;
+        }
+    };
+
+    const f2 px2 = {p.x, p.x}, py2 = {p.y, p.y}, pz2 = {p.z, p.z};
+    bool pend = live, direct = false;
+    while (true) {
+        const unsigned long long pm = __ballot(pend);
+        if (pm == 0ull) break;
+        /* the group: every pending lane if the union box fits the 64-lane row
+         * map, else the leader's neighbourhood (k_gather_tile) */
+        uint32_t X0, X1, Y0, Y1, Z0, Z1;
+        bool mine = pend;
+        union_box6(g, mine, x0, x1, y0, y1, z0, z1, X0, X1, Y0, Y1, Z0, Z1);
+        uint32_t LY = Y1 > Y0 ? 32u - (uint32_t)__builtin_clz(Y1 - Y0) : 0u;
+        if (LY > 6u || ((uint64_t)(Z1 - Z0 + 1u) << LY) > 64u) {
+            const int leader = __builtin_ctzll(pm);
+            const uint32_t lx = __builtin_amdgcn_readlane(x0, leader), ly = __builtin_amdgcn_readlane(y0, leader),
+                           lz = __builtin_amdgcn_readlane(z0, leader);
+            mine = pend && x0 + KT_GROUP_R - lx <= 2u * KT_GROUP_R && y0 + KT_GROUP_R - ly <= 2u * KT_GROUP_R &&
+                   z0 + KT_GROUP_R - lz <= 2u * KT_GROUP_R;
+            if (__builtin_popcountll(__ballot(mine)) < KT_GROUP_MIN) {
+                direct = direct || pend;
+                break;
+            }
+            union_box6(g, mine, x0, x1, y0, y1, z0, z1, X0, X1, Y0, Y1, Z0, Z1);
+            LY = Y1 > Y0 ? 32u - (uint32_t)__builtin_clz(Y1 - Y0) : 0u;
+            if (LY > 6u || ((uint64_t)(Z1 - Z0 + 1u) << LY) > 64u) { /* a grid too coarse for the bound: per lane */
+                direct = direct || pend;
+                break;
+            }
+        }
+        pend = pend && !mine;
+        TILE_STAT(0, 1);
+        /* union row u = lane: photons [B, B + len) of cells X0..X1 */
+        uint32_t B = 0u, len = 0u;
+        const uint32_t cy = Y0 + ((uint32_t)lane & ((1u << LY) - 1u)), cz = Z0 + ((uint32_t)lane >> LY);
+        if (cy <= Y1 && cz <= Z1) {
+            const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+            B = P.cell_start[row + X0];
+            len = P.cell_start[row + X1 + 1u] - B;
+        }
+        const uint32_t incl = wave_incl_sum_u32(len), pre = incl - len;
+        const uint32_t U = uniform_u32(__builtin_amdgcn_readlane(incl, 63));
+        const uint32_t gofs = B - pre;
+        /* passes until every lane of the group has its estimate */
+        while (__ballot(mine && S.phase != KP_DONE)) {
+            const bool act = mine && S.phase != KP_DONE;
+            TILE_STAT(1, 1);
+            TILE_STAT(6, __builtin_popcountll(__ballot(act && S.phase == KP_MIN)));
+            TILE_STAT(7, __builtin_popcountll(__ballot(act && S.phase == KP_HIST && S.level > 0)));
+            const float blo = act ? S.blo : INFINITY, bhi = act ? S.bhi : 0.f;
+            const bool hl = act && S.phase == KP_HIST; /* counts inline */
+            const bool hist_any = __ballot(hl) != 0ull;
+            const bool other_any = __ballot(act && !hl) != 0ull;
+            /* the sums need the photons' flux and direction */
+            const bool flux = __ballot(act && S.phase == KP_SUM) != 0ull;
+            const f2 lo2 = {S.lo, S.lo}, s2 = {S.s, S.s};
+            uint32_t cntf = 0u;
+            auto window = [&](uint32_t n, auto DO_HIST, auto DO_OTHER) PM_INLINE {
+                /* every lane tests every staged photon, two per packed step,
+                 * 32 at a time: HIST lanes count them into their histogram on
+                 * the spot, the others collect a hit mask and then take the
+                 * hits one per lane per iteration */
+                for (uint32_t vb = 0; vb < n; vb += 32) {
+                    const uint32_t cnt = min(32u, n - vb);
+                    uint32_t bits = 0u;
+#pragma unroll 4
+                    for (uint32_t j = 0; j < cnt; j += 2) {
+                        const f2 ddx = px2 - f2{L.x[vb + j], L.x[vb + j + 1]}, ddy = py2 - f2{L.y[vb + j], L.y[vb + j + 1]},
+                                 ddz = pz2 - f2{L.z[vb + j], L.z[vb + j + 1]};
+                        const f2 d2 = (ddx * ddx + ddy * ddy) + ddz * ddz;
+                        const bool hx = d2.x >= blo && d2.x < bhi && j < cnt, hy = d2.y >= blo && d2.y < bhi && j + 1 < cnt;
+                        if (decltype(DO_HIST)::value) {
+                            if (hl) {
+                                /* S.bin of both, packed: the same IEEE operations.
+                                 * Branch-free: a miss adds 0 to bin 0 */
+                                const f2 bb = (d2 - lo2) * s2;
+                                const int b0 = hx ? (int)fminf(bb.x, (float)(KT_BINS - 1)) : 0;
+                                const int b1 = hy ? (int)fminf(bb.y, (float)(KT_BINS - 1)) : 0;
+#ifdef PM_KT_BRANCHY
+                                if (hx) atomicAdd(&L.hist[b0 >> 1][lane], 1u << ((b0 & 1) * 16));
+                                if (hy) atomicAdd(&L.hist[b1 >> 1][lane], 1u << ((b1 & 1) * 16));
+#else
+                                atomicAdd(&L.hist[b0 >> 1][lane], (uint32_t)hx << ((b0 & 1) * 16));
+                                atomicAdd(&L.hist[b1 >> 1][lane], (uint32_t)hy << ((b1 & 1) * 16));
+#endif
+                                cntf += (uint32_t)hx + (uint32_t)hy;
+                            }
+                        }
+                        if (decltype(DO_OTHER)::value) {
+                            if (hx) bits |= 1u << j;
+                            if (hy) bits |= 2u << j;
+                        }
+                    }
+                    if (decltype(DO_OTHER)::value) {
+                        if (hl) bits = 0u;
+                        TILE_STAT(4, wave_max_u32(__builtin_popcount(bits)));
+                        while (bits) {
+                            const uint32_t t = vb + (uint32_t)__builtin_ctz(bits);
+                            bits &= bits - 1u;
+                            const v3 diff = p - mk(L.x[t], L.y[t], L.z[t]);
+                            const float d2 = diff.x * diff.x + diff.y * diff.y + diff.z * diff.z;
+                            on_hit(d2, [&](float4 &fb, float &wx, float &wz) PM_INLINE { fb = L.b[t]; wx = L.w[t]; wz = L.c[t]; });
+                        }
+                    }
+                }
+            };
+            for (uint32_t T0 = 0; T0 < U; T0 += KT_CAP) {
+                const uint32_t n = min((uint32_t)KT_CAP, U - T0);
+                TILE_STAT(2, 1);
+                TILE_STAT(3, n);
+                constexpr int H = KT_CAP / 64;
+                /* stage positions T0 + lane + 64 h: the row of each from a max
+                 * scan over the row-start marks */
+#pragma unroll
+                for (int h = 0; h < H; ++h) L.mark[lane + 64 * h] = -1;
+                wave_lds_sync();
+                if (len > 0u) {
+                    if (pre >= T0 && pre < T0 + KT_CAP) L.mark[pre - T0] = lane;
+                    else if (pre < T0 && pre + len > T0) L.mark[0] = lane;
+                }
+                wave_lds_sync();
+                int u[H];
+                u[0] = wave_incl_max_i32(L.mark[lane]);
+#pragma unroll
+                for (int h = 1; h < H; ++h) u[h] = max(wave_incl_max_i32(L.mark[lane + 64 * h]), __builtin_amdgcn_readlane(u[h - 1], 63));
+                uint32_t gi[H];
+#pragma unroll
+                for (int h = 0; h < H; ++h) gi[h] = T0 + 64u * h + (uint32_t)lane + (uint32_t)__shfl((int)gofs, u[h]);
+                const float *phb = reinterpret_cast<const float *>(P.ph_b);
+                const uint32_t g0 = (uint32_t)__builtin_amdgcn_readlane((int)gi[0], 0);
+                float4 pa[H], qa[H];
+                float ca[H];
+#pragma unroll
+                for (int h = 0; h < H; ++h) {
+                    const uint32_t j = (uint32_t)lane + 64u * h < n ? gi[h] : g0;
+                    pa[h] = P.ph_a[j];
+                    qa[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    ca[h] = 0.f;
+                    if (flux) { qa[h] = P.ph_b[2 * (size_t)j]; ca[h] = phb[8 * (size_t)j + 4]; }
+                }
+#pragma unroll
+                for (int h = 0; h < H; ++h) {
+                    const int q = lane + 64 * h;
+                    L.x[q] = pa[h].x; L.y[q] = pa[h].y; L.z[q] = pa[h].z;
+                    if (flux) { L.w[q] = pa[h].w; L.b[q] = qa[h]; L.c[q] = ca[h]; }
+                }
+                wave_lds_sync();
+                using T_ = std::true_type;
+                using F_ = std::false_type;
+                if (hist_any && other_any) window(n, T_{}, T_{});
+                else if (hist_any) window(n, T_{}, F_{});
+                else window(n, F_{}, T_{});
+                wave_lds_sync(); /* the window is read before the next one overwrites it */
+            }
+            if (hl) S.cntf += cntf;
+            if (act) finish();
+        }
+    }
+    /* lanes of incoherent tiles: the same passes over their own rows */
+    TILE_STAT(5, __builtin_popcountll(__ballot(direct)));
+    KnnGrid G;
+    unsigned long long nv = 0, nr = 0;
+    if (__ballot(direct)) {
+        if (direct) G.init(P.grid, p, maxd2);
+        const float *phb = reinterpret_cast<const float *>(P.ph_b);
+        while (__ballot(direct && S.phase != KP_DONE)) {
+            if (direct && S.phase != KP_DONE) {
+                G.scan(P.cell_start, P.ph_a, p, [&]() { return S.bhi; },
+                       [&](uint32_t j, const float4 &a, float d2) {
+                           if (!(d2 >= S.blo && d2 < S.bhi)) return;
+                           on_hit(d2, [&](float4 &fb, float &wx, float &wz) PM_INLINE {
+                               fb = P.ph_b[2 * (size_t)j]; wx = a.w; wz = phb[8 * (size_t)j + 4];
+                           });
+                       }, nv, nr);
+                finish();
+            }
+        }
+    }
+    /* r_k^2 = 0 with more photons at the query point than places: the lowest
+     * slots are the found ones (k_gather_knn's third scan) */
+    if (__ballot(S.tiefix)) {
+        if (S.tiefix) {
+            if (!direct) G.init(P.grid, p, maxd2);
+            const float *phb = reinterpret_cast<const float *>(P.ph_b);
+            const int need = K - S.less;
+            uint32_t last = 0u;
+            bool first = true, nan = false;
+            for (int t = 0; t < need; ++t) {
+                uint32_t best = 0xffffffffu, bj = 0u;
+                float4 ba = make_float4(0.f, 0.f, 0.f, 0.f);
+                G.scan(P.cell_start, P.ph_a, p, [&]() { return S.md2; },
+                       [&](uint32_t j, const float4 &a, float d2) {
+                           if (d2 != S.md2) return;
+                           const uint32_t sl = __float_as_uint(phb[8 * (size_t)j + 5]);
+                           if ((first || sl > last) && sl <= best) { best = sl; bj = j; ba = a; }
+                       }, nv, nr);
+                nan |= knn_facing(ns, back, P.ph_b[2 * (size_t)bj], ba.w, phb[8 * (size_t)bj + 4]); /* r_k^2 = 0: 0/0 */
+                last = best;
+                first = false;
+            }
+            S.nan |= nan;
+        }
+    }
+    if (active) {
+        if (!live) S.md2 = maxd2; /* specular: nothing found, cnt 0 */
+        const float4 st = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : P.R.state[r];
+        const double isc = 1.0 / (double)S.sc;
+        v3 Lr = mk((float)(S.acc.x * isc), (float)(S.acc.y * isc), (float)(S.acc.z * isc));
+        if (S.nan) Lr = mk(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
+        const v3 flux = xyz(st) + Lr;
+        P.R.state[r] = make_float4(flux.x, flux.y, flux.z, S.md2);
+        P.R.n[r] = (float)S.cnt;
+    }
+}
+
 hipError_t launch_gather_knn(const GatherParams &p, int count, hipStream_t s) {
     if (p.rec_end <= p.rec_begin) return hipSuccess;
     if (p.knn_k < 1 || p.knn_k > PM_KNN_MAX) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)((p.rec_end - p.rec_begin + KNN_BLOCK - 1) / KNN_BLOCK);
+    /* census launches run the per-lane kernel (its photons-tested count is the
+     * per-record unit bench.py prices); the tile kernel finds the same set */
+    if (!count && p.kernel == PM_GK_TILE) {
+        pm_launch(k_gather_knn_tile, dim3(grid), dim3(KNN_BLOCK), 0, s, p);
+        return hipGetLastError();
+    }
     const uint32_t lds = (uint32_t)(p.knn_k * KNN_BLOCK * sizeof(uint32_t));
     if (count) pm_launch(k_gather_knn<1>, dim3(grid), dim3(KNN_BLOCK), lds, s, p);
     else pm_launch(k_gather_knn<0>, dim3(grid), dim3(KNN_BLOCK), lds, s, p);

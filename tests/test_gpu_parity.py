@@ -494,6 +494,49 @@ def test_knn_render_parity(cornell):
     assert np.array_equal(img.view(np.uint32), again.view(np.uint32))
 
 
+@pytest.mark.parametrize("scene,W,H,paths,K,radius2", [
+    ("cornell", 160, 120, 16384, 50, 900.0),
+    ("cornell", 160, 120, 16384, 64, 2500.0),
+    ("cornell", 160, 120, 16384, 1, 25.0),
+    ("caustic", 128, 128, 65536, 64, 400.0),      # dense caustic: deeper re-binning
+    ("soup", 128, 96, 16384, 16, 100.0),          # incoherent tiles: per-lane passes
+    ("cornell", 32, 24, 40000, 8, 1.0e7),         # >= 2^16 photons inside maxD: minimum extraction
+])
+def test_knn_kernels_agree(scene, W, H, paths, K, radius2, oracle_mod, hip_mod, monkeypatch):
+    """The kNN tile kernel (LDS-staged tile unions, histogram selection of
+    r_k^2) and the per-lane heap kernel give bit-identical records: same
+    found count, r_k^2 and fixed-point flux, over two accumulating passes."""
+    from pmrender.abi import PM_ESTIMATOR_KNN
+    sc = {"cornell": lambda: scenes.cornell_box(W, H), "caustic": lambda: scenes.caustic_scene(W, H),
+          "soup": lambda: scenes.triangle_soup(20000, W, H)}[scene]()
+    orc = sc.load_into(oracle_mod.Oracle())
+    p = RenderParams.defaults(paths_per_pass=paths, initial_radius2=radius2, estimator=PM_ESTIMATOR_KNN,
+                              knn_lookup=K)
+    recs = orc.eye_pass(p)
+    slots = [orc.trace_photons(p, i, 0, paths) for i in range(2)]
+    outs = {}
+    for name in ("lane", "tile"):
+        monkeypatch.setenv("PM_GATHER_KERNEL", name)
+        ctx = sc.load_into(hip_mod.Context(0))
+        try:
+            ctx.upload_records(recs)
+            for s in slots:
+                ctx.upload_slots(s)
+                ctx.build_photon_map(p, len(s))
+                ctx.gather(p)
+            outs[name] = ctx.download_records()
+        finally:
+            ctx.close()
+    act = (recs["flags"] & 7) == 0
+    n = outs["lane"]["photon_count"][act]
+    assert (n > 0).mean() > 0.5
+    if radius2 < 1e6:
+        assert (n == K).any() and (n < K).any()   # both full and partial lookups occur
+    else:
+        assert (n == K).all() and (slots[1]["bits"] & 1).sum() >= 65536
+    assert_bitexact(outs["tile"], outs["lane"], f"kNN tile vs per-lane ({scene}, K={K})")
+
+
 def test_knn_rejects_partial_gathers(cornell, hip_mod):
     torch = pytest.importorskip("torch")
     from pmrender.abi import PM_ESTIMATOR_KNN

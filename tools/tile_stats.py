@@ -1,4 +1,4 @@
-"""k_gather_tile event counts at C2 (PM_TILE_STATS variant build):
+"""k_gather_tile (or with argument knn: k_gather_knn_tile) event counts at C2 (PM_TILE_STATS variant build):
    make -C cuda-raytrace_amd variant NAME=tstats VFLAGS=-DPM_TILE_STATS
    PMHIP_LIB=cuda-raytrace_amd/lib/variants/libpmhip_tstats.so python tools/tile_stats.py"""
 import os, sys
@@ -9,7 +9,12 @@ from pmrender import hip, scenes
 from pmrender.abi import RenderParams
 sc = scenes.cornell_box(1920, 1080)
 ctx = sc.load_into(hip.Context(0))
-p = RenderParams.defaults(paths_per_pass=262144)
+KNN = len(sys.argv) > 1 and sys.argv[1] == "knn"
+if KNN:
+    from pmrender.abi import PM_ESTIMATOR_KNN
+    p = RenderParams.defaults(paths_per_pass=262144, initial_radius2=100.0, estimator=PM_ESTIMATOR_KNN, knn_lookup=50)
+else:
+    p = RenderParams.defaults(paths_per_pass=262144)
 ctx.eye_pass(p)
 ctx.trace_photons(p, 0, 0, 262144)
 ctx.build_photon_map(p, 262144 * 4)
@@ -19,5 +24,7 @@ ctx.gather(p)
 ctx.synchronize()
 v = list(ctx.trace_profile().values())
 names = ["tile_waves", "windows", "test_pairs", "hit_iters", "direct_lanes", "chunks", "wide_waves", "staged"]
+if KNN:  # k_gather_knn_tile: per-wave sums
+    names = ["groups", "passes", "windows", "staged", "hit_iters", "direct_lanes", "min_lane_passes", "rebin_lane_passes"]
 for k, x in zip(names, v):
     print(f"{k:14s} {x:12d}  per tile wave {x / max(v[0], 1):8.2f}")
