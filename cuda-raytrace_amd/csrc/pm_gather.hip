@@ -1179,21 +1179,40 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
         }
         pend = pend && !mine;
         TILE_STAT(0, 1);
-        /* union row u = lane: photons [B, B + len) of cells X0..X1 */
-        uint32_t B = 0u, len = 0u;
-        const uint32_t cy = Y0 + ((uint32_t)lane & ((1u << LY) - 1u)), cz = Z0 + ((uint32_t)lane >> LY);
-        if (cy <= Y1 && cz <= Z1) {
-            const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
-            B = P.cell_start[row + X0];
-            len = P.cell_start[row + X1 + 1u] - B;
-        }
-        const uint32_t incl = wave_incl_sum_u32(len), pre = incl - len;
-        const uint32_t U = uniform_u32(__builtin_amdgcn_readlane(incl, 63));
-        const uint32_t gofs = B - pre;
         /* passes until every lane of the group has its estimate */
         while (__ballot(mine && S.phase != KP_DONE)) {
             const bool act = mine && S.phase != KP_DONE;
             TILE_STAT(1, 1);
+            /* this pass's union: the cells of [p - r', p + r'] for r'^2 = the
+             * pass's upper bound (after level 0 mostly r_k^2, not maxD^2) —
+             * a sub-box of the group's, so it fits the row map as well */
+            uint32_t PX0 = X0, PX1 = X1, PY0 = Y0, PY1 = Y1, PZ0 = Z0, PZ1 = Z1, PLY = LY;
+            {
+                uint32_t a0 = 0, a1 = 0, b0 = 0, b1 = 0, c0 = 0, c1 = 0;
+                if (act) {
+                    const float rq = sqrtf(S.bhi) * 1.0001f + 1e-4f;
+                    a0 = cell_axis(p.x - rq, g.gx, g.inv_cs, g.dx); a1 = cell_axis(p.x + rq, g.gx, g.inv_cs, g.dx);
+                    b0 = cell_axis(p.y - rq, g.gy, g.inv_cs, g.dy); b1 = cell_axis(p.y + rq, g.gy, g.inv_cs, g.dy);
+                    c0 = cell_axis(p.z - rq, g.gz, g.inv_cs, g.dz); c1 = cell_axis(p.z + rq, g.gz, g.inv_cs, g.dz);
+                }
+                uint32_t QX0, QX1, QY0, QY1, QZ0, QZ1;
+                union_box6(g, act, a0, a1, b0, b1, c0, c1, QX0, QX1, QY0, QY1, QZ0, QZ1);
+                const uint32_t QLY = QY1 > QY0 ? 32u - (uint32_t)__builtin_clz(QY1 - QY0) : 0u;
+                if (QLY <= 6u && ((uint64_t)(QZ1 - QZ0 + 1u) << QLY) <= 64u) {
+                    PX0 = QX0; PX1 = QX1; PY0 = QY0; PY1 = QY1; PZ0 = QZ0; PZ1 = QZ1; PLY = QLY;
+                }
+            }
+            /* union row u = lane: photons [B, B + len) of cells PX0..PX1 */
+            uint32_t B = 0u, len = 0u;
+            const uint32_t cy = PY0 + ((uint32_t)lane & ((1u << PLY) - 1u)), cz = PZ0 + ((uint32_t)lane >> PLY);
+            if (cy <= PY1 && cz <= PZ1) {
+                const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+                B = P.cell_start[row + PX0];
+                len = P.cell_start[row + PX1 + 1u] - B;
+            }
+            const uint32_t incl = wave_incl_sum_u32(len), pre = incl - len;
+            const uint32_t U = uniform_u32(__builtin_amdgcn_readlane(incl, 63));
+            const uint32_t gofs = B - pre;
             TILE_STAT(6, __builtin_popcountll(__ballot(act && S.phase == KP_MIN)));
             TILE_STAT(7, __builtin_popcountll(__ballot(act && S.phase == KP_HIST && S.level > 0)));
             const float blo = act ? S.blo : INFINITY, bhi = act ? S.bhi : 0.f;
