@@ -100,6 +100,12 @@ struct Ctx {
     bool view_active = false;
     int64_t n_view = 0;
     DevBuf d_vflags, d_vrank, d_vlist, d_vsums;
+    /* tiles (64 records) holding an active record, in record order: full-range
+     * tile gathers launch over these only (records fixed after the eye pass) */
+    DevBuf d_tiles, d_tile_flags;
+    int64_t n_tiles = 0;
+    bool tiles_valid = false;
+    bool tile_list = true; /* env PM_TILE_LIST=0: launch over every tile */
     /* pm_reset_records is deferred: records read as (flux 0, N 0, r2 = rec_fresh_r2) */
     bool rec_fresh = false;
     float rec_fresh_r2 = 0.f;
@@ -298,6 +304,7 @@ int ensure_records(Ctx *c) {
     HIPCHK(c, c->d_n.ensure(n * sizeof(float)));
     HIPCHK(c, c->d_dl.ensure(n * sizeof(float4)));
     c->nrec = n;
+    c->tiles_valid = false;
     return PM_OK;
 }
 
@@ -429,6 +436,7 @@ int pm_create(void **out, const pm_config *cfg) {
     if (const char *e = getenv("PM_GATHER_XCD")) c->gather_xcd = atoi(e) != 0;
     if (const char *e = getenv("PM_TRACE_POOL")) c->trace_pool = atoi(e) != 0;
     if (const char *e = getenv("PM_POOL_WAVES")) c->pool_waves = std::max(1LL, atoll(e));
+    if (const char *e = getenv("PM_TILE_LIST")) c->tile_list = atoi(e) != 0;
     if (const char *e = getenv("PM_KD_STACK")) c->kd_stack = std::max(1, std::min(KD_STACK, atoi(e)));
     if (const char *e = getenv("PM_STAGE_TIMERS")) if (atoi(e) == 0) c->timed_stages.clear();
     (void)hipSetDevice(dev);
@@ -825,6 +833,7 @@ int pm_eye_pass(void *ptr, const pm_render_params *p, void *stream) {
     HIPCHK(c, launch_eye(E, s));
     timer_end(c, "eye", s);
     c->rec_fresh = false; /* the eye pass writes every record */
+    c->tiles_valid = false;
     if (c->view_active && (rc = build_view(c, s))) return rc;
     return PM_OK;
 }
@@ -1024,6 +1033,30 @@ int pm_build_photon_map(void *ptr, const pm_render_params *p, int64_t n_slots, v
     return PM_OK;
 }
 
+
+/* the tile list of the current records (flags on the device, ordered list
+ * built on the host: one 1-byte-per-tile copy after each eye pass / upload) */
+static int ensure_tiles(Ctx *c, hipStream_t s) {
+    if (c->tiles_valid) return PM_OK;
+    const int64_t nt = (c->nrec + 63) / 64;
+    HIPCHK(c, c->d_tile_flags.ensure(std::max<int64_t>(nt, 16)));
+    HIPCHK(c, c->d_tiles.ensure(std::max<int64_t>(nt * 4, 16)));
+    HIPCHK(c, launch_tile_flags(recs(c), c->d_tile_flags.as<uint8_t>(), s));
+    std::vector<uint8_t> f((size_t)nt);
+    HIPCHK(c, hipMemcpyAsync(f.data(), c->d_tile_flags.p, (size_t)nt, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    std::vector<uint32_t> list;
+    list.reserve((size_t)nt);
+    for (int64_t t = 0; t < nt; ++t)
+        if (f[(size_t)t]) list.push_back((uint32_t)t);
+    if (!list.empty())
+        HIPCHK(c, hipMemcpyAsync(c->d_tiles.p, list.data(), list.size() * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->n_tiles = (int64_t)list.size();
+    c->tiles_valid = true;
+    return PM_OK;
+}
+
 static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, int64_t rec_begin, int64_t rec_count,
                          void *stream, int *count = nullptr, long long *flux = nullptr) {
     int rc;
@@ -1049,6 +1082,14 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
     const bool consume = c->rec_fresh && !partial && !split && rec_begin == 0 && rec_count == c->nrec;
     if (consume || (split && c->rec_fresh)) { G.fresh = 1; G.r2init = c->rec_fresh_r2; }
     else if ((rc = materialize_reset(c, s))) return rc;
+    /* full-range tile gathers skip the tiles without an active record (their
+     * records are neither read nor written, except as partials outside a view) */
+    if (c->tile_list && c->gather_kernel == PM_GK_TILE && !c->counting && rec_begin == 0 && rec_count == c->nrec &&
+        p->gather_structure == PM_GATHER_GRID && ((!partial && !split) || c->view_active)) {
+        if ((rc = ensure_tiles(c, s))) return rc;
+        G.tiles = c->d_tiles.as<uint32_t>();
+        G.n_tiles = c->n_tiles;
+    }
     if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters.p, 0, 32, s));
     timer_begin(c, "gather", s);
     if (p->estimator == PM_ESTIMATOR_KNN) {
@@ -1371,6 +1412,7 @@ int pm_upload_records(void *ptr, const pm_record *in, int64_t n) {
     HIPCHK(c, hipMemcpy(c->d_dl.p, dl.data(), n * 16, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_n.p, N.data(), n * 4, hipMemcpyHostToDevice));
     c->rec_fresh = false; /* every record overwritten */
+    c->tiles_valid = false;
     if (c->view_active && (rc = build_view(c, c->stream))) return rc;
     return PM_OK;
 }

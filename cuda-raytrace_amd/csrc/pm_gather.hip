@@ -362,7 +362,14 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
     __shared__ TileLds tiles[GATHER_BLOCK / 64];
     TileLds &T = tiles[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
-    const int64_t r = P.rec_begin + gather_block(P) * GATHER_BLOCK + threadIdx.x;
+    int64_t r;
+    if (P.tiles) { /* only tiles with an active record (no block-level barrier below: a wave may leave) */
+        const int64_t w = (int64_t)blockIdx.x * (GATHER_BLOCK / 64) + (threadIdx.x >> 6);
+        if (w >= P.n_tiles) return;
+        r = P.rec_begin + (int64_t)P.tiles[w] * 64 + lane;
+    } else {
+        r = P.rec_begin + gather_block(P) * GATHER_BLOCK + threadIdx.x;
+    }
     const GridDesc &g = P.grid;
     GatherRec R;
     R.load<PARTIAL>(P, r);
@@ -970,7 +977,8 @@ struct KnnSel {
 __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
     __shared__ KnnLds L;
     const int lane = threadIdx.x & 63;
-    const int64_t r = P.rec_begin + (int64_t)blockIdx.x * KNN_BLOCK + threadIdx.x;
+    const int64_t r = P.rec_begin + (P.tiles ? (int64_t)P.tiles[blockIdx.x] * 64 + lane
+                                             : (int64_t)blockIdx.x * KNN_BLOCK + threadIdx.x);
     const GridDesc &g = P.grid;
     const int K = P.knn_k;
     const float maxd2 = P.knn_r2;
@@ -1388,7 +1396,8 @@ hipError_t launch_gather_knn(const GatherParams &p, int count, hipStream_t s) {
     /* census launches run the per-lane kernel (its photons-tested count is the
      * per-record unit bench.py prices); the tile kernel finds the same set */
     if (!count && p.kernel == PM_GK_TILE) {
-        pm_launch(k_gather_knn_tile, dim3(grid), dim3(KNN_BLOCK), 0, s, p);
+        const unsigned g = p.tiles ? (unsigned)p.n_tiles : grid;
+        if (g) pm_launch(k_gather_knn_tile, dim3(g), dim3(KNN_BLOCK), 0, s, p);
         return hipGetLastError();
     }
     const uint32_t lds = (uint32_t)(p.knn_k * KNN_BLOCK * sizeof(uint32_t));
@@ -1485,6 +1494,14 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_kd(GatherParams P) {
 template <int STRUCT, int PARTIAL, int COUNT>
 static void launch_g(const GatherParams &p, hipStream_t s) {
     unsigned grid = (unsigned)((p.rec_end - p.rec_begin + GATHER_BLOCK - 1) / GATHER_BLOCK);
+    if (STRUCT == PM_GATHER_GRID && !COUNT && p.kernel == PM_GK_TILE && p.tiles) {
+        /* the tile list: only tiles with an active record */
+        const unsigned g = (unsigned)((p.n_tiles + GATHER_BLOCK / 64 - 1) / (GATHER_BLOCK / 64));
+        if (g == 0) return;
+        if (p.fx_nonneg) pm_launch((k_gather_tile<PARTIAL, 1>), dim3(g), dim3(GATHER_BLOCK), 0, s, p);
+        else pm_launch((k_gather_tile<PARTIAL, 0>), dim3(g), dim3(GATHER_BLOCK), 0, s, p);
+        return;
+    }
     /* a counting launch always runs the per-lane kernel: its census (rows and
      * photons per RECORD) is the algorithm's unit count bench.py prices; the
      * tile and wave kernels find exactly the same photons (bit-identical records) */
@@ -1666,6 +1683,19 @@ __global__ __launch_bounds__(256) void k_final(FinalParams P) {
     P.out[3 * o + 0] = out.x;
     P.out[3 * o + 1] = out.y;
     P.out[3 * o + 2] = out.z;
+}
+
+__global__ __launch_bounds__(256) void k_tile_flags(RecordsDev R, uint8_t *flags) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    bool act = false;
+    if (r < R.count) act = !((uint32_t)__float_as_int(R.pos[r].w) & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID));
+    const unsigned long long m = __ballot(act);
+    if ((threadIdx.x & 63) == 0 && r < R.count) flags[r >> 6] = m != 0ull ? 1 : 0;
+}
+hipError_t launch_tile_flags(const RecordsDev &R, uint8_t *flags, hipStream_t s) {
+    if (R.count <= 0) return hipSuccess;
+    pm_launch(k_tile_flags, dim3((unsigned)((R.count + 255) / 256)), dim3(256), 0, s, R, flags);
+    return hipGetLastError();
 }
 
 hipError_t launch_final(const FinalParams &p, hipStream_t s) {

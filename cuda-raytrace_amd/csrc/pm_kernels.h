@@ -147,6 +147,11 @@ struct GatherParams {
     float knn_r2, knn_fx;
     const pm_photon *slots;
     unsigned long long *counters; /* [0] visited, [1] in radius */
+    /* tile list (non-null: full-range gathers): the launch covers only the
+     * n_tiles tiles of 64 records (tile t = records [64 t, 64 t + 64)) that
+     * hold an active record, in record order */
+    const uint32_t *tiles;
+    int64_t n_tiles;
 };
 
 struct FinalParams {
@@ -187,6 +192,8 @@ hipError_t launch_ppm_update(const GatherParams &p, const long long *partial, in
 hipError_t launch_ppm_update_split(const GatherParams &p, const int *count, const long long *flux, int64_t n_view,
                                    int64_t v_begin, int64_t v_count, int fresh, hipStream_t s);
 hipError_t launch_final(const FinalParams &p, hipStream_t s);
+/* flags[t] = 1 when tile t (records [64 t, 64 t + 64)) holds an active record */
+hipError_t launch_tile_flags(const RecordsDev &R, uint8_t *flags, hipStream_t s);
 hipError_t launch_radius2_io(const RecordsDev &R, float *buf, int64_t rec_begin, int64_t rec_count, int to_records,
                              const uint32_t *view, hipStream_t s);
 /* exclusive scan of n uint32 (pm_bucket.hip); in/out 16-B aligned; sums: scan_scratch_words(n) */

@@ -235,6 +235,37 @@ def test_partial_plus_update_equals_fused(cornell):
     assert_bitexact(ctx.download_records(), fused, "partial+update vs fused")
 
 
+@pytest.mark.parametrize("view", [False, True])
+def test_deferred_reset_before_partial_gather(cornell, view):
+    """A deferred pm_reset_records is applied before a partial gather (which
+    does not consume it), with and without the active-record view (where the
+    launch covers only the tiles holding active records): the partials equal
+    those of a gather over freshly uploaded records."""
+    torch = pytest.importorskip("torch")
+    ctx, orc = cornell
+    p, recs, slots = _gather_inputs(orc)
+    ctx.upload_slots(slots)
+    ctx.build_photon_map(p, len(slots))
+    ctx.upload_records(recs)
+    n = ctx.set_record_view(True) if view else len(recs)
+    try:
+        ref = torch.zeros((len(recs), 4), dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        ctx.gather_partial(p, ref.data_ptr())
+        ctx.synchronize()
+        ctx.gather(p)                       # PPM state moves away from the initial one
+        ctx.reset_records(p)                # deferred
+        got = torch.zeros((len(recs), 4), dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        ctx.gather_partial(p, got.data_ptr())
+        ctx.synchronize()
+        assert np.array_equal(got.cpu().numpy()[:n], ref.cpu().numpy()[:n])
+        assert (ref.cpu().numpy()[:n, 0] > 0).sum() > 100
+    finally:
+        if view:
+            ctx.set_record_view(False)
+
+
 def test_sharded_reduce_exchange_bitexact(oracle_mod, hip_mod):
     """The multi-GPU "reduce" exchange emulated on one device: two contexts
     each trace half of the global paths, gather all records against their
