@@ -356,6 +356,10 @@ constexpr uint32_t GROUP_R = PM_GROUP_R;
 #define PM_GROUP_MIN 12
 #endif
 constexpr int GROUP_MIN = PM_GROUP_MIN;
+#ifndef PM_TILE_UMAX
+#define PM_TILE_UMAX 1024
+#endif
+constexpr int TILE_UMAX = PM_TILE_UMAX; /* C5: no cap 2.88 ms, 2048 0.44, 1024 0.41, 512 0.43 (per lane 0.42) */
 static_assert(2 * GROUP_R + 2 <= 8, "group rows exceed the 64-lane row map");
 template <int PARTIAL, int NN>
 __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherParams P) {
@@ -433,6 +437,10 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
         const uint32_t incl = wave_incl_sum_u32(len), pre = incl - len;
         const uint32_t U = uniform_u32(__builtin_amdgcn_readlane(incl, 63));
         if (U == 0u) continue;
+        /* a dense union (many photons per cell, e.g. C5's caustic scene: 4x
+         * C2's density) costs more to stage than its lanes read on their own:
+         * above TILE_UMAX photons the group's lanes scan their own cells */
+        if (U > (uint32_t)TILE_UMAX) { direct = direct || mine; continue; }
         const uint32_t gofs = B - pre; /* photon index of concatenated position t in row u: t + gofs_u */
         /* this lane's rows as two runs of the concatenation: rows (y0, z) and
          * (y0 + 1, z) are neighbours in the union, so each z-layer of the

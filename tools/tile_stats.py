@@ -7,17 +7,19 @@ sys.path.insert(0, os.path.join(R, "cuda-raytrace_amd"))
 import torch  # noqa: F401
 from pmrender import hip, scenes
 from pmrender.abi import RenderParams
-sc = scenes.cornell_box(1920, 1080)
+C5 = "c5" in sys.argv[1:]
+sc = scenes.caustic_scene(1920, 1080) if C5 else scenes.cornell_box(1920, 1080)
 ctx = sc.load_into(hip.Context(0))
-KNN = len(sys.argv) > 1 and sys.argv[1] == "knn"
+KNN = "knn" in sys.argv[1:]
+PATHS = 1_048_576 if C5 else 262144
 if KNN:
     from pmrender.abi import PM_ESTIMATOR_KNN
-    p = RenderParams.defaults(paths_per_pass=262144, initial_radius2=100.0, estimator=PM_ESTIMATOR_KNN, knn_lookup=50)
+    p = RenderParams.defaults(paths_per_pass=PATHS, initial_radius2=100.0, estimator=PM_ESTIMATOR_KNN, knn_lookup=50)
 else:
-    p = RenderParams.defaults(paths_per_pass=262144)
+    p = RenderParams.defaults(paths_per_pass=PATHS)
 ctx.eye_pass(p)
-ctx.trace_photons(p, 0, 0, 262144)
-ctx.build_photon_map(p, 262144 * 4)
+ctx.trace_photons(p, 0, 0, PATHS)
+ctx.build_photon_map(p, PATHS * 4)
 ctx.synchronize()
 ctx.trace_profile(reset=True)
 ctx.gather(p)
