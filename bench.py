@@ -307,7 +307,7 @@ def main():
         # every valid photon read once (40 B) — the HBM floor of the gather
         compulsory = 92 * act + 40 * n_valid
         achieved = compulsory / (gather_ms * 1e-3) / 1e9
-        traffic, traffic_src = load_pmc_traffic(kernel_name, args.config)
+        traffic, traffic_src = load_pmc_traffic(kernel_name, args.config + ("_knn" if knn else ""))
         if knn:
             l1_bytes = 72 * act + 16 * inactive + 8 * rows + 16 * vis + 28 * hits
             l1_formula = "72*G_act + 16*G_inactive + 8*bucket_rows + 16*photons_tested + 28*photons_found"
@@ -319,7 +319,8 @@ def main():
             l1_formula = "72*G_act + 16*G_inactive + 16*kd_nodes_visited + 24*photons_in_radius"
         roofline = {
             "bound": "hbm",
-            "kernel": "k_gather_knn<0> (pbrt LPhoton kNN, fused record update)" if knn
+            "kernel": "k_gather_knn_tile (pbrt LPhoton kNN: LDS tile unions, exact histogram selection of r_k^2, "
+                      "fused record update)" if knn
             else "k_gather_tile<0,1> (LDS-staged range query + fused PPM update)" if structure == PM_GATHER_GRID
             else "k_gather_kd<0,0>",
             "achieved": round(achieved, 1),
@@ -337,8 +338,10 @@ def main():
             # tests): what the L1 / LDS deliver, not HBM traffic
             "l1_delivered": {"bytes_per_launch": int(l1_bytes), "formula": l1_formula,
                              "GBs": round(l1_bytes / (gather_ms * 1e-3) / 1e9, 1)},
-            "limiter": "VALU issue + per-wave latency (profiles/r02 counters): the kernel reads each record "
-                       "once and each tile's photons once, so HBM is not what bounds it",
+            "limiter": ("VALU issue (profiles/r02 counters): ~3 selection passes over each tile's staged union, "
+                        "every lane testing every staged photon — arithmetic, not memory" if knn else
+                        "VALU issue + per-wave latency (profiles/r02 counters): the kernel reads each record "
+                        "once and each tile's photons once, so HBM is not what bounds it"),
         }
         if traffic is not None:
             roofline["traffic_GBs"] = round(traffic / (gather_ms * 1e-3) / 1e9, 1)
@@ -379,7 +382,10 @@ def main():
         tbytes = 40 * deposits + 32 * nodes + 36 * prims
         tach = tbytes / (stages["trace"] * 1e-3) / 1e9
         trace_roofline = {
-            "bound": "hbm", "kernel": "k_trace_lane<0,MODE_GLOBAL|MODE_LDS>", "achieved": round(tach, 1), "peak": HBM_PEAK_GBS,
+            "bound": "hbm",
+            "kernel": ("k_trace_pool (4-wide BVH in HBM / MALL, pooled paths)" if ctx.scene_info()["mode"] == "bvh-hbm"
+                       else "k_trace_lane<0,MODE_LDS>"),
+            "achieved": round(tach, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(tach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": int(tbytes),
             "formula": "40*deposits + 32*bvh_nodes + 36*prim_tests (SURVEY.md §8d B_trace)",
             "units": {"rays": rays, "bvh_nodes": nodes, "prim_tests": prims, "deposits": deposits},
