@@ -187,9 +187,18 @@ def main():
 
     import torch  # first: the renderer then shares torch's HIP runtime (one runtime per process)
     import torch.distributed as dist
+    # rehearsal knobs for the N > 1 path on a 1-GPU box (not for measurement):
+    # PM_BENCH_ONE_DEVICE=1 puts every rank on device 0, PM_BENCH_BACKEND=gloo
+    # replaces RCCL (which needs one GPU per rank)
+    if os.environ.get("PM_BENCH_ONE_DEVICE") == "1":
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("PM_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from pmrender import hip
     from pmrender.abi import PM_ESTIMATOR_KNN, PM_ESTIMATOR_PPM, PM_GATHER_GRID, PM_GATHER_KDTREE, \
