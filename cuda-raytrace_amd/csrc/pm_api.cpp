@@ -791,7 +791,11 @@ int pm_commit(void *ptr) {
     S.stack_depth = std::min(BVH_STACK, std::max(2, c->bvh_depth + 2));
     S.wide = wide;
     S.wnodes = wide ? (const float4 *)(base + o_wnodes) : nullptr;
-    if (wide) S.stack_depth = std::min(BVH_STACK, std::max(S.stack_depth, wide_stack + 1));
+    /* wide scenes traverse only the 4-wide tree (traverse() dispatches every
+     * MODE_GLOBAL query to traverse4): its exact stack bound sizes the LDS
+     * stacks, not the binary tree's depth — k_trace_pool's 256-thread blocks
+     * then fit four per CU (its VGPR occupancy) instead of three */
+    if (wide) S.stack_depth = std::min(BVH_STACK, std::max(2, wide_stack + 1));
     for (int a = 0; a < 3; ++a) { c->bbox_lo[a] = blo[a]; c->bbox_hi[a] = bhi[a]; }
     double em = 0.0, kd = 1.0;
     for (const LightDev &L : c->lights) {
