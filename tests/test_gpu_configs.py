@@ -172,3 +172,36 @@ def test_c5_progressive(oracle_mod, hip_mod):
         assert rmse(img, ref_img) < 1e-3
     finally:
         ctx.close()
+
+
+def test_c2_full_knn(oracle_mod, hip_mod, monkeypatch):
+    """The kNN estimator at C2 size (1080p, 262,144 paths, K = 50, r^2 = 100,
+    the bench's kNN line): the tile kernel equals the per-lane heap kernel
+    bit for bit, and both match the oracle's pbrt kd-tree lookup (found
+    count and r_k^2 exact, flux to fp32 summation order)."""
+    from parity_util import compare_knn_records
+    from pmrender.abi import PM_ESTIMATOR_KNN
+    sc = scenes.cornell_box(1920, 1080)
+    orc = sc.load_into(oracle_mod.Oracle())
+    p = RenderParams.defaults(paths_per_pass=262_144, initial_radius2=100.0, estimator=PM_ESTIMATOR_KNN,
+                              knn_lookup=50)
+    recs = orc.eye_pass(p)
+    slots = orc.trace_photons(p, 0, 0, 262_144)
+    outs = {}
+    for name in ("lane", "tile"):
+        monkeypatch.setenv("PM_GATHER_KERNEL", name)
+        ctx = sc.load_into(hip_mod.Context(0))
+        try:
+            ctx.upload_records(recs)
+            ctx.upload_slots(slots)
+            ctx.build_photon_map(p, len(slots))
+            ctx.gather(p)
+            outs[name] = ctx.download_records()
+        finally:
+            ctx.close()
+    assert_bitexact(outs["tile"], outs["lane"], "C2 kNN tile vs per-lane")
+    ref = recs.copy()
+    orc.gather(orc.build_kdtree(slots), ref, p)
+    act = (ref["flags"] & 7) == 0
+    assert act.sum() > 1_000_000 and (ref["photon_count"][act] == 50).mean() > 0.2
+    compare_knn_records(outs["tile"], ref["photon_count"].astype(np.int64), ref["radius2"], ref["flux"])
