@@ -177,7 +177,7 @@ def _worker(rank, world, port, exchange, outdir):
     if exchange == "reduce":   # PPM state is owned per chunk of the active-record view
         owned = eng.view[runner.v_begin:runner.v_begin + runner.v_count]
     else:                      # the rank's interleaved 8-row bands
-        owned = np.concatenate([np.arange(b, b + c) for b, c in runner.bands[rank]])
+        owned = np.concatenate([np.arange(b, b + c) for b, c in runner.bands[rank]] + [np.zeros(0, np.int64)])
     np.save(os.path.join(outdir, f"idx{rank}.npy"), owned)
     np.save(os.path.join(outdir, f"recs{rank}.npy"), eng.recs[owned])
     np.save(os.path.join(outdir, f"img{rank}.npy"), out.numpy())
@@ -203,9 +203,10 @@ def _single_process_reference(world):
     return recs, orc.final(recs, float(PATHS * world * 2))
 
 
-@pytest.mark.parametrize("exchange", ["allgather", "reduce"])
-def test_two_rank_pass_matches_single_process(exchange, tmp_path):
-    world = 2
+@pytest.mark.parametrize("exchange,world", [("allgather", 2), ("reduce", 2), ("reduce", 4), ("allgather", 3)])
+def test_two_rank_pass_matches_single_process(exchange, world, tmp_path):
+    """world-size 2 (and 3 / 4: view chunks and bands that do not divide
+    evenly, as at N = 8) over gloo vs one process over the same global paths"""
     mp.start_processes(_worker, args=(world, _free_port(), exchange, str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
     ref_recs, ref_img = _single_process_reference(world)
