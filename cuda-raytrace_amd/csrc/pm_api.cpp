@@ -102,9 +102,12 @@ struct Ctx {
     DevBuf d_vflags, d_vrank, d_vlist, d_vsums;
     /* tiles (64 records) holding an active record, in record order: full-range
      * tile gathers launch over these only (records fixed after the eye pass) */
-    DevBuf d_tiles, d_tile_flags;
-    int64_t n_tiles = 0;
-    bool tiles_valid = false;
+    DevBuf d_tiles, d_tile_flags, d_tile_count;
+    int64_t n_tiles = 0;           /* valid once tile_count_known */
+    bool tiles_valid = false;      /* the list on the device matches the records */
+    bool tile_count_known = false; /* its length read back (pinned copy + event, never waited on) */
+    uint32_t *h_tile_count = nullptr;
+    hipEvent_t tile_event = nullptr;
     bool tile_list = true; /* env PM_TILE_LIST=0: launch over every tile */
     /* pm_reset_records is deferred: records read as (flux 0, N 0, r2 = rec_fresh_r2) */
     bool rec_fresh = false;
@@ -467,8 +470,10 @@ void pm_destroy(void *ptr) {
     DevBuf *bufs[] = {&c->d_scene, &c->d_rays, &c->d_rand2d, &c->d_pos, &c->d_nrm, &c->d_state, &c->d_n,
                       &c->d_dl, &c->d_slots, &c->d_count, &c->d_scratch, &c->d_vflags, &c->d_vrank, &c->d_vlist, &c->d_vsums,
                       &c->d_cell_start, &c->d_pha, &c->d_phb,
-                      &c->d_kd, &c->d_out, &c->d_counters};
+                      &c->d_kd, &c->d_out, &c->d_counters, &c->d_tiles, &c->d_tile_flags, &c->d_tile_count};
     for (DevBuf *b : bufs) b->release();
+    if (c->tile_event) (void)hipEventDestroy(c->tile_event);
+    if (c->h_tile_count) (void)hipHostFree(c->h_tile_count);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1038,26 +1043,33 @@ int pm_build_photon_map(void *ptr, const pm_render_params *p, int64_t n_slots, v
 }
 
 
-/* the tile list of the current records (flags on the device, ordered list
- * built on the host: one 1-byte-per-tile copy after each eye pass / upload) */
+/* the tile list of the current records, built on the device without a host
+ * wait: flags + an in-order compaction, its length copied to pinned memory
+ * behind an event. Until that copy has landed (hipEventQuery, never waited
+ * on) the gather kernels read the length from device memory and the grid
+ * covers every tile. */
 static int ensure_tiles(Ctx *c, hipStream_t s) {
-    if (c->tiles_valid) return PM_OK;
-    const int64_t nt = (c->nrec + 63) / 64;
-    HIPCHK(c, c->d_tile_flags.ensure(std::max<int64_t>(nt, 16)));
-    HIPCHK(c, c->d_tiles.ensure(std::max<int64_t>(nt * 4, 16)));
-    HIPCHK(c, launch_tile_flags(recs(c), c->d_tile_flags.as<uint8_t>(), s));
-    std::vector<uint8_t> f((size_t)nt);
-    HIPCHK(c, hipMemcpyAsync(f.data(), c->d_tile_flags.p, (size_t)nt, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    std::vector<uint32_t> list;
-    list.reserve((size_t)nt);
-    for (int64_t t = 0; t < nt; ++t)
-        if (f[(size_t)t]) list.push_back((uint32_t)t);
-    if (!list.empty())
-        HIPCHK(c, hipMemcpyAsync(c->d_tiles.p, list.data(), list.size() * 4, hipMemcpyHostToDevice, s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    c->n_tiles = (int64_t)list.size();
-    c->tiles_valid = true;
+    if (!c->tiles_valid) {
+        const int64_t nt = (c->nrec + 63) / 64;
+        HIPCHK(c, c->d_tile_flags.ensure(std::max<int64_t>(nt, 16)));
+        HIPCHK(c, c->d_tiles.ensure(std::max<int64_t>(nt * 4, 16)));
+        HIPCHK(c, c->d_tile_count.ensure(16));
+        if (!c->h_tile_count) HIPCHK(c, hipHostMalloc((void **)&c->h_tile_count, 4, hipHostMallocDefault));
+        if (!c->tile_event) HIPCHK(c, hipEventCreateWithFlags(&c->tile_event, hipEventDisableTiming));
+        /* a previous list's length still in flight (records replaced before
+         * any gather read it): let that copy land before the pinned word is reused */
+        else if (!c->tile_count_known) HIPCHK(c, hipEventSynchronize(c->tile_event));
+        HIPCHK(c, launch_tile_list(recs(c), c->d_tile_flags.as<uint8_t>(), c->d_tiles.as<uint32_t>(),
+                                   c->d_tile_count.as<uint32_t>(), s));
+        HIPCHK(c, hipMemcpyAsync(c->h_tile_count, c->d_tile_count.p, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipEventRecord(c->tile_event, s));
+        c->tiles_valid = true;
+        c->tile_count_known = false;
+    }
+    if (!c->tile_count_known && hipEventQuery(c->tile_event) == hipSuccess) {
+        c->n_tiles = (int64_t)*c->h_tile_count;
+        c->tile_count_known = true;
+    }
     return PM_OK;
 }
 
@@ -1092,7 +1104,8 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
         p->gather_structure == PM_GATHER_GRID && ((!partial && !split) || c->view_active)) {
         if ((rc = ensure_tiles(c, s))) return rc;
         G.tiles = c->d_tiles.as<uint32_t>();
-        G.n_tiles = c->n_tiles;
+        if (c->tile_count_known) { G.n_tiles = c->n_tiles; G.n_tiles_dev = nullptr; }
+        else { G.n_tiles = (c->nrec + 63) / 64; G.n_tiles_dev = c->d_tile_count.as<uint32_t>(); }
     }
     if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters.p, 0, 32, s));
     timer_begin(c, "gather", s);

@@ -369,7 +369,7 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
     int64_t r;
     if (P.tiles) { /* only tiles with an active record (no block-level barrier below: a wave may leave) */
         const int64_t w = (int64_t)blockIdx.x * (GATHER_BLOCK / 64) + (threadIdx.x >> 6);
-        if (w >= P.n_tiles) return;
+        if (w >= (P.n_tiles_dev ? (int64_t)*P.n_tiles_dev : P.n_tiles)) return;
         r = P.rec_begin + (int64_t)P.tiles[w] * 64 + lane;
     } else {
         r = P.rec_begin + gather_block(P) * GATHER_BLOCK + threadIdx.x;
@@ -985,6 +985,7 @@ struct KnnSel {
 __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
     __shared__ KnnLds L;
     const int lane = threadIdx.x & 63;
+    if (P.tiles && P.n_tiles_dev && (int64_t)blockIdx.x >= (int64_t)*P.n_tiles_dev) return; /* one wave per block */
     const int64_t r = P.rec_begin + (P.tiles ? (int64_t)P.tiles[blockIdx.x] * 64 + lane
                                              : (int64_t)blockIdx.x * KNN_BLOCK + threadIdx.x);
     const GridDesc &g = P.grid;
@@ -1700,9 +1701,38 @@ __global__ __launch_bounds__(256) void k_tile_flags(RecordsDev R, uint8_t *flags
     const unsigned long long m = __ballot(act);
     if ((threadIdx.x & 63) == 0 && r < R.count) flags[r >> 6] = m != 0ull ? 1 : 0;
 }
-hipError_t launch_tile_flags(const RecordsDev &R, uint8_t *flags, hipStream_t s) {
+/* one block compacts the flags in order: 1024 tiles per step, ballot ranks
+ * inside each wave, wave totals through LDS */
+__global__ __launch_bounds__(1024) void k_tile_compact(const uint8_t *flags, int64_t nt, uint32_t *list,
+                                                       uint32_t *count) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t base;
+    if (threadIdx.x == 0) base = 0u;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    for (int64_t t0 = 0; t0 < nt; t0 += 1024) {
+        const int64_t t = t0 + threadIdx.x;
+        const bool f = t < nt && flags[t] != 0;
+        const unsigned long long m = __ballot(f);
+        if (lane == 0u) wsum[w] = (uint32_t)__builtin_popcountll(m);
+        __syncthreads();
+        uint32_t off = base;
+        for (uint32_t k = 0; k < w; ++k) off += wsum[k];
+        if (f) list[off + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull))] = (uint32_t)t;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tot = 0u;
+            for (int k = 0; k < 16; ++k) tot += wsum[k];
+            base += tot;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *count = base;
+}
+hipError_t launch_tile_list(const RecordsDev &R, uint8_t *flags, uint32_t *list, uint32_t *count, hipStream_t s) {
     if (R.count <= 0) return hipSuccess;
     pm_launch(k_tile_flags, dim3((unsigned)((R.count + 255) / 256)), dim3(256), 0, s, R, flags);
+    pm_launch(k_tile_compact, dim3(1), dim3(1024), 0, s, (const uint8_t *)flags, (R.count + 63) / 64, list, count);
     return hipGetLastError();
 }
 

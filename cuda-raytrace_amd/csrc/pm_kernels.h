@@ -152,6 +152,9 @@ struct GatherParams {
      * hold an active record, in record order */
     const uint32_t *tiles;
     int64_t n_tiles;
+    /* non-null: the list's length is this device word (the host has not read
+     * it back yet); n_tiles then bounds the grid (every tile) */
+    const uint32_t *n_tiles_dev;
 };
 
 struct FinalParams {
@@ -192,8 +195,9 @@ hipError_t launch_ppm_update(const GatherParams &p, const long long *partial, in
 hipError_t launch_ppm_update_split(const GatherParams &p, const int *count, const long long *flux, int64_t n_view,
                                    int64_t v_begin, int64_t v_count, int fresh, hipStream_t s);
 hipError_t launch_final(const FinalParams &p, hipStream_t s);
-/* flags[t] = 1 when tile t (records [64 t, 64 t + 64)) holds an active record */
-hipError_t launch_tile_flags(const RecordsDev &R, uint8_t *flags, hipStream_t s);
+/* list[0 .. *count) = the tiles (records [64 t, 64 t + 64)) holding an
+ * active record, ascending, built on the device (flags: one byte per tile) */
+hipError_t launch_tile_list(const RecordsDev &R, uint8_t *flags, uint32_t *list, uint32_t *count, hipStream_t s);
 hipError_t launch_radius2_io(const RecordsDev &R, float *buf, int64_t rec_begin, int64_t rec_count, int to_records,
                              const uint32_t *view, hipStream_t s);
 /* exclusive scan of n uint32 (pm_bucket.hip); in/out 16-B aligned; sums: scan_scratch_words(n) */
