@@ -82,7 +82,7 @@ def build_scene(cfg):
 
 
 def kernel_src_sha():
-    """Hash of the HIP sources: a committed PMC profile is this build's only if it matches."""
+    """Hash of the HIP sources and their build flags: a committed PMC profile is this build's only if it matches."""
     import hashlib
     h = hashlib.sha256()
     csrc = os.path.join(ROOT, "cuda-raytrace_amd", "csrc")
@@ -90,6 +90,8 @@ def kernel_src_sha():
         if f.endswith((".hip", ".h", ".cpp")):
             with open(os.path.join(csrc, f), "rb") as fh:
                 h.update(f.encode() + fh.read())
+    with open(os.path.join(ROOT, "cuda-raytrace_amd", "Makefile"), "rb") as fh:  # compile flags
+        h.update(b"Makefile" + fh.read())
     return h.hexdigest()[:16]
 
 

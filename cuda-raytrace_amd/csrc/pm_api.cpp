@@ -946,18 +946,19 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
     T.per_block = c->trace_per_block;
     T.wave_paths = c->trace_wave_paths;
     if (c->trace_pool && T.per_block == 0) {
-        /* pooled kernel: one occupancy round — 4 waves per SIMD (122 VGPRs),
-         * 4 SIMDs per CU — each wave with a contiguous pool of a multiple of
-         * 64 paths. C3 sweep (1M paths, 256 CUs): 4096 waves 5.25 ms, 8192
+        /* pooled kernel: one occupancy round (resident waves per CU from the
+         * occupancy API: VGPRs and the LDS stacks) — each wave with a
+         * contiguous pool of a multiple of 64 paths. C3 sweep (1M paths, 256 CUs): 4096 waves 5.25 ms, 8192
          * (two rounds) 5.81, 5462 (1.33 rounds) 6.73, 2048 7.22 */
         int64_t waves = c->pool_waves;
         if (waves <= 0) {
             int cus = 0;
             if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0) cus = 256;
-            waves = (int64_t)cus * 16;
+            const int per_cu = trace_pool_waves_per_cu((size_t)c->S.stack_depth * TRACE_BLOCK * 4 + c->S.lds_bytes);
+            waves = (int64_t)cus * (per_cu > 0 ? per_cu : 16);
         }
-        int64_t per = (path_count + waves - 1) / waves;
-        per = std::max<int64_t>(64, (per + 63) / 64 * 64);
+        /* any pool size works (the wave's cursor hands out paths to dead lanes) */
+        const int64_t per = std::max<int64_t>(1, (path_count + waves - 1) / waves);
         T.pool_paths = per;
     }
     T.refill_min = c->trace_refill_min;

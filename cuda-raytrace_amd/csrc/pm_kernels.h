@@ -177,6 +177,8 @@ hipError_t launch_eye(const EyeParams &p, hipStream_t s);
  * (float3, raster / sample order); only p.R.count of the records is read */
 hipError_t launch_simple(const EyeParams &p, float *out, hipStream_t s);
 /* writes every slot of its paths (deposits, then zeros); count: census */
+/* resident waves of k_trace_pool per CU with `lds` bytes of dynamic LDS per block */
+int trace_pool_waves_per_cu(size_t lds);
 hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s);
 /* photon-bucket build (pm_bucket.hip): count + rank, scan, fill.
  * count and cell_start have ncells + 1 entries; cell_start[ncells] = valid

@@ -564,7 +564,12 @@ constexpr int POOL_STEPS = 4, POOL_SHADE_MIN = PM_POOL_SHADE_MIN;
 enum { PHASE_DEAD = 0, PHASE_TRAV = 1, PHASE_SHADE = 2 };
 
 template <int COUNT>
-__global__ __launch_bounds__(TRACE_BLOCK) void k_trace_pool(TraceParams P) { /* 122 VGPRs: 4 waves/SIMD (5 spill: slower) */
+#ifdef PM_POOL_EU /* experiment: make variant VFLAGS=-DPM_POOL_EU=5 */
+#define POOL_OCC __attribute__((amdgpu_waves_per_eu(PM_POOL_EU, PM_POOL_EU)))
+#else
+#define POOL_OCC
+#endif
+__global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams P) { /* ~102 VGPRs without SLP: 4 waves/SIMD */
     extern __shared__ __attribute__((aligned(16))) int stk[];
     __shared__ uint32_t perm[28];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -643,6 +648,13 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_pool(TraceParams P) { /* 
         else pm_launch((KERNEL<0, MODE_GLOBAL>), GRID, BLOCK, LDS, STREAM, PARAMS);                     \
         break;                                                                                                   \
     }
+
+/* resident waves of the pooled kernel per CU at this LDS size (0 if unknown) */
+int trace_pool_waves_per_cu(size_t lds) {
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0>, TRACE_BLOCK, lds) != hipSuccess) return 0;
+    return blocks * (TRACE_BLOCK / 64);
+}
 
 hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s) {
     if (p.path_count <= 0) return hipSuccess;
