@@ -33,7 +33,13 @@
 
 namespace pm {
 
-constexpr int SCAN_BLOCK = 256, SCAN_ITEMS = 16, SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS; /* 4096 u32 per block */
+/* 2048 counters per block: at C2's 2.7 M cells, 1,320 blocks instead of 660
+ * with 16 per thread (build 37.2 -> 34.3 us: the scan kernels were short of
+ * waves to hide their latency); 4 per thread measured the same */
+#ifndef PM_SCAN_ITEMS
+#define PM_SCAN_ITEMS 8
+#endif
+constexpr int SCAN_BLOCK = 256, SCAN_ITEMS = PM_SCAN_ITEMS, SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
 
 __global__ __launch_bounds__(256) void k_bucket_count(const pm_photon *slots, int64_t n, GridDesc g,
                                                       uint32_t *count, uint32_t *key_out, uint32_t *rank_out) {
@@ -81,7 +87,7 @@ PMD uint32_t block_excl_scan(uint32_t v, uint32_t *excl, uint32_t *lds /* >= 4 *
     return tot;
 }
 
-/* per-tile sums; thread t owns 16 contiguous words (four 16-B loads) */
+/* per-tile sums; thread t owns SCAN_ITEMS contiguous words (16-B loads) */
 __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_reduce(const uint32_t *in, int64_t n, uint32_t *sums) {
     __shared__ uint32_t lds[4];
     const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
