@@ -924,8 +924,8 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn(GatherParams P) {
  *    interval into 32 bins of a monotone bin function (float subtract,
  *    multiply, clamp, truncate: every step is monotone, so a bin is an
  *    interval of d^2 values) with one LDS add per photon; a prefix walk finds
- *    the bin holding the K-th. COLLECT then keeps that bin's values (<= 8, in
- *    LDS) with their min and max: <= 8 values are ranked directly, equal
+ *    the bin holding the K-th. COLLECT then keeps that bin's values (<= 12,
+ *    in LDS) with their min and max: <= 12 values are ranked directly, equal
  *    values are the answer, otherwise [min, max] is re-binned (the extremes
  *    land in bins 0 and 31, so every level shrinks the set). A deep or
  *    overflowing (>= 2^16 photons) search extracts minima one by one instead.
@@ -944,11 +944,17 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn(GatherParams P) {
 #define PM_KT_GROUP_MIN 12
 #endif
 constexpr int KT_CAP = PM_KT_CAP;  /* photons per LDS window (one per lane) */
+/* bins / kept values (C2 kNN, ms): 64/8 1.25, 48/8 1.12, 32/16 1.10, 24/12
+ * 1.08, 32/10 1.07, 32/12 1.03 — 32/12 keeps the LDS at ~9.8 KB per wave
+ * (4 waves/SIMD, the VGPR limit) with few re-binning passes */
 #ifndef PM_KT_BINS
-#define PM_KT_BINS 64
+#define PM_KT_BINS 32
 #endif
 constexpr int KT_BINS = PM_KT_BINS; /* histogram bins per pass */
-constexpr int KT_LIST = 8;         /* values a COLLECT pass keeps per lane */
+#ifndef PM_KT_LIST
+#define PM_KT_LIST 12
+#endif
+constexpr int KT_LIST = PM_KT_LIST; /* values a COLLECT pass keeps per lane */
 constexpr int KT_LEVELS = 4;       /* re-binning levels before minimum extraction */
 constexpr uint32_t KT_GROUP_R = 1; /* lane boxes span <= 5 cells: a group's union <= 7 per axis */
 constexpr int KT_GROUP_MIN = PM_KT_GROUP_MIN;
