@@ -352,8 +352,10 @@ PMD void union_box(const GridDesc &g, const GatherRec &R, bool in, uint32_t &X0,
  * leader's: y rows [ly - R, ly + R + 1] fit the row pitch 8, z layers x 8
  * rows fit the 64 lanes */
 constexpr uint32_t GROUP_R = PM_GROUP_R;
+/* C2 gather: 12 -> 51.9 us, 8 -> 51.3, 4 -> 48.5, 2 -> 48.8, 1 -> 48.9 (C3
+ * unchanged): a small LDS group still beats its lanes scanning per lane */
 #ifndef PM_GROUP_MIN
-#define PM_GROUP_MIN 12
+#define PM_GROUP_MIN 4
 #endif
 constexpr int GROUP_MIN = PM_GROUP_MIN;
 #ifndef PM_TILE_UMAX
