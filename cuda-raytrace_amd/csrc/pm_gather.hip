@@ -942,8 +942,11 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn(GatherParams P) {
 #ifndef PM_KT_CAP
 #define PM_KT_CAP 64
 #endif
+/* C2 kNN: 12 -> 1.07 ms, 4 -> 0.99, 1 -> 0.95: every lane gets an LDS group
+ * (its own if need be); per-lane passes remain for grids too coarse for the
+ * row map */
 #ifndef PM_KT_GROUP_MIN
-#define PM_KT_GROUP_MIN 12
+#define PM_KT_GROUP_MIN 1
 #endif
 constexpr int KT_CAP = PM_KT_CAP;  /* photons per LDS window (one per lane) */
 /* bins / kept values (C2 kNN, ms): 64/8 1.25, 48/8 1.12, 32/16 1.10, 24/12
