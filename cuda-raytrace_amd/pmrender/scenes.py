@@ -12,6 +12,8 @@ bit-identical inputs.
   cudamaterial.cpp:40), numpy seed 1 (C3).
 * caustic_scene: Cornell box + glass sphere r=100 (+ mirror sphere) (C5
   substitute; killeroo/caustic-glass .pbrt files are not in the container).
+* figure_scene: Cornell enclosure + two instances of a procedural 5,120-
+  triangle closed mesh (killeroo substitute, scenes/killeroo-proxy.pbrt).
 """
 import math
 from dataclasses import dataclass, field
@@ -188,6 +190,62 @@ def caustic_scene(W=256, H=256, mirror=True):
         mir = s.material(PM_MIRROR, (0.9, 0.9, 0.9))
         o2w, w2o = translate(150.0, 90.0, 380.0)
         s.spheres.append((np.float32(90.0), o2w, w2o, mir, -1))
+    return s
+
+
+FIGURE_INSTANCES = ((180.0, 0.0, 200.0), (370.0, 0.0, 340.0))
+
+
+def figure_mesh(subdiv=4):
+    """Killeroo substitute (the killeroo mesh is not in the container): a
+    closed, smoothly bumped blob — an icosphere subdivided `subdiv` times
+    (20 * 4^subdiv triangles), displaced radially and scaled to ~140 x 180 x
+    110 units, resting above y = 0. Coordinates are multiples of 1/64, so the
+    float32 values round-trip through a .pbrt file's decimal text exactly."""
+    t = (1.0 + math.sqrt(5.0)) / 2.0
+    V = [(-1, t, 0), (1, t, 0), (-1, -t, 0), (1, -t, 0), (0, -1, t), (0, 1, t), (0, -1, -t), (0, 1, -t),
+         (t, 0, -1), (t, 0, 1), (-t, 0, -1), (-t, 0, 1)]
+    V = [np.asarray(v, np.float64) / np.linalg.norm(v) for v in V]
+    F = [(0, 11, 5), (0, 5, 1), (0, 1, 7), (0, 7, 10), (0, 10, 11), (1, 5, 9), (5, 11, 4), (11, 10, 2), (10, 7, 6),
+         (7, 1, 8), (3, 9, 4), (3, 4, 2), (3, 2, 6), (3, 6, 8), (3, 8, 9), (4, 9, 5), (2, 4, 11), (6, 2, 10),
+         (8, 6, 7), (9, 8, 1)]
+    for _ in range(subdiv):
+        mid = {}
+
+        def midpoint(a, b):
+            k = (min(a, b), max(a, b))
+            if k not in mid:
+                m = V[a] + V[b]
+                V.append(m / np.linalg.norm(m))
+                mid[k] = len(V) - 1
+            return mid[k]
+
+        F2 = []
+        for a, b, c in F:
+            ab, bc, ca = midpoint(a, b), midpoint(b, c), midpoint(c, a)
+            F2 += [(a, ab, ca), (b, bc, ab), (c, ca, bc), (ab, bc, ca)]
+        F = F2
+    P = np.asarray(V)
+    x, y, z = P[:, 0], P[:, 1], P[:, 2]
+    r = 1.0 + 0.18 * np.sin(3.0 * x + 1.0) * np.cos(2.0 * y) + 0.12 * np.sin(4.0 * z) * np.sin(2.0 * x + y)
+    P = P * r[:, None] * np.asarray([70.0, 90.0, 55.0])
+    P[:, 1] -= P[:, 1].min() - 1.0
+    P = np.round(P * 64.0) / 64.0
+    return P.astype(np.float32), np.asarray(F, np.int32)
+
+
+def figure_scene(W=256, H=256, subdiv=4):
+    """killeroo-proxy.pbrt as an in-code scene: the Cornell enclosure and
+    ceiling light with two instances of `figure_mesh` (pbrt ObjectInstance,
+    flattened to world space like the adapter, translations only) in a
+    bluish matte. The BVH exceeds the 16 KB LDS budget, so this is a global
+    (4-wide BVH, pooled trace kernel) scene of moderate size."""
+    s = cornell_box(W, H, blocks=False)
+    blue = s.material(PM_MATTE, (0.5, 0.5, 0.8))
+    P, idx = figure_mesh(subdiv)
+    for t in FIGURE_INSTANCES:
+        s.meshes.append(dict(P=(P + np.float32(t)).astype(np.float32), idx=idx, N=None, uv=None,
+                             material=blue, light=-1))
     return s
 
 

@@ -418,12 +418,14 @@ def test_grid_gather_independent_of_photon_order(cornell):
     assert_bitexact(outs[0], outs[1], "records after permuted-photon gather")
 
 
-@pytest.mark.parametrize("builder", ["caustic", "feature", "soup"])
+@pytest.mark.parametrize("builder", ["caustic", "feature", "soup", "figure"])
 def test_scene_parity(builder, oracle_mod, hip_mod):
     if builder == "caustic":
         sc = scenes.caustic_scene(96, 64)
     elif builder == "feature":
         sc = scenes.feature_scene(72, 40)
+    elif builder == "figure":   # killeroo substitute: instanced 5,120-triangle mesh, 4-wide BVH + pooled trace
+        sc = scenes.figure_scene(80, 64)
     else:
         sc = scenes.triangle_soup(20000, 80, 48)
     ctx, orc = make_pair(sc, oracle_mod, hip_mod)

@@ -94,6 +94,31 @@ def test_caustic_pbrt_is_the_c5_substitute():
     assert d["passes"] == 4 and d["warnings"] == 0, err
 
 
+def test_killeroo_proxy_pbrt_is_the_figure_scene():
+    """scenes/killeroo-proxy.pbrt (killeroo substitute): one figure mesh
+    defined inside ObjectBegin and two ObjectInstance calls whose
+    translations, applied as the adapter flattens instances, give exactly
+    figure_scene()'s meshes."""
+    d, err = dump(os.path.join(SCENES, "killeroo-proxy.pbrt"))
+    sc = scenes.figure_scene(256, 256)
+    calls = d["calls"]
+    proto = [c for c in calls if c["call"] == "shape" and c.get("instance", -1) == 0]
+    insts = [c for c in calls if c["call"] == "instance"]
+    assert len(proto) == 1 and len(insts) == len(scenes.FIGURE_INSTANCES) == 2
+    P, idx = scenes.figure_mesh()
+    np.testing.assert_array_equal(f32(proto[0]["P"]), P.reshape(-1))
+    np.testing.assert_array_equal(np.int32(proto[0]["indices"]), idx.reshape(-1))
+    np.testing.assert_array_equal(f32(proto[0]["k"]), f32([0.5, 0.5, 0.8]))
+    figs = sc.meshes[-2:]
+    for inst, want in zip(insts, figs):
+        m = f32(inst["o2w"]).reshape(4, 4)
+        assert np.array_equal(m[:3, :3], np.eye(3, dtype=np.float32))
+        np.testing.assert_array_equal((P + m[:3, 3]).astype(np.float32), want["P"])
+    assert sc.num_triangles == 10 + 2 * len(idx) and len(idx) == 5120
+    check_camera(d, sc.camera)
+    assert d["warnings"] == 0, err
+
+
 def test_pbrt_transform_and_state_semantics(tmp_path):
     d, err = parse_text(tmp_path, """
         LookAt 0 0 0  0 0 1  0 1 0
@@ -220,7 +245,8 @@ def read_pfm(path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("scene,renderer", [("cornell-box", "photonmapping"), ("cornell-box", "simple"),
-                                            ("caustic-glass", "photonmapping"), ("caustic-glass", "simple")])
+                                            ("caustic-glass", "photonmapping"), ("caustic-glass", "simple"),
+                                            ("killeroo-proxy", "photonmapping"), ("killeroo-proxy", "simple")])
 def test_pbrt_render_matches_stage_driver(scene, renderer, tmp_path, hip_mod):
     paths, passes = 16384, 2
     out = tmp_path / "img.pfm"
@@ -229,7 +255,8 @@ def test_pbrt_render_matches_stage_driver(scene, renderer, tmp_path, hip_mod):
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     img = read_pfm(out)
-    sc = scenes.cornell_box(256, 256) if scene == "cornell-box" else scenes.caustic_scene(256, 256)
+    sc = {"cornell-box": scenes.cornell_box, "caustic-glass": scenes.caustic_scene,
+          "killeroo-proxy": scenes.figure_scene}[scene](256, 256)
     ctx = sc.load_into(hip_mod.Context(0))
     if renderer == "simple":
         ref, _ = ctx.render_simple(RenderParams.simple_defaults())
