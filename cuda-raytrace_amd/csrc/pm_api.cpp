@@ -762,9 +762,14 @@ int pm_commit(void *ptr) {
             const char *le = getenv("PM_BVH4_LEAF");
             Bvh4Out w;
             collapse_bvh4(bvh, le ? atoi(le) : 1, w);
+            /* node format fixed at build time (pm_device.h PM_BVH4_QUANT) */
+            std::vector<uint32_t> qn;
+            const bool quant = PM_BVH4_QUANT != 0;
+            if (quant && !quantize_bvh4(w.nodes, qn)) FAIL(c, PM_ERR_INVALID, "BVH leaf too large for quantized nodes");
             if (w.max_stack <= BVH_STACK) {
-                o_wnodes = put(w.nodes.data(), w.nodes.size() * sizeof(float));
-                wide = 1;
+                o_wnodes = quant ? put(qn.data(), qn.size() * sizeof(uint32_t))
+                                 : put(w.nodes.data(), w.nodes.size() * sizeof(float));
+                wide = quant ? 2 : 1;
                 wide_stack = w.max_stack;
                 c->bvh4_nodes = (int64_t)(w.nodes.size() / 32);
                 c->bvh4_depth = w.depth;

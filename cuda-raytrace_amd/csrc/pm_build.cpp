@@ -252,6 +252,57 @@ void collapse_bvh4(const BvhOut &bin, int leaf_prims, Bvh4Out &out) {
     out.max_stack = need + 1;
 }
 
+/* the device's decode of a quantized bound (traverse4 / trav_step) */
+static float qdecode(float o, uint32_t q, int e) { return o + (float)q * std::ldexp(1.0f, e); }
+
+bool quantize_bvh4(const std::vector<float> &nodes, std::vector<uint32_t> &q) {
+    const size_t nn = nodes.size() / 32;
+    q.assign(nn * 16, 0u);
+    for (size_t i = 0; i < nn; ++i) {
+        const float *n = &nodes[i * 32];
+        int codes[4], counts[4];
+        std::memcpy(codes, &n[24], sizeof(codes));
+        std::memcpy(counts, &n[28], sizeof(counts));
+        uint32_t *w = &q[i * 16];
+        uint32_t ebytes = 0;
+        for (int a = 0; a < 3; ++a) {
+            float lo = INFINITY, hi = -INFINITY;
+            for (int k = 0; k < 4; ++k)
+                if (counts[k] != -1) { lo = std::min(lo, n[4 * a + k]); hi = std::max(hi, n[4 * (3 + a) + k]); }
+            if (!(lo <= hi)) lo = hi = 0.f; /* no children (empty scene root) */
+            const double ext = (double)hi - (double)lo;
+            int e = -126;
+            while (e < 127 && std::ldexp(255.0, e) < ext) ++e;
+            const double s = std::ldexp(1.0, e);
+            std::memcpy(&w[a], &lo, 4);
+            ebytes |= (uint32_t)(e + 128) << (8 * a);
+            uint32_t ql = 0, qh = 0;
+            for (int k = 0; k < 4; ++k) {
+                uint32_t bl = 0, bh = 0;
+                if (counts[k] != -1) {
+                    const float clo = n[4 * a + k], chi = n[4 * (3 + a) + k];
+                    bl = (uint32_t)std::min(255.0, std::max(0.0, std::floor(((double)clo - lo) / s)));
+                    bh = (uint32_t)std::min(255.0, std::max(0.0, std::ceil(((double)chi - lo) / s)));
+                    while (bl > 0 && qdecode(lo, bl, e) > clo) --bl;
+                    while (bh < 255 && qdecode(lo, bh, e) < chi) ++bh;
+                    if (qdecode(lo, bl, e) > clo || qdecode(lo, bh, e) < chi) return false;
+                }
+                ql |= bl << (8 * k);
+                qh |= bh << (8 * k);
+            }
+            w[4 + a] = ql;
+            w[7 + a] = qh;
+        }
+        w[3] = ebytes;
+        for (int k = 0; k < 4; ++k) {
+            if (counts[k] > 32767) return false;
+            w[10 + k / 2] |= (uint32_t)(uint16_t)(int16_t)counts[k] << (16 * (k & 1));
+        }
+        std::memcpy(&w[12], codes, sizeof(codes));
+    }
+    return true;
+}
+
 void build_bvh(std::vector<BuildPrim> &prims, int max_depth, BvhOut &out, const BvhCost &cost) {
     out.nodes.clear();
     out.refs.clear();

@@ -55,6 +55,18 @@ struct Bvh4Out {
 };
 void collapse_bvh4(const BvhOut &bin, int leaf_prims, Bvh4Out &out);
 
+/* 64-B quantized copy of the 4-wide nodes (16 u32 per node, half the bytes
+ * of a node visit): [0..2] node origin o (float: min corner of its
+ * children), [3] per-axis step exponents e + 128 (bytes 0..2; step 2^e,
+ * 255 steps span the node); [4..9] lox loy loz hix hiy hiz, one byte per
+ * child (child k in byte k); [10..11] counts as int16 pairs (children 0|1,
+ * 2|3); [12..15] child codes. A bound decodes as o + q * 2^e in float
+ * (q * 2^e exact, one rounding in the add); q is floor / ceil of the exact
+ * offset, so by monotone rounding every decoded box contains the float box,
+ * which is checked here: the culling test only gets more conservative.
+ * Returns false if a node cannot be encoded (leaf count > 32767). */
+bool quantize_bvh4(const std::vector<float> &nodes, std::vector<uint32_t> &q);
+
 /* returns the number of nodes (= valid photons); nodes sized >= that */
 int64_t build_kdtree_pbrt(const pm_photon *slots, int64_t nslots, std::vector<pm_photon> &nodes);
 

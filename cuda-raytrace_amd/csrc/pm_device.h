@@ -93,11 +93,12 @@ struct SceneDev {
      * them with wave-uniform indices through the scalar cache into SGPRs */
     const float4 *tri_geo_g;
     const uint32_t *tri_id_g;
-    /* 4-wide BVH (8 float4 per node, pm_build.h collapse_bvh4) for scenes
+    /* 4-wide BVH (4 uint4 per quantized node, pm_build.h quantize_bvh4; 8
+     * float4 per node in PM_BVH4_QUANT=0 builds, collapse_bvh4) for scenes
      * traversed from HBM (MODE_GLOBAL) when wide != 0; the binary nodes stay
      * for the LDS modes */
     const float4 *wnodes;
-    int wide;
+    int wide;        /* 4-wide BVH in wnodes: 1 = 128-B float nodes, 2 = 64-B quantized (pm_build.h) */
     /* all arrays above are 16-B aligned sections of one blob in HBM */
     const char *blob;
     uint32_t blob_bytes;
@@ -569,6 +570,49 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
     }
     return ANY ? false : best.ref != 0xffffffffu;
 }
+/* entry distances of the four children of 4-wide node `cur` (INF: missed)
+ * and their codes / counts: 64-B quantized nodes (pm_build.h quantize_bvh4:
+ * each bound decoded as o + q * 2^e, a box containing the float one; S.wide
+ * == 2) or, in builds with PM_BVH4_QUANT=0, 128-B float nodes (S.wide == 1).
+ * C3 trace 5.16 -> 4.75 ms per 1M paths (same box): half the bytes per visit,
+ * 24 byte conversions + 24 multiply-adds more per node. */
+#ifndef PM_BVH4_QUANT
+#define PM_BVH4_QUANT 1 /* build-time node format: 1 = quantized 64-B nodes, 0 = 128-B float nodes */
+#endif
+PMD void node4_test(const SceneDev &S, int cur, const v3 &oinv, const v3 &inv, float tmin, float tmax, float t[4],
+                    int c[4], int n[4]) {
+    if (PM_BVH4_QUANT) {
+        const uint4 *nd = reinterpret_cast<const uint4 *>(S.wnodes) + 4 * cur;
+        const uint4 w0 = nd[0], w1 = nd[1], w2 = nd[2], w3 = nd[3];
+        const float ox = __uint_as_float(w0.x), oy = __uint_as_float(w0.y), oz = __uint_as_float(w0.z);
+        /* step 2^e: exponent field e + 127 = stored byte - 1 */
+        const float sx = __uint_as_float(((w0.w & 0xffu) - 1u) << 23);
+        const float sy = __uint_as_float((((w0.w >> 8) & 0xffu) - 1u) << 23);
+        const float sz = __uint_as_float((((w0.w >> 16) & 0xffu) - 1u) << 23);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t sh = 8u * (uint32_t)k;
+            const float lx = ox + (float)((w1.x >> sh) & 0xffu) * sx, ly = oy + (float)((w1.y >> sh) & 0xffu) * sy;
+            const float lz = oz + (float)((w1.z >> sh) & 0xffu) * sz, hx = ox + (float)((w1.w >> sh) & 0xffu) * sx;
+            const float hy = oy + (float)((w2.x >> sh) & 0xffu) * sy, hz = oz + (float)((w2.y >> sh) & 0xffu) * sz;
+            t[k] = box_near(lx, ly, lz, hx, hy, hz, oinv, inv, tmin, tmax);
+        }
+        c[0] = (int)w3.x; c[1] = (int)w3.y; c[2] = (int)w3.z; c[3] = (int)w3.w;
+        n[0] = (int)(int16_t)(w2.z & 0xffffu); n[1] = (int)(int16_t)(w2.z >> 16);
+        n[2] = (int)(int16_t)(w2.w & 0xffffu); n[3] = (int)(int16_t)(w2.w >> 16);
+    } else {
+        const float4 *nd = S.wnodes + 8 * cur;
+        const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
+        const int4 ch = *reinterpret_cast<const int4 *>(nd + 6), cn = *reinterpret_cast<const int4 *>(nd + 7);
+        t[0] = box_near(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, oinv, inv, tmin, tmax);
+        t[1] = box_near(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, oinv, inv, tmin, tmax);
+        t[2] = box_near(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, oinv, inv, tmin, tmax);
+        t[3] = box_near(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, oinv, inv, tmin, tmax);
+        c[0] = ch.x; c[1] = ch.y; c[2] = ch.z; c[3] = ch.w;
+        n[0] = cn.x; n[1] = cn.y; n[2] = cn.z; n[3] = cn.w;
+    }
+}
+
 /* 4-wide traversal (MODE_GLOBAL scenes with S.wide): one 128-B node per
  * visit, its four boxes tested at once; hit internal children are ordered
  * near to far with a sorting network, the nearest entered next and the rest
@@ -590,15 +634,9 @@ PMD bool traverse4(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int
         while (cur >= 0 && l0n == 0 && guard <= S.n_nodes) {
             ++guard;
             cen.node();
-            const float4 *nd = S.wnodes + 8 * cur;
-            const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
-            const int4 ch = *reinterpret_cast<const int4 *>(nd + 6), cn = *reinterpret_cast<const int4 *>(nd + 7);
-            float t[4] = {box_near(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, oinv, inv, ray.tmin, best.t),
-                          box_near(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, oinv, inv, ray.tmin, best.t),
-                          box_near(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, oinv, inv, ray.tmin, best.t),
-                          box_near(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, oinv, inv, ray.tmin, best.t)};
-            int c[4] = {ch.x, ch.y, ch.z, ch.w};
-            const int n[4] = {cn.x, cn.y, cn.z, cn.w};
+            float t[4];
+            int c[4], n[4];
+            node4_test(S, cur, oinv, inv, ray.tmin, best.t, t, c, n);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 if (t[k] != INF && n[k] > 0) { /* leaf: postpone */
@@ -664,15 +702,9 @@ PMD bool trav_step(const SceneDev &S, const Ray &ray, TravState &T, int *stack, 
     ++T.guard;
     cen.node();
     const float INF = __int_as_float(0x7f800000);
-    const float4 *nd = S.wnodes + 8 * T.cur;
-    const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
-    const int4 ch = *reinterpret_cast<const int4 *>(nd + 6), cn = *reinterpret_cast<const int4 *>(nd + 7);
-    float t[4] = {box_near(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, T.oinv, T.inv, ray.tmin, T.best.t),
-                  box_near(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, T.oinv, T.inv, ray.tmin, T.best.t),
-                  box_near(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, T.oinv, T.inv, ray.tmin, T.best.t),
-                  box_near(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, T.oinv, T.inv, ray.tmin, T.best.t)};
-    int c[4] = {ch.x, ch.y, ch.z, ch.w};
-    const int n[4] = {cn.x, cn.y, cn.z, cn.w};
+    float t[4];
+    int c[4], n[4];
+    node4_test(S, T.cur, T.oinv, T.inv, ray.tmin, T.best.t, t, c, n);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         if (t[k] != INF && n[k] > 0) {

@@ -353,11 +353,20 @@ PMD void union_box(const GridDesc &g, const GatherRec &R, bool in, uint32_t &X0,
  * rows fit the 64 lanes */
 constexpr uint32_t GROUP_R = PM_GROUP_R;
 /* C2 gather: 12 -> 51.9 us, 8 -> 51.3, 4 -> 48.5, 2 -> 48.8, 1 -> 48.9 (C3
- * unchanged): a small LDS group still beats its lanes scanning per lane */
+ * unchanged): a small LDS group still beats its lanes scanning per lane.
+ * Sparse maps are the exception: with under 1/SPARSE_CELLS photons per
+ * cell (C1: 52K photons in 2.7M cells) a lane's own cells hold almost
+ * nothing and a small group's staging overhead is the larger cost — C1 14.9
+ * us with 12, 34.9 us with 4 — so they keep groups of >= 12 lanes. The
+ * density is read on the device (cell_start[ncells] = photons in the map). */
 #ifndef PM_GROUP_MIN
 #define PM_GROUP_MIN 4
 #endif
-constexpr int GROUP_MIN = PM_GROUP_MIN;
+#ifndef PM_GROUP_MIN_SPARSE
+#define PM_GROUP_MIN_SPARSE 12
+#endif
+constexpr int GROUP_MIN = PM_GROUP_MIN, GROUP_MIN_SPARSE = PM_GROUP_MIN_SPARSE;
+constexpr uint32_t SPARSE_CELLS = 20;
 #ifndef PM_TILE_UMAX
 #define PM_TILE_UMAX 1024
 #endif
@@ -399,6 +408,8 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
      * tile across a depth edge two or three, never one huge box. */
     bool pend = R.small;
     bool direct = R.big; /* lanes that scan their own cells from global memory */
+    const int group_min =
+        (uint64_t)P.cell_start[g.ncells] * SPARSE_CELLS < (uint64_t)g.ncells ? GROUP_MIN_SPARSE : GROUP_MIN;
     while (true) {
         const unsigned long long pm = __ballot(pend);
         if (pm == 0ull) break;
@@ -418,7 +429,7 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
             /* an incoherent tile (lanes on many far-apart surfaces, e.g. a
              * triangle soup) would need a group per few lanes: below
              * GROUP_MIN lanes the rest scan their own cells per lane */
-            if (__builtin_popcountll(__ballot(mine)) < GROUP_MIN) {
+            if (__builtin_popcountll(__ballot(mine)) < group_min) {
                 direct = direct || pend;
                 break;
             }

@@ -1,0 +1,24 @@
+"""Quantized 4-wide BVH nodes (pm_build.h quantize_bvh4, 64 B per node): the
+encoder's boxes must contain the float boxes after the device's float decode,
+so the culling test stays conservative and closest hits are unchanged (the
+GPU side: test_gpu_parity scene tests on the soup / figure scenes, which
+traverse the quantized nodes). CPU only: compiles a small checker against
+pm_build.cpp."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "cuda-raytrace_amd", "csrc")
+
+
+@pytest.mark.parametrize("nprims", [1, 7, 50000])
+def test_quantized_boxes_contain_float_boxes(tmp_path, nprims):
+    exe = tmp_path / "qcheck"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", CSRC, "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "native", "bvh4_quant_check.cpp"), os.path.join(CSRC, "pm_build.cpp"),
+                    "-o", str(exe)], check=True, timeout=300)
+    r = subprocess.run([str(exe), str(nprims)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "bad 0" in r.stdout
