@@ -765,7 +765,8 @@ int pm_commit(void *ptr) {
             /* node format fixed at build time (pm_device.h PM_BVH4_QUANT) */
             std::vector<uint32_t> qn;
             const bool quant = PM_BVH4_QUANT != 0;
-            if (quant && !quantize_bvh4(w.nodes, qn)) FAIL(c, PM_ERR_INVALID, "BVH leaf too large for quantized nodes");
+            const char *lt = getenv("PM_LEAF_TRIS"); /* 0: every leaf through its refs (A/B knob) */
+            if (quant && !quantize_bvh4(w.nodes, lt && atoi(lt) == 0 ? std::vector<uint32_t>() : bvh.refs, qn)) FAIL(c, PM_ERR_INVALID, "BVH leaf too large for quantized nodes");
             if (w.max_stack <= BVH_STACK) {
                 o_wnodes = quant ? put(qn.data(), qn.size() * sizeof(uint32_t))
                                  : put(w.nodes.data(), w.nodes.size() * sizeof(float));

@@ -256,6 +256,10 @@ void collapse_bvh4(const BvhOut &bin, int leaf_prims, Bvh4Out &out) {
 static float qdecode(float o, uint32_t q, int e) { return o + (float)q * std::ldexp(1.0f, e); }
 
 bool quantize_bvh4(const std::vector<float> &nodes, std::vector<uint32_t> &q) {
+    return quantize_bvh4(nodes, std::vector<uint32_t>(), q);
+}
+
+bool quantize_bvh4(const std::vector<float> &nodes, const std::vector<uint32_t> &refs, std::vector<uint32_t> &q) {
     const size_t nn = nodes.size() / 32;
     q.assign(nn * 16, 0u);
     for (size_t i = 0; i < nn; ++i) {
@@ -295,7 +299,14 @@ bool quantize_bvh4(const std::vector<float> &nodes, std::vector<uint32_t> &q) {
         }
         w[3] = ebytes;
         for (int k = 0; k < 4; ++k) {
-            if (counts[k] > 32767) return false;
+            if (counts[k] >= LEAF_TRIS) return false;
+            if (counts[k] > 0 && !refs.empty()) { /* triangles-only leaf at consecutive slots? */
+                const uint32_t f = (uint32_t)~codes[k], s0 = refs[f] & 0x3fffffffu;
+                bool tris = true;
+                for (int j = 0; j < counts[k] && tris; ++j)
+                    tris = (refs[f + j] >> 30) == 0u && (refs[f + j] & 0x3fffffffu) == s0 + (uint32_t)j;
+                if (tris) { codes[k] = ~(int)s0; counts[k] |= LEAF_TRIS; }
+            }
             w[10 + k / 2] |= (uint32_t)(uint16_t)(int16_t)counts[k] << (16 * (k & 1));
         }
         std::memcpy(&w[12], codes, sizeof(codes));

@@ -66,6 +66,13 @@ void collapse_bvh4(const BvhOut &bin, int leaf_prims, Bvh4Out &out);
  * which is checked here: the culling test only gets more conservative.
  * Returns false if a node cannot be encoded (leaf count > 32767). */
 bool quantize_bvh4(const std::vector<float> &nodes, std::vector<uint32_t> &q);
+/* With the scene's refs (kind << 30 | storage index): a leaf whose refs
+ * are all triangles at consecutive storage slots s0, s0 + 1, ... is coded
+ * ~s0 with LEAF_TRIS set in its count, so the traversal tests
+ * tri_geo[s0 ..] directly, without loading the refs (one dependent load
+ * less per leaf). */
+constexpr int LEAF_TRIS = 0x4000;
+bool quantize_bvh4(const std::vector<float> &nodes, const std::vector<uint32_t> &refs, std::vector<uint32_t> &q);
 
 /* returns the number of nodes (= valid photons); nodes sized >= that */
 int64_t build_kdtree_pbrt(const pm_photon *slots, int64_t nslots, std::vector<pm_photon> &nodes);

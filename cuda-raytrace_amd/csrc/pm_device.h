@@ -467,6 +467,20 @@ PMD bool brute_isect(const SceneDev &S, const Ray &ray, Hit &best, C &cen) {
 /* Tests the primitives of one leaf; for ANY=true returns at the first hit. */
 template <bool ANY, class C>
 PMD bool leaf_isect(const SceneDev &S, uint32_t start, uint32_t count, const Ray &ray, Hit &best, C &cen) {
+    if (count & 0x4000u) { /* pm_build.h LEAF_TRIS: triangles at storage slots [start, start + n), no refs */
+        for (uint32_t idx = start; idx < start + (count & 0x3fffu); ++idx) {
+            cen.prim();
+            float t, b, g;
+            const bool ok = isect_tri(S.tri_geo + 3 * idx, ray, &t, &b, &g);
+            if (ANY) { if (ok) return true; continue; }
+            if (!ok || t > best.t) continue;
+            const uint32_t gid = S.tri_id[idx];
+            if (t < best.t || gid < best.gid) {
+                best.t = t; best.beta = b; best.gamma = g; best.ref = (PRIM_TRI << 30) | idx; best.gid = gid;
+            }
+        }
+        return false;
+    }
     for (uint32_t k = start; k < start + count; ++k) {
         cen.prim();
         uint32_t ref = S.refs[k];
@@ -589,17 +603,25 @@ PMD void node4_test(const SceneDev &S, int cur, const v3 &oinv, const v3 &inv, f
         const float sx = __uint_as_float(((w0.w & 0xffu) - 1u) << 23);
         const float sy = __uint_as_float((((w0.w >> 8) & 0xffu) - 1u) << 23);
         const float sz = __uint_as_float((((w0.w >> 16) & 0xffu) - 1u) << 23);
+        /* o + q * 2^e as one FMA: the product is exact, so the single
+         * rounding is the add's — the encoder's decode, bit for bit */
+#ifdef PM_QDECODE_MULADD
+#define QDEC(o, q, s) ((o) + (q) * (s))
+#else
+#define QDEC(o, q, s) __builtin_fmaf((q), (s), (o))
+#endif
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t sh = 8u * (uint32_t)k;
-            const float lx = ox + (float)((w1.x >> sh) & 0xffu) * sx, ly = oy + (float)((w1.y >> sh) & 0xffu) * sy;
-            const float lz = oz + (float)((w1.z >> sh) & 0xffu) * sz, hx = ox + (float)((w1.w >> sh) & 0xffu) * sx;
-            const float hy = oy + (float)((w2.x >> sh) & 0xffu) * sy, hz = oz + (float)((w2.y >> sh) & 0xffu) * sz;
+            const float lx = QDEC(ox, (float)((w1.x >> sh) & 0xffu), sx), ly = QDEC(oy, (float)((w1.y >> sh) & 0xffu), sy);
+            const float lz = QDEC(oz, (float)((w1.z >> sh) & 0xffu), sz), hx = QDEC(ox, (float)((w1.w >> sh) & 0xffu), sx);
+            const float hy = QDEC(oy, (float)((w2.x >> sh) & 0xffu), sy), hz = QDEC(oz, (float)((w2.y >> sh) & 0xffu), sz);
             t[k] = box_near(lx, ly, lz, hx, hy, hz, oinv, inv, tmin, tmax);
         }
         c[0] = (int)w3.x; c[1] = (int)w3.y; c[2] = (int)w3.z; c[3] = (int)w3.w;
         n[0] = (int)(int16_t)(w2.z & 0xffffu); n[1] = (int)(int16_t)(w2.z >> 16);
         n[2] = (int)(int16_t)(w2.w & 0xffffu); n[3] = (int)(int16_t)(w2.w >> 16);
+#undef QDEC
     } else {
         const float4 *nd = S.wnodes + 8 * cur;
         const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
