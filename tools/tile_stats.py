@@ -8,10 +8,12 @@ import torch  # noqa: F401
 from pmrender import hip, scenes
 from pmrender.abi import RenderParams
 C5 = "c5" in sys.argv[1:]
-sc = scenes.caustic_scene(1920, 1080) if C5 else scenes.cornell_box(1920, 1080)
+C3 = "c3" in sys.argv[1:]
+sc = (scenes.caustic_scene(1920, 1080) if C5 else
+      scenes.triangle_soup(1_000_000, 1920, 1080) if C3 else scenes.cornell_box(1920, 1080))
 ctx = sc.load_into(hip.Context(0))
 KNN = "knn" in sys.argv[1:]
-PATHS = 1_048_576 if C5 else 262144
+PATHS = 1_048_576 if (C5 or C3) else 262144
 if KNN:
     from pmrender.abi import PM_ESTIMATOR_KNN
     p = RenderParams.defaults(paths_per_pass=PATHS, initial_radius2=100.0, estimator=PM_ESTIMATOR_KNN, knn_lookup=50)
