@@ -349,6 +349,10 @@ def main():
             # tests): what the L1 / LDS deliver, not HBM traffic
             "l1_delivered": {"bytes_per_launch": int(l1_bytes), "formula": l1_formula,
                              "GBs": round(l1_bytes / (gather_ms * 1e-3) / 1e9, 1)},
+            # the roofline the kernel is priced against (the contract's "hbm");
+            # what actually limits it is stated in "limiter"
+            "achieved_basis": "SURVEY.md §8d compulsory bytes since round 2 (round 1 priced the per-lane "
+                              "algorithmic bytes, so r01 fractions are not comparable)",
             "limiter": ("VALU issue (profiles/r02 counters): ~3 selection passes over each tile's staged union, "
                         "every lane testing every staged photon — arithmetic, not memory" if knn else
                         "VALU issue + per-wave latency (profiles/r02 counters): the kernel reads each record "

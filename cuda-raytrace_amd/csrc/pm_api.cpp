@@ -766,8 +766,11 @@ int pm_commit(void *ptr) {
             std::vector<uint32_t> qn;
             const bool quant = PM_BVH4_QUANT != 0;
             const char *lt = getenv("PM_LEAF_TRIS"); /* 0: every leaf through its refs (A/B knob) */
-            if (quant && !quantize_bvh4(w.nodes, lt && atoi(lt) == 0 ? std::vector<uint32_t>() : bvh.refs, qn)) FAIL(c, PM_ERR_INVALID, "BVH leaf too large for quantized nodes");
-            if (w.max_stack <= BVH_STACK) {
+            /* a leaf the quantized count cannot code (>= LEAF_TRIS primitives,
+             * possible at build_bvh's depth limit) keeps the binary traversal,
+             * like a tree whose stack bound exceeds BVH_STACK */
+            const bool coded = !quant || quantize_bvh4(w.nodes, lt && atoi(lt) == 0 ? std::vector<uint32_t>() : bvh.refs, qn);
+            if (coded && w.max_stack <= BVH_STACK) {
                 o_wnodes = quant ? put(qn.data(), qn.size() * sizeof(uint32_t))
                                  : put(w.nodes.data(), w.nodes.size() * sizeof(float));
                 wide = quant ? 2 : 1;
@@ -994,8 +997,11 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
     HIPCHK(c, launch_trace(T, c->counting, s));
     timer_end(c, "trace", s);
     if (fuse) { c->fused.valid = true; c->fused.n = end_slot; c->fused.grid = T.grid; c->count_zero_words = 0; }
+    /* traced photons carry the scene's signs (scene_nonneg); slots outside
+     * the traced range keep theirs, so the flag is reset only when this
+     * trace rewrote every slot in use */
+    if (path_begin == slot_path_base && end_slot >= c->slots_used) c->slots_nonneg = true;
     c->slots_used = std::max(c->slots_used, end_slot);
-    c->slots_nonneg = true; /* traced photons carry the scene's signs (scene_nonneg) */
     return PM_OK;
 }
 

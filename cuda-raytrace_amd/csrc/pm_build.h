@@ -64,7 +64,7 @@ void collapse_bvh4(const BvhOut &bin, int leaf_prims, Bvh4Out &out);
  * (q * 2^e exact, one rounding in the add); q is floor / ceil of the exact
  * offset, so by monotone rounding every decoded box contains the float box,
  * which is checked here: the culling test only gets more conservative.
- * Returns false if a node cannot be encoded (leaf count > 32767). */
+ * Returns false if a node cannot be encoded (leaf count > 16383 = 0x3fff: bit 14 is the LEAF_TRIS flag). */
 bool quantize_bvh4(const std::vector<float> &nodes, std::vector<uint32_t> &q);
 /* With the scene's refs (kind << 30 | storage index): a leaf whose refs
  * are all triangles at consecutive storage slots s0, s0 + 1, ... is coded

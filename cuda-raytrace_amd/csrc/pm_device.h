@@ -464,10 +464,13 @@ PMD bool brute_isect(const SceneDev &S, const Ray &ray, Hit &best, C &cen) {
     return false;
 }
 
-/* Tests the primitives of one leaf; for ANY=true returns at the first hit. */
-template <bool ANY, class C>
+/* Tests the primitives of one leaf; for ANY=true returns at the first hit.
+ * TRIRUN: the leaf comes from a quantized 4-wide node, whose count may carry
+ * pm_build.h's LEAF_TRIS flag (only quantize_bvh4 sets it; binary and float
+ * 4-wide leaves are always decoded through their refs, whatever their size). */
+template <bool ANY, bool TRIRUN = false, class C>
 PMD bool leaf_isect(const SceneDev &S, uint32_t start, uint32_t count, const Ray &ray, Hit &best, C &cen) {
-    if (count & 0x4000u) { /* pm_build.h LEAF_TRIS: triangles at storage slots [start, start + n), no refs */
+    if (TRIRUN && (count & 0x4000u)) { /* LEAF_TRIS: triangles at storage slots [start, start + n), no refs */
         for (uint32_t idx = start; idx < start + (count & 0x3fffu); ++idx) {
             cen.prim();
             float t, b, g;
@@ -683,7 +686,7 @@ PMD bool traverse4(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int
             else cur = -1;
         }
         while (l0n != 0) {
-            if (leaf_isect<ANY>(S, l0s, l0n, ray, best, cen)) return true;
+            if (leaf_isect<ANY, PM_BVH4_QUANT != 0>(S, l0s, l0n, ray, best, cen)) return true;
             l0s = l1s; l0n = l1n; l1s = l2s; l1n = l2n; l2s = l3s; l2n = l3n; l3n = 0;
         }
         if (cur < 0 || guard > S.n_nodes) break;
@@ -716,7 +719,7 @@ PMD void trav_begin(const Ray &ray, TravState &t) {
 template <class C>
 PMD bool trav_step(const SceneDev &S, const Ray &ray, TravState &T, int *stack, int stride, C &cen) {
     if (T.l0n != 0) {
-        leaf_isect<false>(S, T.l0s, T.l0n, ray, T.best, cen);
+        leaf_isect<false, PM_BVH4_QUANT != 0>(S, T.l0s, T.l0n, ray, T.best, cen);
         T.l0s = T.l1s; T.l0n = T.l1n; T.l1s = T.l2s; T.l1n = T.l2n; T.l2s = T.l3s; T.l2n = T.l3n; T.l3n = 0;
         return T.l0n != 0 || T.cur >= 0;
     }

@@ -568,7 +568,7 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
      * of incoherent tiles, scan their own cells from global memory */
     TILE_STAT(4, __builtin_popcountll(__ballot(direct)));
     if (NN) {
-        if (fmax(fmax(dx, dy), dz) < 0x1p53) {
+        if (dx < 0x1p53 && dy < 0x1p53 && dz < 0x1p53) { /* NaN / inf fail: int64 path */
             Lf.x = d2ll(dx); Lf.y = d2ll(dy); Lf.z = d2ll(dz);
         } else if (R.small) { /* inexact (or NaN): this record again in int64 */
             M = 0;

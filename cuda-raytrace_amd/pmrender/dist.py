@@ -181,10 +181,14 @@ class HipEngine:
 
 
 class PassRunner:
-    def __init__(self, engine, params, rank=0, world=1, exchange="reduce"):
+    def __init__(self, engine, params, rank=0, world=1, exchange="reduce", force_exchange=False):
+        """force_exchange: run the N > 1 code path (record view, collectives,
+        owned chunks / bands) even at world size 1 — how a 1-GPU box executes
+        the RCCL branch of the exchange (tests/test_dist_gpu.py)."""
         if exchange not in ("reduce", "allgather"):
             raise ValueError(exchange)
-        if world > 1 and exchange == "reduce" and int(getattr(params, "estimator", 0)) != 0:
+        self.multi = world > 1 or force_exchange
+        if self.multi and exchange == "reduce" and int(getattr(params, "estimator", 0)) != 0:
             # the kNN estimate is not a sum over photon shards
             raise ValueError("the kNN estimator needs the all-gather exchange")
         self.e, self.p, self.rank, self.world, self.exchange = engine, params, rank, world, exchange
@@ -197,7 +201,7 @@ class PassRunner:
         self.padded = self.rec_per * world
         self.slot_buf = None
         self._pending = None
-        if world > 1 and exchange == "reduce":
+        if self.multi and exchange == "reduce":
             # exchange over the active records only, owned in contiguous chunks of the view
             self.n_view = engine.set_record_view(True)
             self.v_begin, self.v_count, self.v_per = _chunk(self.n_view, world, rank)
@@ -207,7 +211,7 @@ class PassRunner:
             self.count = engine.alloc((self.v_per * world,), torch.int32)
             self.flux = engine.alloc((self.v_per * world, 3), torch.int64)
             self.flux_chunk = engine.alloc((self.v_per, 3), torch.int64)
-        if world > 1 and exchange == "allgather":
+        if self.multi and exchange == "allgather":
             self.slot_buf = engine.alloc((world * self.slots_per_rank * PHOTON_DTYPE.itemsize,), torch.uint8)
             engine.use_slot_buffer(self.slot_buf)
             unit = engine.band_records() if hasattr(engine, "band_records") else 512
@@ -250,7 +254,7 @@ class PassRunner:
     def step(self, pass_index, reset=False):
         """One PPM pass: trace this rank's paths, build, gather (+ exchange)."""
         e, p = self.e, self.p
-        if self.world == 1:
+        if not self.multi:
             if reset:
                 e.reset_records(p)
             e.trace_photons(p, pass_index, 0, self.paths, 0)
@@ -280,7 +284,7 @@ class PassRunner:
     def final_gather(self, emitted, out_full):
         """Final radiance of all records (record order) on every rank."""
         self.flush()
-        if self.world == 1:
+        if not self.multi:
             self.e.final(emitted, 0, self.n_records, out_full)
             return out_full
         if self.exchange == "reduce":

@@ -13,12 +13,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "cuda-raytrace_amd", "csrc")
 
 
-@pytest.mark.parametrize("nprims", [1, 7, 50000])
-def test_quantized_boxes_contain_float_boxes(tmp_path, nprims):
+@pytest.mark.parametrize("nprims,mode", [(1, ""), (7, ""), (50000, ""), (7, "refs"), (50000, "refs"), (1, "bigleaf")])
+def test_quantized_boxes_contain_float_boxes(tmp_path, nprims, mode):
+    """boxes contain the float boxes; with refs, LEAF_TRIS codes exactly the
+    all-triangle leaves (~first storage slot); a leaf of >= LEAF_TRIS
+    primitives is rejected (the scene then keeps the binary traversal)."""
     exe = tmp_path / "qcheck"
     subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", CSRC, "-I", os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "tests", "native", "bvh4_quant_check.cpp"), os.path.join(CSRC, "pm_build.cpp"),
                     "-o", str(exe)], check=True, timeout=300)
-    r = subprocess.run([str(exe), str(nprims)], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([str(exe), str(nprims)] + ([mode] if mode else []), capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "bad 0" in r.stdout

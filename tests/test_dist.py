@@ -168,7 +168,7 @@ def _worker(rank, world, port, exchange, outdir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     p = RenderParams.defaults(paths_per_pass=PATHS, initial_radius2=25.0)
     eng = OracleEngine(_scene(), p)
-    runner = PassRunner(eng, p, rank, world, exchange)
+    runner = PassRunner(eng, p, rank, world, exchange, force_exchange=world == 1)
     for pass_index in range(2):
         runner.step(pass_index)
     runner.flush()
@@ -203,10 +203,13 @@ def _single_process_reference(world):
     return recs, orc.final(recs, float(PATHS * world * 2))
 
 
-@pytest.mark.parametrize("exchange,world", [("allgather", 2), ("reduce", 2), ("reduce", 4), ("allgather", 3)])
+@pytest.mark.parametrize("exchange,world", [("allgather", 2), ("reduce", 2), ("reduce", 4), ("allgather", 3),
+                                            ("reduce", 1), ("allgather", 1)])
 def test_two_rank_pass_matches_single_process(exchange, world, tmp_path):
     """world-size 2 (and 3 / 4: view chunks and bands that do not divide
-    evenly, as at N = 8) over gloo vs one process over the same global paths"""
+    evenly, as at N = 8) over gloo vs one process over the same global paths;
+    world 1 with the exchange path forced (force_exchange: what the GPU test
+    runs on RCCL)"""
     mp.start_processes(_worker, args=(world, _free_port(), exchange, str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
     ref_recs, ref_img = _single_process_reference(world)
@@ -218,7 +221,8 @@ def test_two_rank_pass_matches_single_process(exchange, world, tmp_path):
     assert np.array_equal(recs["photon_count"], ref_recs["photon_count"])
     assert np.array_equal(recs["radius2"].view(np.uint32), ref_recs["radius2"].view(np.uint32))
     img = np.load(tmp_path / "img0.npy")
-    assert np.array_equal(img, np.load(tmp_path / "img1.npy"))        # every rank holds the full image
+    for r in range(1, world):                                          # every rank holds the full image
+        assert np.array_equal(img, np.load(tmp_path / f"img{r}.npy"))
     if exchange == "allgather":
         # replicated map over identical slots + canonical kd-tree: bit-exact
         assert np.array_equal(recs["flux"].view(np.uint32), ref_recs["flux"].view(np.uint32))

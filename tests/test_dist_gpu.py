@@ -25,7 +25,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, exchange, outdir):
+def _worker(rank, world, port, exchange, outdir, backend="gloo"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -34,13 +34,18 @@ def _worker(rank, world, port, exchange, outdir):
     from pmrender import hip, scenes
     from pmrender.abi import RenderParams
     from pmrender.dist import HipEngine, PassRunner
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":   # RCCL: one rank per GPU, so world 1 on the test box
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     ctx = scenes.cornell_box(W, H).load_into(hip.Context(0))
     p = RenderParams.defaults(paths_per_pass=PATHS, initial_radius2=25.0)
     with torch.cuda.stream(torch.cuda.Stream()):
         eng = HipEngine(ctx)
         ctx.eye_pass(p, eng._s())
-        runner = PassRunner(eng, p, rank, world, exchange)
+        runner = PassRunner(eng, p, rank, world, exchange, force_exchange=True)
+        assert runner.multi
         for k in range(PASSES):
             runner.step(k)
         out = torch.zeros((runner.n_records, 3), dtype=torch.float32, device="cuda")
@@ -52,13 +57,9 @@ def _worker(rank, world, port, exchange, outdir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("exchange", ["reduce", "allgather"])
-def test_two_ranks_one_gpu_match_single_context(exchange, tmp_path, hip_mod):
+def _single_context_image(world, hip_mod):
     from pmrender import scenes
     from pmrender.abi import RenderParams
-    world = 2
-    mp.start_processes(_worker, args=(world, _free_port(), exchange, str(tmp_path)), nprocs=world, join=True,
-                       start_method="spawn")
     ref = scenes.cornell_box(W, H).load_into(hip_mod.Context(0))
     p = RenderParams.defaults(paths_per_pass=world * PATHS, initial_radius2=25.0)
     ref.eye_pass(p)
@@ -73,6 +74,31 @@ def test_two_ranks_one_gpu_match_single_context(exchange, tmp_path, hip_mod):
     ref.synchronize()
     want = img.cpu().numpy()
     ref.close()
+    return want
+
+
+@pytest.mark.parametrize("exchange", ["reduce", "allgather"])
+def test_two_ranks_one_gpu_match_single_context(exchange, tmp_path, hip_mod):
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), exchange, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    want = _single_context_image(world, hip_mod)
     for r in range(world):
         got = np.load(tmp_path / f"img{r}.npy")
         assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"rank {r} image differs"
+
+
+@pytest.mark.parametrize("exchange", ["reduce", "allgather"])
+def test_rccl_world1_exchange_matches_single_context(exchange, tmp_path, hip_mod):
+    """The RCCL branch of the exchange (dist.py _AsyncExchange.start: async
+    all_reduce + reduce_scatter_tensor on the device tensors, joined by a
+    stream-ordered wait; all_gather_into_tensor of the slots) on an nccl
+    process group of world size 1, the N > 1 path forced (record view,
+    pm_gather_split, pm_ppm_update_split, pm_final_view / bands): image bit
+    for bit equal to one context without any exchange."""
+    mp.start_processes(_worker, args=(1, _free_port(), exchange, str(tmp_path), "nccl"), nprocs=1, join=True,
+                       start_method="spawn")
+    want = _single_context_image(1, hip_mod)
+    got = np.load(tmp_path / "img0.npy")
+    assert (want > 0).any()
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"RCCL world-1 {exchange} image differs"

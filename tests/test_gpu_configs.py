@@ -126,6 +126,44 @@ def test_c2_full_records(oracle_mod, hip_mod):
         ctx.close()
 
 
+def shard_records(ctx, orc, p, path_begin):
+    """One rank's photon shard at its global path ids (slots of paths
+    [path_begin, path_begin + paths_per_pass)), gathered over all records:
+    GPU stage API (grid) vs the oracle's pbrt kd-tree pass over the same
+    global paths."""
+    n = p.paths_per_pass
+    ctx.eye_pass(p)
+    recs = orc.eye_pass(p)
+    ctx.trace_photons(p, 0, path_begin, n, slot_path_base=path_begin)
+    ctx.build_photon_map(p, n * 4)
+    ctx.gather(p)
+    slots = orc.trace_photons(p, 0, path_begin, n)
+    orc.gather(orc.build_kdtree(slots), recs, p)
+    return ctx.download_records(), recs, ctx.download_slots(n * 4), slots
+
+
+@pytest.mark.parametrize("rank", [0, 7])
+def test_c4_share(rank, oracle_mod, hip_mod):
+    """C4 per-GPU share at full size (the bench's --config c4 line): Cornell
+    3840x2160 (8,294,400 gather points), 524,288 paths = 2,097,152 slots of
+    rank `rank` of 8 (global paths [rank * 524,288, ...): rank 7's pm_index
+    runs to 16,777,212, past the 12,582,912 limit of the Halton quirk).
+    Slots bit-exact; per-record M -> N', r^2 exact and flux <= 2e-5 relative
+    vs the oracle (photontracing.cu:80-103, gathering.cu:104-126)."""
+    sc = scenes.cornell_box(3840, 2160)
+    ctx, orc = make_pair(sc, oracle_mod, hip_mod)
+    try:
+        paths = 524_288
+        p = RenderParams.defaults(paths_per_pass=paths)
+        got, ref, slots, ref_slots = shard_records(ctx, orc, p, rank * paths)
+        assert_bitexact(slots, ref_slots, f"C4 rank {rank} slots")
+        assert len(got) == 3840 * 2160
+        assert (ref["photon_count"] > 0).sum() > 2_000_000
+        compare_gathered_records(got, ref)
+    finally:
+        ctx.close()
+
+
 def test_c3_full_workload(oracle_mod, hip_mod):
     """C3: Cornell enclosure + 1M-triangle soup, 1,048,576 paths, 1080p.
     Oracle: eye records and every photon slot bit-exact, per-record PPM

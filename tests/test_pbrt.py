@@ -9,7 +9,8 @@ point light "from" + CTM, "scale", named materials, constant textures,
 ObjectBegin/Instance, fallbacks) come out as pbrt defines them.
 GPU: rendering the .pbrt file through the C++ layer gives the same image, bit
 for bit, as the Python stage driver on the in-code scene — photon mapping and
-the simple renderer.
+the simple renderer — and matches the CPU oracle on that scene (simple
+renderer bit for bit, photon mapping within RMSE 1e-3).
 """
 import json
 import math
@@ -247,7 +248,7 @@ def read_pfm(path):
 @pytest.mark.parametrize("scene,renderer", [("cornell-box", "photonmapping"), ("cornell-box", "simple"),
                                             ("caustic-glass", "photonmapping"), ("caustic-glass", "simple"),
                                             ("killeroo-proxy", "photonmapping"), ("killeroo-proxy", "simple")])
-def test_pbrt_render_matches_stage_driver(scene, renderer, tmp_path, hip_mod):
+def test_pbrt_render_matches_stage_driver(scene, renderer, tmp_path, hip_mod, oracle_mod):
     paths, passes = 16384, 2
     out = tmp_path / "img.pfm"
     r = subprocess.run([CLI, "--pbrt", os.path.join(SCENES, scene + ".pbrt"), "--renderer", renderer,
@@ -258,10 +259,22 @@ def test_pbrt_render_matches_stage_driver(scene, renderer, tmp_path, hip_mod):
     sc = {"cornell-box": scenes.cornell_box, "caustic-glass": scenes.caustic_scene,
           "killeroo-proxy": scenes.figure_scene}[scene](256, 256)
     ctx = sc.load_into(hip_mod.Context(0))
+    orc = sc.load_into(oracle_mod.Oracle())
     if renderer == "simple":
         ref, _ = ctx.render_simple(RenderParams.simple_defaults())
+        want = orc.render_simple(RenderParams.simple_defaults())
     else:
-        ref, _ = ctx.render(RenderParams.defaults(paths_per_pass=paths, passes=passes, gather_structure=PM_GATHER_GRID))
+        p = RenderParams.defaults(paths_per_pass=paths, passes=passes, gather_structure=PM_GATHER_GRID)
+        ref, _ = ctx.render(p)
+        want, _ = orc.render(p)
     ctx.close()
     assert img.shape == ref.shape
     assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), f"{scene}/{renderer}: .pbrt image differs"
+    # the .pbrt render vs the CPU oracle of the same scene: the simple
+    # renderer bit for bit, photon mapping (bucket gather) within RMSE 1e-3
+    want = np.asarray(want, np.float32).reshape(img.shape)
+    if renderer == "simple":
+        assert np.array_equal(img.view(np.uint32), want.view(np.uint32)), f"{scene}/simple: differs from the oracle"
+    else:
+        err = float(np.sqrt(np.mean((img.astype(np.float64) - want) ** 2)))
+        assert err < 1e-3, f"{scene}: .pbrt image vs oracle RMSE {err}"

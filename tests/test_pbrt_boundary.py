@@ -9,7 +9,9 @@ CPU: the host links, exports the four functions with pbrt's C++ signatures,
 and stops with pbrt's Severe() when no device exists. GPU: the image that
 reaches Film::AddSample is bit-identical to the stage driver rendering the
 same eye rays and light randoms through the C-ABI (photon mapper with both
-photon-map structures, the simple renderer, an ObjectInstance'd scene)."""
+photon-map structures, the simple renderer, an ObjectInstance'd scene), and
+matches the CPU oracle (kd-tree gather and simple renderer bit for bit,
+bucket gather within RMSE 1e-3)."""
 import os
 import subprocess
 
@@ -74,7 +76,7 @@ def read_host_output(path, W, H):
 @pytest.mark.parametrize("renderer,photonmap,nsamples,instanced", [
     ("photonmap", "grid", 1, False), ("photonmap", "kdtree", 1, False), ("photonmap", "grid", 4, True),
     ("simple", "grid", 2, False)])
-def test_boundary_matches_stage_driver(renderer, photonmap, nsamples, instanced, tmp_path, hip_mod):
+def test_boundary_matches_stage_driver(renderer, photonmap, nsamples, instanced, tmp_path, hip_mod, oracle_mod):
     from pmrender import scenes
     from pmrender.abi import PM_GATHER_GRID, PM_GATHER_KDTREE, RenderParams
     W, H, paths = 64, 48, 16384
@@ -101,3 +103,18 @@ def test_boundary_matches_stage_driver(renderer, photonmap, nsamples, instanced,
     ref = ref.reshape(-1, 3)
     assert (ref > 0).any()
     assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), "Film::AddSample image differs from the stage driver"
+    # and the image pbrt receives matches the CPU oracle on the same eye rays
+    # and light randoms: kd-tree gather and simple renderer bit for bit
+    # (gathering.cu, simplerender.cu), bucket gather within RMSE 1e-3
+    orc = sc.load_into(oracle_mod.Oracle())
+    if renderer == "simple":
+        want = orc.render_simple(RenderParams.simple_defaults())
+    else:
+        want, _ = orc.render(RenderParams.defaults(
+            paths_per_pass=paths, gather_structure=PM_GATHER_KDTREE if photonmap == "kdtree" else PM_GATHER_GRID))
+    want = np.asarray(want, np.float32).reshape(-1, 3)
+    if renderer == "simple" or photonmap == "kdtree":
+        assert np.array_equal(img.view(np.uint32), want.view(np.uint32)), "Film::AddSample image differs from the oracle"
+    else:
+        err = float(np.sqrt(np.mean((img.astype(np.float64) - want) ** 2)))
+        assert err < 1e-3, f"Film::AddSample image vs oracle: RMSE {err}"
