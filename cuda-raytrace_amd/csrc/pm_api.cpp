@@ -84,8 +84,9 @@ struct Ctx {
     int64_t slots_used = 0;
     /* photon buckets */
     DevBuf d_count, d_cell_start, d_scratch, d_pha, d_phb;
-    struct { bool valid = false; int64_t n = 0; GridDesc grid{}; } fused; /* counts made by the last trace */
+    struct { bool valid = false; int64_t n = 0; GridDesc grid{}; float r2 = 0.f; } fused; /* counts made by the last trace */
     GridDesc grid{};
+    float grid_r2 = 0.f; /* radius^2 the photon map's grid is designed for */
     int64_t bvh4_nodes = 0; /* 4-wide BVH of an HBM scene (0: binary traversal) */
     int bvh4_depth = 0;
     int map_kind = -1;
@@ -121,9 +122,37 @@ struct Ctx {
     bool fuse_count = true;        /* bucket counting inside the trace kernel (env PM_FUSE_COUNT=0 disables) */
     int kd_stack = KD_STACK;        /* kd gather stack entries (env PM_KD_STACK, tests only) */
     bool trace_pool = true;         /* pooled trace kernel for 4-wide BVH scenes (env PM_TRACE_POOL=0 disables) */
+    bool trace_hold = true;         /* deposits written once per path (env PM_TRACE_HOLD=0: per deposit) */
     int64_t pool_waves = 0;         /* pooled kernel: waves per launch (env PM_POOL_WAVES; 0 = one occupancy round) */
     int gather_kernel = PM_GK_TILE; /* bucket gather kernel (env PM_GATHER_KERNEL=tile|lane|wave) */
     bool gather_xcd = false;        /* tile gather: contiguous tile ranges per XCD (env PM_GATHER_XCD=1) */
+    int cell_span = 2;              /* PPM grid: cells per axis of a query box (env PM_CELL_SPAN 2..5) */
+    /* adaptive grid radius (progressive PPM: radii shrink pass by pass). The
+     * fused tile gather bins every updated r^2 (R2_BINS log bins per copy,
+     * 8 copies) into d_r2hist; the histogram is copied to pinned memory
+     * behind r2_event and, once landed, sets the next passes' grid radius to
+     * the grid_quantile of the records' radii (the rest scan per lane).
+     * Staleness is safe (radii only shrink); anything that can raise a
+     * radius (eye pass, reset, upload, set_radius2, split / partial updates)
+     * invalidates it. env PM_GRID_QUANTILE (default 0.99; <= 0 disables). */
+    /* gather order (incoherent scenes, launch_record_order): active records
+     * in cell order, built once per eye pass; env PM_REC_ORDER = 1 always,
+     * -1 auto (when > 20 % of the active tiles do not fit one LDS group),
+     * default 0 off: measured slower on C3 (gather 0.56 -> 0.67 ms: the
+     * records' own reads become scattered) */
+    DevBuf d_order, d_ocount, d_ostart, d_oscratch, d_ostats;
+    bool order_valid = false, use_order = false;
+    int64_t n_order = 0;
+    int rec_order_mode = 0;
+    DevBuf d_r2hist;
+    uint32_t *h_r2hist = nullptr, *h_r2hist_dev = nullptr; /* host-mapped R2_BINS words, its device address */
+    hipEvent_t r2_event = nullptr;
+    bool r2_wanted = false;    /* a progressive pass asked for the radii (no histogram otherwise) */
+    bool r2_pending = false;   /* a histogram copy in flight */
+    bool r2_valid = false;     /* the last landed / in-flight histogram describes the records */
+    float r2_hist_init = 0.f;  /* the r^2 its bins are relative to */
+    float design_r2 = 0.f;     /* grid radius^2 of the current photon map (0: initial_radius2) */
+    double grid_quantile = 0.99;
     /* leading words of d_count known to be zero (the bucket scan clears the
      * counters it reads); valid while d_count.p == count_zero_ptr */
     size_t count_zero_words = 0;
@@ -308,6 +337,9 @@ int ensure_records(Ctx *c) {
     HIPCHK(c, c->d_dl.ensure(n * sizeof(float4)));
     c->nrec = n;
     c->tiles_valid = false;
+    c->order_valid = false;
+    c->r2_valid = false;
+    c->design_r2 = 0.f;
     return PM_OK;
 }
 
@@ -316,6 +348,15 @@ RecordsDev recs(Ctx *c) {
     R.pos = c->d_pos.as<float4>(); R.nrm = c->d_nrm.as<float4>(); R.state = c->d_state.as<float4>();
     R.n = c->d_n.as<float>(); R.dl = c->d_dl.as<float4>(); R.count = c->nrec;
     return R;
+}
+
+/* cells per axis of a box of width 2 r' (r' of radius2) on grid g: the tile
+ * kernel's run count (GatherParams::span), clamped to its instances 2..5
+ * (larger boxes scan per lane) */
+int grid_span(const GridDesc &g, float radius2) {
+    const double rq = sqrt((double)radius2) * 1.0001 + 1e-4;
+    const double w = 2.0 * rq * (double)g.inv_cs * (1.0 + 1e-6);
+    return std::max(2, std::min(5, (int)std::floor(w) + 2));
 }
 
 GatherParams gather_params(Ctx *c, const pm_render_params *p) {
@@ -333,6 +374,7 @@ GatherParams gather_params(Ctx *c, const pm_render_params *p) {
     G.error = reinterpret_cast<unsigned int *>(c->d_counters.as<unsigned long long>() + 16);
     G.fx_nonneg = c->scene_nonneg && c->slots_nonneg ? 1 : 0;
     G.xcd = c->gather_xcd ? 1 : 0;
+    G.span = grid_span(c->grid, c->grid_r2 > 0.f ? c->grid_r2 : p->initial_radius2);
     if (c->view_active) { G.view_rank = c->d_vrank.as<uint32_t>(); G.view_list = c->d_vlist.as<uint32_t>(); }
     /* fixed-point scale 2^S: a single contribution is bounded by
      * alpha_max * Kd_max / pi with alpha_max = emission * Kd_max^mpc (Lambert
@@ -437,7 +479,11 @@ int pm_create(void **out, const pm_config *cfg) {
         c->gather_kernel = !strcmp(e, "lane") ? PM_GK_LANE : !strcmp(e, "wave") ? PM_GK_WAVE : PM_GK_TILE;
     if (const char *e = getenv("PM_GATHER_WAVE")) if (atoi(e)) c->gather_kernel = PM_GK_WAVE;
     if (const char *e = getenv("PM_GATHER_XCD")) c->gather_xcd = atoi(e) != 0;
+    if (const char *e = getenv("PM_CELL_SPAN")) c->cell_span = std::max(2, std::min(5, atoi(e)));
+    if (const char *e = getenv("PM_GRID_QUANTILE")) c->grid_quantile = atof(e);
+    if (const char *e = getenv("PM_REC_ORDER")) c->rec_order_mode = atoi(e);
     if (const char *e = getenv("PM_TRACE_POOL")) c->trace_pool = atoi(e) != 0;
+    if (const char *e = getenv("PM_TRACE_HOLD")) c->trace_hold = atoi(e) != 0;
     if (const char *e = getenv("PM_POOL_WAVES")) c->pool_waves = std::max(1LL, atoll(e));
     if (const char *e = getenv("PM_TILE_LIST")) c->tile_list = atoi(e) != 0;
     if (const char *e = getenv("PM_KD_STACK")) c->kd_stack = std::max(1, std::min(KD_STACK, atoi(e)));
@@ -470,9 +516,12 @@ void pm_destroy(void *ptr) {
     DevBuf *bufs[] = {&c->d_scene, &c->d_rays, &c->d_rand2d, &c->d_pos, &c->d_nrm, &c->d_state, &c->d_n,
                       &c->d_dl, &c->d_slots, &c->d_count, &c->d_scratch, &c->d_vflags, &c->d_vrank, &c->d_vlist, &c->d_vsums,
                       &c->d_cell_start, &c->d_pha, &c->d_phb,
-                      &c->d_kd, &c->d_out, &c->d_counters, &c->d_tiles, &c->d_tile_flags, &c->d_tile_count};
+                      &c->d_kd, &c->d_out, &c->d_counters, &c->d_tiles, &c->d_tile_flags, &c->d_tile_count,
+                      &c->d_r2hist, &c->d_order, &c->d_ocount, &c->d_ostart, &c->d_oscratch, &c->d_ostats};
     for (DevBuf *b : bufs) b->release();
     if (c->tile_event) (void)hipEventDestroy(c->tile_event);
+    if (c->r2_event) (void)hipEventDestroy(c->r2_event);
+    if (c->h_r2hist) (void)hipHostFree(c->h_r2hist);
     if (c->h_tile_count) (void)hipHostFree(c->h_tile_count);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -852,6 +901,9 @@ int pm_eye_pass(void *ptr, const pm_render_params *p, void *stream) {
     timer_end(c, "eye", s);
     c->rec_fresh = false; /* the eye pass writes every record */
     c->tiles_valid = false;
+    c->order_valid = false;
+    c->r2_valid = false;
+    c->design_r2 = 0.f;
     if (c->view_active && (rc = build_view(c, s))) return rc;
     return PM_OK;
 }
@@ -893,21 +945,56 @@ int pm_set_slot_buffer(void *ptr, void *d, int64_t n) {
     return PM_OK;
 }
 
-/* photon-bucket grid of a render: cell edge >= 2 r_max over the scene box
+/* photon-bucket grid of a render: cell edge 2 r_max / (span - 1) over the
+ * scene box, so a query box [p - r', p + r'] spans <= span cells per axis
  * (PPM radii only shrink, so it holds for every pass of the render) */
-static GridDesc make_grid(const Ctx *c, const pm_render_params *p) {
+/* radius^2 the PPM grid is designed for: the grid_quantile of the records'
+ * current radii from the last landed histogram (k_gather_tile), else the
+ * initial radius. Refreshed only where a photon map's grid is chosen
+ * (pm_trace_photons with fused counting, or pm_build_photon_map without), so
+ * the trace and the build of one pass agree. */
+static float grid_radius2(Ctx *c, const pm_render_params *p, bool refresh) {
+    const float init = p->initial_radius2;
+    if (p->estimator == PM_ESTIMATOR_KNN || c->grid_quantile <= 0.0) return init;
+    /* a pass that continues a render (no reset pending): the next fused
+     * gather bins its radii for the passes after it */
+    if (refresh && !c->rec_fresh) c->r2_wanted = true;
+    if (c->rec_fresh || !c->r2_valid || c->r2_hist_init != init) return init;
+    if (refresh && c->r2_pending && hipEventQuery(c->r2_event) == hipSuccess) {
+        c->r2_pending = false;
+        uint64_t cnt[R2_BINS] = {0}, total = 0;
+        for (int b = 0; b < R2_BINS; ++b) cnt[b] = ((volatile uint32_t *)c->h_r2hist)[b];
+        for (int b = 0; b < R2_BINS; ++b) total += cnt[b];
+        /* bins b.. hold t = r^2 / init <= 2^(-b/8): the largest b that still
+         * covers the quantile */
+        int best = 0;
+        uint64_t above = total;
+        for (int b = 0; b < R2_BINS; ++b) {
+            if ((double)above < c->grid_quantile * (double)total) break;
+            best = b;
+            above -= cnt[b];
+        }
+        /* the bins come from an approximate log2: a small margin */
+        c->design_r2 = total ? std::min(init, (float)(init * std::exp2(-best / (double)R2_PER_OCTAVE) * 1.01)) : 0.f;
+    }
+    return c->design_r2 > 0.f ? c->design_r2 : init;
+}
+
+static GridDesc make_grid(const Ctx *c, const pm_render_params *p, float radius2) {
     GridDesc g{};
-    const float rq = sqrtf(p->initial_radius2) * 1.0001f + 1e-4f;
-    /* PPM: cell edge >= 2 r_max, so a query reads at most 2x2x2 cells. kNN:
+    const float rq = sqrtf(radius2) * 1.0001f + 1e-4f;
+    /* PPM: span 2 by default (cell edge >= 2 r_max: at most 2x2x2 cells;
+     * env PM_CELL_SPAN 3..5 for finer cells, DESIGN.md §5 sweep). kNN:
      * r_max / 2 — the query visits rows nearest first and prunes cells
      * beyond the shrinking k-th distance (k_gather_knn) */
-    float cs = (p->estimator == PM_ESTIMATOR_KNN ? 0.5f : 2.0f) * rq * 1.001f;
+    const float f = p->estimator == PM_ESTIMATOR_KNN ? 0.5f : 2.0f / (float)(c->cell_span - 1);
+    float cs = f * rq * 1.001f;
     float ext[3];
     for (int a = 0; a < 3; ++a) ext[a] = std::max(c->bbox_hi[a] - c->bbox_lo[a], 1e-3f);
     int64_t dims[3];
     while (true) {
         for (int a = 0; a < 3; ++a) dims[a] = std::max<int64_t>(1, (int64_t)std::ceil(ext[a] / cs) + 1);
-        if (dims[0] * dims[1] * dims[2] <= (int64_t)1 << 26) break;
+        if (dims[0] * dims[1] * dims[2] <= (int64_t)1 << 25) break;
         cs *= 1.25f;
     }
     g.gx = c->bbox_lo[0]; g.gy = c->bbox_lo[1]; g.gz = c->bbox_lo[2];
@@ -954,6 +1041,11 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
     T.path_begin = path_begin; T.path_count = path_count; T.slot_path_base = slot_path_base;
     T.per_block = c->trace_per_block;
     T.wave_paths = c->trace_wave_paths;
+    T.hold = c->trace_hold ? 1 : 0;
+    if (T.hold && !c->S.wide) { /* per-lane kernel: only when the held deposits' LDS costs no resident waves */
+        const size_t lds = (size_t)c->S.stack_depth * TRACE_BLOCK * 4 + c->S.lds_bytes;
+        if (trace_lane_waves_per_cu(c->S, lds, 1) < trace_lane_waves_per_cu(c->S, lds, 0)) T.hold = 0;
+    }
     if (c->trace_pool && T.per_block == 0) {
         /* pooled kernel: one occupancy round (resident waves per CU from the
          * occupancy API: VGPRs and the LDS stacks) — each wave with a
@@ -963,7 +1055,13 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
         if (waves <= 0) {
             int cus = 0;
             if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0) cus = 256;
-            const int per_cu = trace_pool_waves_per_cu((size_t)c->S.stack_depth * TRACE_BLOCK * 4 + c->S.lds_bytes);
+            const size_t lds = (size_t)c->S.stack_depth * TRACE_BLOCK * 4 + c->S.lds_bytes;
+            int per_cu = trace_pool_waves_per_cu(lds, 0);
+            if (T.hold && c->S.wide) { /* pooled kernel: the held deposits' LDS must not cost resident waves */
+                const int per_cu_h = trace_pool_waves_per_cu(lds, 1);
+                if (per_cu_h < per_cu) T.hold = 0;
+                else per_cu = per_cu_h;
+            }
             waves = (int64_t)cus * (per_cu > 0 ? per_cu : 16);
         }
         /* any pool size works (the wave's cursor hands out paths to dead lanes) */
@@ -982,7 +1080,8 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
     c->fused.valid = false;
     const bool fuse = c->fuse_count && p->gather_structure == PM_GATHER_GRID && path_begin == slot_path_base;
     if (fuse) {
-        const GridDesc g = make_grid(c, p);
+        c->fused.r2 = grid_radius2(c, p, true);
+        const GridDesc g = make_grid(c, p, c->fused.r2);
         HIPCHK(c, c->d_count.ensure(((size_t)g.ncells + 1) * 4));
         HIPCHK(c, c->d_scratch.ensure(bucket_scratch_words(end_slot, g.ncells) * 4));
         HIPCHK(c, count_zeroed(c, (size_t)g.ncells + 1, s));
@@ -1033,8 +1132,11 @@ int pm_build_photon_map(void *ptr, const pm_render_params *p, int64_t n_slots, v
     }
     /* photon buckets: cell size >= 2 r_max (PPM radii only shrink) */
     GridDesc &g = c->grid;
-    g = make_grid(c, p);
-    const bool counted = c->fused.valid && c->fused.n == n_slots && same_grid(c->fused.grid, g);
+    /* the grid of the trace's fused counts, if they cover these slots */
+    const bool fused_ok = c->fused.valid && c->fused.n == n_slots;
+    c->grid_r2 = fused_ok ? c->fused.r2 : grid_radius2(c, p, true);
+    g = make_grid(c, p, c->grid_r2);
+    const bool counted = fused_ok && same_grid(c->fused.grid, g);
     const size_t n = (size_t)n_slots;
     HIPCHK(c, c->d_count.ensure(((size_t)g.ncells + 1) * 4));
     HIPCHK(c, c->d_cell_start.ensure(((size_t)g.ncells + 1) * 4));
@@ -1086,6 +1188,31 @@ static int ensure_tiles(Ctx *c, hipStream_t s) {
     return PM_OK;
 }
 
+/* the gather order of the active records (records fixed after the eye pass;
+ * synchronizes once to read its length and the tile census) */
+static int ensure_order(Ctx *c, const pm_render_params *p, hipStream_t s) {
+    if (c->order_valid) return PM_OK;
+    const GridDesc g = make_grid(c, p, p->initial_radius2);
+    const int64_t n = c->nrec;
+    HIPCHK(c, c->d_order.ensure(std::max<int64_t>(n, 16) * 4));
+    HIPCHK(c, c->d_ocount.ensure(((size_t)g.ncells + 1) * 4));
+    HIPCHK(c, c->d_ostart.ensure(((size_t)g.ncells + 1) * 4));
+    HIPCHK(c, c->d_oscratch.ensure(record_order_scratch_words(n, g.ncells) * 4));
+    HIPCHK(c, c->d_ostats.ensure(16));
+    HIPCHK(c, launch_record_order(recs(c), g, p->initial_radius2, c->d_ocount.as<uint32_t>(), c->d_ostart.as<uint32_t>(),
+                                  c->d_oscratch.as<uint32_t>(), c->d_order.as<uint32_t>(),
+                                  c->d_ostats.as<unsigned long long>(), s));
+    unsigned long long st[2] = {0, 0};
+    uint32_t na = 0;
+    HIPCHK(c, hipMemcpyAsync(st, c->d_ostats.p, 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(&na, c->d_ostart.as<uint32_t>() + g.ncells, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->n_order = na;
+    c->use_order = c->rec_order_mode == 1 || (c->rec_order_mode < 0 && (double)st[0] > 0.2 * (double)st[1]);
+    c->order_valid = true;
+    return PM_OK;
+}
+
 static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, int64_t rec_begin, int64_t rec_count,
                          void *stream, int *count = nullptr, long long *flux = nullptr) {
     int rc;
@@ -1119,8 +1246,33 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
         G.tiles = c->d_tiles.as<uint32_t>();
         if (c->tile_count_known) { G.n_tiles = c->n_tiles; G.n_tiles_dev = nullptr; }
         else { G.n_tiles = (c->nrec + 63) / 64; G.n_tiles_dev = c->d_tile_count.as<uint32_t>(); }
+        /* incoherent tiles (fused gathers): waves over the records in cell order */
+        if (!partial && !split && c->rec_order_mode != 0 && p->estimator == PM_ESTIMATOR_PPM) {
+            if ((rc = ensure_order(c, p, s))) return rc;
+            if (c->use_order) { G.order = c->d_order.as<uint32_t>(); G.n_order = c->n_order; G.tiles = nullptr; }
+        }
     }
     if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters.p, 0, 32, s));
+    /* a fused full PPM tile gather bins the updated radii (grid_radius2) */
+    /* (not while the previous histogram's copy is in flight: the pinned
+     * buffer is reused, and a stale histogram only overestimates radii) */
+    const bool hist = p->estimator == PM_ESTIMATOR_PPM && p->gather_structure == PM_GATHER_GRID && !partial &&
+                      !split && rec_begin == 0 && rec_count == c->nrec && c->gather_kernel == PM_GK_TILE &&
+                      !c->counting && c->grid_quantile > 0.0 && c->r2_wanted &&
+                      !(c->r2_pending && hipEventQuery(c->r2_event) != hipSuccess);
+    if (hist) {
+        if (!c->d_r2hist.p) {
+            HIPCHK(c, c->d_r2hist.ensure(R2_COPIES * R2_BINS * 4));
+            HIPCHK(c, hipMemsetAsync(c->d_r2hist.p, 0, R2_COPIES * R2_BINS * 4, s)); /* the reduce re-zeroes it */
+        }
+        if (!c->h_r2hist) {
+            HIPCHK(c, hipHostMalloc((void **)&c->h_r2hist, R2_BINS * 4, hipHostMallocMapped));
+            HIPCHK(c, hipHostGetDevicePointer((void **)&c->h_r2hist_dev, c->h_r2hist, 0));
+        }
+        if (!c->r2_event) HIPCHK(c, hipEventCreateWithFlags(&c->r2_event, hipEventDisableTiming));
+        G.r2hist = c->d_r2hist.as<uint32_t>();
+        G.r2hist_inv = 1.0f / p->initial_radius2;
+    }
     timer_begin(c, "gather", s);
     if (p->estimator == PM_ESTIMATOR_KNN) {
         G.knn_k = p->knn_lookup;
@@ -1148,6 +1300,19 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
     }
     c->rec_estimator = p->estimator;
     if (consume) c->rec_fresh = false;
+    if (hist) {
+        /* summed into host-mapped memory by a one-block kernel: no copy-engine
+         * transfer in the stream (a per-pass D2H copy cost ~0.5 ms of C2 step) */
+        HIPCHK(c, launch_r2hist_reduce(c->d_r2hist.as<uint32_t>(), c->h_r2hist_dev, s));
+        HIPCHK(c, hipEventRecord(c->r2_event, s));
+        c->r2_pending = true;
+        c->r2_wanted = false;
+        c->r2_valid = true;
+        c->r2_hist_init = p->initial_radius2;
+    } else if (p->estimator == PM_ESTIMATOR_KNN) {
+        c->r2_valid = false; /* r_k^2 replaced the radii */
+        c->design_r2 = 0.f;
+    }
     return PM_OK;
 }
 
@@ -1226,6 +1391,8 @@ int pm_set_radius2(void *ptr, const void *d_in, int64_t rec_begin, int64_t rec_c
     int rc;
     if ((rc = materialize_reset(c, pick(c, stream)))) return rc;
     HIPCHK(c, launch_radius2_io(recs(c), (float *)d_in, rec_begin, rec_count, 1, view_list(c), pick(c, stream)));
+    c->r2_valid = false; /* radii may have grown */
+    c->design_r2 = 0.f;
     return PM_OK;
 }
 
@@ -1443,6 +1610,9 @@ int pm_upload_records(void *ptr, const pm_record *in, int64_t n) {
     HIPCHK(c, hipMemcpy(c->d_n.p, N.data(), n * 4, hipMemcpyHostToDevice));
     c->rec_fresh = false; /* every record overwritten */
     c->tiles_valid = false;
+    c->order_valid = false;
+    c->r2_valid = false;
+    c->design_r2 = 0.f;
     if (c->view_active && (rc = build_view(c, c->stream))) return rc;
     return PM_OK;
 }
@@ -1615,6 +1785,8 @@ int pm_reset_records(void *ptr, const pm_render_params *p, void *stream) {
      * other reader applies it first (materialize_reset) */
     c->rec_fresh = true;
     c->rec_fresh_r2 = p->initial_radius2;
+    c->r2_valid = false;
+    c->design_r2 = 0.f;
     return PM_OK;
 }
 

@@ -372,13 +372,58 @@ constexpr uint32_t SPARSE_CELLS = 20;
 #endif
 constexpr int TILE_UMAX = PM_TILE_UMAX; /* C5: no cap 2.88 ms, 2048 0.44, 1024 0.41, 512 0.43 (per lane 0.42) */
 static_assert(2 * GROUP_R + 2 <= 8, "group rows exceed the 64-lane row map");
-template <int PARTIAL, int NN>
+/* the updated radii of a wave into the adaptive-grid histogram
+ * (GatherParams::r2hist): one atomic per distinct bin of the wave (a tile's
+ * radii are alike), in one of R2_COPIES copies by block */
+PMD void r2_histogram(const GatherParams &P, bool live, float r2) {
+    int b = -1;
+    if (live) {
+        const float t = r2 * P.r2hist_inv;
+        b = t >= 1.f ? 0 : !(t > 0.f) ? R2_BINS - 1 : min(R2_BINS - 1, (int)(-__log2f(t) * (float)R2_PER_OCTAVE));
+    }
+    unsigned long long pend = __ballot(b >= 0);
+    uint32_t *h = P.r2hist + (blockIdx.x % (unsigned)R2_COPIES) * R2_BINS;
+    while (pend) {
+        const int l = __builtin_ctzll(pend);
+        const int bb = __builtin_amdgcn_readlane(b, l);
+        const unsigned long long same = __ballot(b == bb);
+        if ((threadIdx.x & 63) == (unsigned)l) atomicAdd(&h[bb], (uint32_t)__builtin_popcountll(same));
+        pend &= ~same;
+    }
+}
+__global__ __launch_bounds__(R2_BINS) void k_r2hist_reduce(uint32_t *hist, uint32_t *out) {
+    const int b = threadIdx.x;
+    uint32_t t = 0u;
+    for (int k = 0; k < R2_COPIES; ++k) {
+        t += hist[k * R2_BINS + b];
+        hist[k * R2_BINS + b] = 0u; /* ready for the next histogram */
+    }
+    out[b] = t;
+}
+hipError_t launch_r2hist_reduce(uint32_t *hist, uint32_t *out_mapped, hipStream_t s) {
+    pm_launch(k_r2hist_reduce, dim3(1), dim3(R2_BINS), 0, s, hist, out_mapped);
+    return hipGetLastError();
+}
+/* KR: cells per axis a lane's box [p - r', p + r'] spans at most, for the
+ * grid's design radius (GatherParams::span: cell edge 2 r' / (KR - 1), the
+ * cell-edge sweep of DESIGN.md §5). A lane reads KR z-layers, each one
+ * contiguous run of <= KR rows of the union; its group radius keeps the union
+ * inside the 64-lane row map (2 GR + KR <= 8 rows per axis). */
+template <int KR>
+constexpr uint32_t tile_group_r() { return KR == 2 ? GROUP_R : (8u - (uint32_t)KR) / 2u; }
+template <int PARTIAL, int NN, int KR>
 __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherParams P) {
+    static_assert(KR >= 2 && KR <= 5 && 2 * tile_group_r<KR>() + KR <= 8, "lane box / group radius");
+    constexpr uint32_t GR = tile_group_r<KR>();
     __shared__ TileLds tiles[GATHER_BLOCK / 64];
     TileLds &T = tiles[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     int64_t r;
-    if (P.tiles) { /* only tiles with an active record (no block-level barrier below: a wave may leave) */
+    if (P.order) { /* active records in cell order (incoherent tiles); past the end: not live */
+        const int64_t i = ((int64_t)blockIdx.x * (GATHER_BLOCK / 64) + (threadIdx.x >> 6)) * 64 + lane;
+        if (i - lane >= P.n_order) return;
+        r = i < P.n_order ? (int64_t)P.order[i] : P.rec_end;
+    } else if (P.tiles) { /* only tiles with an active record (no block-level barrier below: a wave may leave) */
         const int64_t w = (int64_t)blockIdx.x * (GATHER_BLOCK / 64) + (threadIdx.x >> 6);
         if (w >= (P.n_tiles_dev ? (int64_t)*P.n_tiles_dev : P.n_tiles)) return;
         r = P.rec_begin + (int64_t)P.tiles[w] * 64 + lane;
@@ -388,6 +433,9 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
     const GridDesc &g = P.grid;
     GatherRec R;
     R.load<PARTIAL>(P, r);
+    /* a box of <= KR cells per axis takes part in the LDS groups; larger
+     * (radius above the grid's design radius) scans its own cells */
+    const bool small = R.live && R.r2 > 0.f && R.y1 - R.y0 < (uint32_t)KR && R.z1 - R.z0 < (uint32_t)KR;
     int M = 0;
     Fx3 Lf{0, 0, 0};
     const float sc = P.fx_scale;
@@ -402,12 +450,12 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
     const v3 fvs = R.fv * sc;
     const f2 px2 = {R.p.x, R.p.x}, py2 = {R.p.y, R.p.y}, pz2 = {R.p.z, R.p.z};
     /* Groups: the first pending lane leads; every pending lane whose box
-     * starts within GROUP_R cells of the leader's on each axis joins. A
-     * group's union box is at most (2 GROUP_R + 2)^3 cells (<= 8 x 8 rows),
-     * so it always fits the 64-lane row map; a coherent tile is one group, a
-     * tile across a depth edge two or three, never one huge box. */
-    bool pend = R.small;
-    bool direct = R.big; /* lanes that scan their own cells from global memory */
+     * starts within GR cells of the leader's on each axis joins. A group's
+     * union box is at most (2 GR + KR)^3 cells (<= 8 x 8 rows), so it always
+     * fits the 64-lane row map; a coherent tile is one group, a tile across a
+     * depth edge two or three, never one huge box. */
+    bool pend = small;
+    bool direct = R.live && R.r2 > 0.f && !small; /* lanes that scan their own cells from global memory */
     const int group_min =
         (uint64_t)P.cell_start[g.ncells] * SPARSE_CELLS < (uint64_t)g.ncells ? GROUP_MIN_SPARSE : GROUP_MIN;
     while (true) {
@@ -424,8 +472,7 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
             const int leader = __builtin_ctzll(pm);
             const uint32_t lx = __builtin_amdgcn_readlane(R.x0, leader), ly = __builtin_amdgcn_readlane(R.y0, leader),
                            lz = __builtin_amdgcn_readlane(R.z0, leader);
-            mine = pend && R.x0 + GROUP_R - lx <= 2u * GROUP_R && R.y0 + GROUP_R - ly <= 2u * GROUP_R &&
-                   R.z0 + GROUP_R - lz <= 2u * GROUP_R;
+            mine = pend && R.x0 + GR - lx <= 2u * GR && R.y0 + GR - ly <= 2u * GR && R.z0 + GR - lz <= 2u * GR;
             /* an incoherent tile (lanes on many far-apart surfaces, e.g. a
              * triangle soup) would need a group per few lanes: below
              * GROUP_MIN lanes the rest scan their own cells per lane */
@@ -455,18 +502,21 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
          * above TILE_UMAX photons the group's lanes scan their own cells */
         if (U > (uint32_t)TILE_UMAX) { direct = direct || mine; continue; }
         const uint32_t gofs = B - pre; /* photon index of concatenated position t in row u: t + gofs_u */
-        /* this lane's rows as two runs of the concatenation: rows (y0, z) and
-         * (y0 + 1, z) are neighbours in the union, so each z-layer of the
-         * lane's box is one contiguous run [sA, eA) / [sB, eB) */
+        /* this lane's rows as KR runs of the concatenation: rows (y0 .. y1, z)
+         * are neighbours in the union, so each z-layer of the lane's box is
+         * one contiguous run [s_k, e_k) */
         const uint32_t ny = mine ? R.y1 - R.y0 + 1u : 1u;
-        const int uA = mine ? (int)(((R.z0 - Z0) << LY) + (R.y0 - Y0)) : 0;
-        const int uB = mine && R.z1 > R.z0 ? uA + (1 << LY) : uA;
-        /* every lane shuffles: a bpermute from a lane that is inactive at the
-         * shuffle reads 0 */
-        const uint32_t sA0 = (uint32_t)__shfl((int)pre, uA), eA0 = (uint32_t)__shfl((int)incl, uA + (int)ny - 1);
-        const uint32_t sB0 = (uint32_t)__shfl((int)pre, uB), eB0 = (uint32_t)__shfl((int)incl, uB + (int)ny - 1);
-        const uint32_t sA = mine ? sA0 : 0u, eA = mine ? eA0 : 0u;
-        const uint32_t sB = mine && R.z1 > R.z0 ? sB0 : 0u, eB = mine && R.z1 > R.z0 ? eB0 : 0u;
+        const uint32_t nz = mine ? R.z1 - R.z0 + 1u : 0u;
+        uint32_t sK[KR], eK[KR];
+#pragma unroll
+        for (int k = 0; k < KR; ++k) {
+            /* every lane shuffles: a bpermute from a lane that is inactive at
+             * the shuffle reads 0 */
+            const int u = mine && (uint32_t)k < nz ? (int)(((R.z0 + (uint32_t)k - Z0) << LY) + (R.y0 - Y0)) : 0;
+            const uint32_t s0 = (uint32_t)__shfl((int)pre, u), e0 = (uint32_t)__shfl((int)incl, u + (int)ny - 1);
+            sK[k] = (uint32_t)k < nz ? s0 : 0u;
+            eK[k] = (uint32_t)k < nz ? e0 : 0u;
+        }
         for (uint32_t T0 = 0; T0 < U; T0 += TILE_CAP) {
             const uint32_t n = min((uint32_t)TILE_CAP, U - T0);
             TILE_STAT(1, 1);
@@ -508,7 +558,7 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
             wave_lds_sync();
             /* 3. each run of this lane within the window: LDS positions [base,
              * base + m). Tested two photons per packed instruction, 32
-             * positions at a time, into hit masks; the hits of both runs are
+             * positions at a time, into hit masks; the hits of all runs are
              * then summed in one loop with every lane busy (max over lanes of
              * its hits per chunk, not one masked pass per photon any lane hits). */
             auto test32 = [&](uint32_t base, uint32_t v0, uint32_t cnt, uint32_t m) {
@@ -539,25 +589,43 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
                     add_hit(Lf, R.ns, R.fv, make_float4(0.f, 0.f, 0.f, wi.x), qb4, wi.z, sc);
                 }
             };
-            const uint32_t loA = max(sA, T0), hiA = min(eA, T0 + n), mA = hiA > loA ? hiA - loA : 0u;
-            const uint32_t loB = max(sB, T0), hiB = min(eB, T0 + n), mB = hiB > loB ? hiB - loB : 0u;
-            const uint32_t baseA = mA ? loA - T0 : 0u, baseB = mB ? loB - T0 : 0u; /* < TILE_CAP */
-            const uint32_t vmaxA = wave_max_u32(mA), vmaxB = wave_max_u32(mB);
-            const uint32_t vmax = max(vmaxA, vmaxB);
+            uint32_t mK[KR], baseK[KR], vK[KR];
+            uint32_t vmax = 0u;
+#pragma unroll
+            for (int k = 0; k < KR; ++k) {
+                const uint32_t lo = max(sK[k], T0), hi = min(eK[k], T0 + n);
+                mK[k] = hi > lo ? hi - lo : 0u;
+                baseK[k] = mK[k] ? lo - T0 : 0u; /* < TILE_CAP */
+                vK[k] = wave_max_u32(mK[k]);
+                vmax = max(vmax, vK[k]);
+            }
             for (uint32_t vb = 0; vb < vmax; vb += 32) {
                 TILE_STAT(5, 1);
-                TILE_STAT(2, (min(32u, vmaxA > vb ? vmaxA - vb : 0u) + 1) / 2 + (min(32u, vmaxB > vb ? vmaxB - vb : 0u) + 1) / 2);
-                uint32_t bA = vmaxA > vb ? test32(baseA, vb, min(32u, vmaxA - vb), mA) : 0u;
-                uint32_t bB = vmaxB > vb ? test32(baseB, vb, min(32u, vmaxB - vb), mB) : 0u;
-                M += __builtin_popcount(bA) + __builtin_popcount(bB);
-                TILE_STAT(3, wave_max_u32(__builtin_popcount(bA) + __builtin_popcount(bB)));
-                while (bA | bB) {
-                    const bool fromA = bA != 0u;
-                    const uint32_t bits = fromA ? bA : bB;
-                    const uint32_t t = (fromA ? baseA : baseB) + vb + (uint32_t)__builtin_ctz(bits);
-                    const uint32_t rest = bits & (bits - 1u);
-                    bA = fromA ? rest : bA;
-                    bB = fromA ? bB : rest;
+                uint32_t bK[KR], any = 0u;
+                int nh = 0;
+#pragma unroll
+                for (int k = 0; k < KR; ++k) {
+                    TILE_STAT(2, (min(32u, vK[k] > vb ? vK[k] - vb : 0u) + 1) / 2);
+                    bK[k] = vK[k] > vb ? test32(baseK[k], vb, min(32u, vK[k] - vb), mK[k]) : 0u;
+                    nh += __builtin_popcount(bK[k]);
+                    any |= bK[k];
+                }
+                M += nh;
+                TILE_STAT(3, wave_max_u32(nh));
+                while (any) {
+                    /* the first run with a hit left: its lowest position */
+                    uint32_t t = 0u;
+                    bool took = false;
+                    any = 0u;
+#pragma unroll
+                    for (int k = 0; k < KR; ++k) {
+                        if (!took && bK[k]) {
+                            t = baseK[k] + vb + (uint32_t)__builtin_ctz(bK[k]);
+                            bK[k] &= bK[k] - 1u;
+                            took = true;
+                        }
+                        any |= bK[k];
+                    }
                     hit(t);
                 }
             }
@@ -570,13 +638,14 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
     if (NN) {
         if (dx < 0x1p53 && dy < 0x1p53 && dz < 0x1p53) { /* NaN / inf fail: int64 path */
             Lf.x = d2ll(dx); Lf.y = d2ll(dy); Lf.z = d2ll(dz);
-        } else if (R.small) { /* inexact (or NaN): this record again in int64 */
+        } else if (small) { /* inexact (or NaN): this record again in int64 */
             M = 0;
             direct = true;
         }
     }
     if (direct) lane_scan<0>(P, R.p, R.r2, R.ns, R.fv, R.x0, R.x1, R.y0, R.y1, R.z0, R.z1, M, Lf, nv, nr);
     R.store<PARTIAL>(P, r, M, Lf);
+    if (!PARTIAL && P.r2hist) r2_histogram(P, R.live, R.st.w);
 }
 
 /* Wave-cooperative bucket gather. A wave's 64 records are one 8x8 pixel
@@ -1522,24 +1591,38 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_kd(GatherParams P) {
     if (COUNT) count4(P.counters, vis, hits, rows, act);
 }
 
+template <int PARTIAL, int NN>
+static void launch_tile_nn(const GatherParams &p, unsigned g, hipStream_t s) {
+    switch (p.span) { /* cells per axis of a lane box at the grid's design radius */
+    case 2: pm_launch((k_gather_tile<PARTIAL, NN, 2>), dim3(g), dim3(GATHER_BLOCK), 0, s, p); break;
+    case 3: pm_launch((k_gather_tile<PARTIAL, NN, 3>), dim3(g), dim3(GATHER_BLOCK), 0, s, p); break;
+    case 4: pm_launch((k_gather_tile<PARTIAL, NN, 4>), dim3(g), dim3(GATHER_BLOCK), 0, s, p); break;
+    default: pm_launch((k_gather_tile<PARTIAL, NN, 5>), dim3(g), dim3(GATHER_BLOCK), 0, s, p); break;
+    }
+}
+template <int PARTIAL>
+static void launch_tile(const GatherParams &p, unsigned g, hipStream_t s) {
+    if (p.fx_nonneg) launch_tile_nn<PARTIAL, 1>(p, g, s);
+    else launch_tile_nn<PARTIAL, 0>(p, g, s);
+}
+
 template <int STRUCT, int PARTIAL, int COUNT>
 static void launch_g(const GatherParams &p, hipStream_t s) {
     unsigned grid = (unsigned)((p.rec_end - p.rec_begin + GATHER_BLOCK - 1) / GATHER_BLOCK);
-    if (STRUCT == PM_GATHER_GRID && !COUNT && p.kernel == PM_GK_TILE && p.tiles) {
-        /* the tile list: only tiles with an active record */
-        const unsigned g = (unsigned)((p.n_tiles + GATHER_BLOCK / 64 - 1) / (GATHER_BLOCK / 64));
+    if (STRUCT == PM_GATHER_GRID && !COUNT && p.kernel == PM_GK_TILE && (p.tiles || p.order)) {
+        /* the tile list: only tiles with an active record; or the active
+         * records in cell order, 64 per wave */
+        const int64_t waves = p.order ? (p.n_order + 63) / 64 : p.n_tiles;
+        const unsigned g = (unsigned)((waves + GATHER_BLOCK / 64 - 1) / (GATHER_BLOCK / 64));
         if (g == 0) return;
-        if (p.fx_nonneg) pm_launch((k_gather_tile<PARTIAL, 1>), dim3(g), dim3(GATHER_BLOCK), 0, s, p);
-        else pm_launch((k_gather_tile<PARTIAL, 0>), dim3(g), dim3(GATHER_BLOCK), 0, s, p);
+        launch_tile<PARTIAL>(p, g, s);
         return;
     }
     /* a counting launch always runs the per-lane kernel: its census (rows and
      * photons per RECORD) is the algorithm's unit count bench.py prices; the
      * tile and wave kernels find exactly the same photons (bit-identical records) */
-    if (STRUCT == PM_GATHER_GRID && !COUNT && p.kernel == PM_GK_TILE && p.fx_nonneg)
-        pm_launch((k_gather_tile<PARTIAL, 1>), dim3(grid), dim3(GATHER_BLOCK), 0, s, p);
-    else if (STRUCT == PM_GATHER_GRID && !COUNT && p.kernel == PM_GK_TILE)
-        pm_launch((k_gather_tile<PARTIAL, 0>), dim3(grid), dim3(GATHER_BLOCK), 0, s, p);
+    if (STRUCT == PM_GATHER_GRID && !COUNT && p.kernel == PM_GK_TILE)
+        launch_tile<PARTIAL>(p, grid, s);
     else if (STRUCT == PM_GATHER_GRID && !COUNT && p.kernel == PM_GK_WAVE)
         pm_launch((k_gather_wave<PARTIAL>), dim3(grid), dim3(GATHER_BLOCK), 0, s, p);
     else if (STRUCT == PM_GATHER_GRID)

@@ -64,6 +64,7 @@ struct EyeParams {
     uint32_t light_seed;
 };
 
+constexpr int R2_BINS = 64, R2_COPIES = 256, R2_PER_OCTAVE = 8; /* radius histogram (adaptive grid) */
 struct GridDesc {
     float gx, gy, gz, inv_cs;
     int dx, dy, dz;
@@ -98,6 +99,10 @@ struct TraceParams {
     int bucket;
     GridDesc grid;
     uint32_t *count, *key, *rank;
+    /* per-lane / pooled kernels: a path's deposits held in registers and
+     * written once per path (pm_trace.hip Held; used when mpc == 4 and the
+     * slot buffer is 16-B aligned) */
+    int hold;
 };
 
 struct GatherParams {
@@ -139,6 +144,16 @@ struct GatherParams {
      * scalar-cache experiment); census launches always run k_gather_grid */
     int kernel;
     int xcd; /* tile kernel: contiguous tile ranges per XCD (gather_block) */
+    int span; /* tile kernel: cells per axis of a lane box at the grid's design radius (2..5) */
+    /* non-null: k_gather_tile bins every updated radius, R2_COPIES x R2_BINS
+     * counters, bin = floor(-log2(r^2 * r2hist_inv) * R2_PER_OCTAVE) clamped */
+    uint32_t *r2hist;
+    float r2hist_inv;
+    /* non-null (k_gather_tile, full fused gathers of incoherent scenes): wave
+     * w gathers records order[64 w + lane] (< n_order), the active records in
+     * cell order, instead of tile w */
+    const uint32_t *order;
+    int64_t n_order;
     /* kNN estimator (k_gather_knn): knn_k nearest photons with d^2 < knn_r2;
      * per-record fixed-point scale = power of two below knn_fx * r_k^2;
      * slots = the slot buffer the buckets were built from (ph_b carries the
@@ -178,7 +193,11 @@ hipError_t launch_eye(const EyeParams &p, hipStream_t s);
 hipError_t launch_simple(const EyeParams &p, float *out, hipStream_t s);
 /* writes every slot of its paths (deposits, then zeros); count: census */
 /* resident waves of k_trace_pool per CU with `lds` bytes of dynamic LDS per block */
-int trace_pool_waves_per_cu(size_t lds);
+int trace_pool_waves_per_cu(size_t lds, int hold);
+int trace_lane_waves_per_cu(const SceneDev &S, size_t lds, int hold);
+/* adaptive-grid histogram: sum the R2_COPIES copies into host-mapped
+ * out[R2_BINS] with plain stores (no copy engine) and zero the copies */
+hipError_t launch_r2hist_reduce(uint32_t *hist, uint32_t *out_mapped, hipStream_t s);
 hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s);
 /* photon-bucket build (pm_bucket.hip): count + rank, scan, fill.
  * count and cell_start have ncells + 1 entries; cell_start[ncells] = valid
@@ -205,6 +224,12 @@ hipError_t launch_radius2_io(const RecordsDev &R, float *buf, int64_t rec_begin,
 /* exclusive scan of n uint32 (pm_bucket.hip); in/out 16-B aligned; sums: scan_scratch_words(n) */
 size_t scan_scratch_words(int64_t n);
 hipError_t launch_exclusive_scan(const uint32_t *in, int64_t n, uint32_t *out, uint32_t *sums, hipStream_t s);
+/* gather order of the active records (cell order on g) + tile census
+ * stats[0] = tiles whose union exceeds one group, stats[1] = active tiles;
+ * start[ncells] = number of active records */
+size_t record_order_scratch_words(int64_t nrec, uint32_t ncells);
+hipError_t launch_record_order(const RecordsDev &R, GridDesc g, float r2, uint32_t *count, uint32_t *start,
+                               uint32_t *scratch, uint32_t *order, unsigned long long *stats, hipStream_t s);
 /* active-record view: flags/rank n+1 words, list n words; rank[n] = active count */
 hipError_t launch_record_view(const RecordsDev &R, uint32_t *flags, uint32_t *rank, uint32_t *list, uint32_t *sums,
                               hipStream_t s);

@@ -264,6 +264,76 @@ PMD void flush_rank(const TraceParams &P, PathState &st) {
     if (st.pslot != PSLOT_NONE) { P.rank[st.pslot] = st.prank; st.pslot = PSLOT_NONE; }
 }
 
+/* HOLD kernels (k_trace_lane, k_trace_pool when max_photon_count is 4): a
+ * path's first three deposits wait in LDS until the path ends, then its
+ * 160-B slot block is written with 16-B stores, with its four bucket keys
+ * and ranks as one 16-B store each (the fourth deposit ends the path, so it
+ * is stored at once, next to the block's other writes). Writing each deposit
+ * as it happens (photontracing.cu:141-151's owner-writes) stored five 8-B
+ * pieces at a 160-B lane stride at different times, so L2 wrote partial lines
+ * back several times (PMC: 2.2x the slot + key + rank bytes at C2, 2.9x at
+ * C3). Registers were not an option: holding 36 words cost ~90 VGPRs in
+ * the brute-force trace (4 -> 3 waves/SIMD). LDS: HOLD_WORDS x TRACE_BLOCK
+ * words after the stacks and the scene blob, a column per thread. */
+constexpr int HOLD_MPC = 4;
+constexpr int HOLD_WORDS = 27; /* slots 0..2: p, alpha, wi */
+struct Held {
+    uint32_t *col;    /* this thread's LDS column: word i at col[i * TRACE_BLOCK] */
+    uint4 key, rank;  /* shift registers, .x the newest deposit's */
+};
+PMD void held_clear(Held &h) { (void)h; } /* deposits beyond the path's count are never read */
+PMD void held_put(Held &h, const TraceParams &P, size_t slot, uint32_t k, v3 p, v3 a, v3 wi, uint32_t key,
+                  uint32_t rank) {
+    if (k < 3u) {
+        uint32_t *c = h.col + 9u * k * TRACE_BLOCK;
+        c[0 * TRACE_BLOCK] = __float_as_uint(p.x); c[1 * TRACE_BLOCK] = __float_as_uint(p.y);
+        c[2 * TRACE_BLOCK] = __float_as_uint(p.z); c[3 * TRACE_BLOCK] = __float_as_uint(a.x);
+        c[4 * TRACE_BLOCK] = __float_as_uint(a.y); c[5 * TRACE_BLOCK] = __float_as_uint(a.z);
+        c[6 * TRACE_BLOCK] = __float_as_uint(wi.x); c[7 * TRACE_BLOCK] = __float_as_uint(wi.y);
+        c[8 * TRACE_BLOCK] = __float_as_uint(wi.z);
+    } else {
+        store_photon(P.slots + slot, p, a, wi); /* the last deposit: the block is written right after */
+    }
+    h.key = make_uint4(key, h.key.x, h.key.y, h.key.z);
+    h.rank = make_uint4(rank, h.rank.x, h.rank.y, h.rank.z);
+}
+/* the path's slot block (16-B aligned: 160 B per path from a 16-B aligned
+ * buffer, launch_trace checks): slots 0..2 from LDS (zero past the n
+ * deposits), slot 3 zero unless its deposit was stored; with fused counting
+ * the key and rank quads (key 0xffffffff past n) */
+PMD void held_write(const TraceParams &P, uint32_t pid, const Held &h, uint32_t n) {
+    const size_t path = (size_t)(pid - (uint64_t)P.slot_path_base);
+    uint32_t w[HOLD_WORDS];
+#pragma unroll
+    for (int i = 0; i < HOLD_WORDS; ++i) w[i] = (uint32_t)(i / 9) < n ? h.col[i * TRACE_BLOCK] : 0u;
+    const uint32_t va = n > 0u, vb = n > 1u, vc = n > 2u;
+    uint4 *dst = reinterpret_cast<uint4 *>(P.slots + path * HOLD_MPC);
+    dst[0] = make_uint4(va, w[0], w[1], w[2]);
+    dst[1] = make_uint4(w[3], w[4], w[5], w[6]);
+    dst[2] = make_uint4(w[7], w[8], vb, w[9]);
+    dst[3] = make_uint4(w[10], w[11], w[12], w[13]);
+    dst[4] = make_uint4(w[14], w[15], w[16], w[17]);
+    dst[5] = make_uint4(vc, w[18], w[19], w[20]);
+    dst[6] = make_uint4(w[21], w[22], w[23], w[24]);
+    if (n > 3u) {
+        reinterpret_cast<uint2 *>(dst + 7)[0] = make_uint2(w[25], w[26]); /* slot 3 already stored */
+    } else {
+        dst[7] = make_uint4(w[25], w[26], 0u, 0u);
+        dst[8] = make_uint4(0u, 0u, 0u, 0u);
+        dst[9] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (P.bucket) {
+        /* slot j = push n - 1 - j (wraps for j >= n: invalid) */
+        const uint32_t q0 = n - 1u, q1 = n - 2u, q2 = n - 3u, q3 = n - 4u;
+#define PICKQ(V, Q, DEF) ((Q) == 0u ? V.x : (Q) == 1u ? V.y : (Q) == 2u ? V.z : (Q) == 3u ? V.w : (DEF))
+        reinterpret_cast<uint4 *>(P.key)[path] = make_uint4(PICKQ(h.key, q0, 0xffffffffu), PICKQ(h.key, q1, 0xffffffffu),
+                                                            PICKQ(h.key, q2, 0xffffffffu), PICKQ(h.key, q3, 0xffffffffu));
+        reinterpret_cast<uint4 *>(P.rank)[path] = make_uint4(PICKQ(h.rank, q0, 0u), PICKQ(h.rank, q1, 0u),
+                                                             PICKQ(h.rank, q2, 0u), PICKQ(h.rank, q3, 0u));
+#undef PICKQ
+    }
+}
+
 /* Phase profile of k_trace (profiling builds only: `make prof` ->
  * lib/libpmhip_prof.so): per-wave s_memtime cycles accumulated per phase,
  * summed over waves into TraceParams::prof (pm_trace_profile). */
@@ -306,20 +376,24 @@ PMD bool emit_path(const TraceParams &P, const SceneDev &S, const uint32_t *perm
 
 /* one ray of a path: trace, then specular continuation or diffuse deposit +
  * Lambert bounce (photontracing.cu:119-183); false when the path ends */
-PMD bool path_shade(const TraceParams &P, const SceneDev &S, PathState &st, const Hit &h, TProf &prof);
+template <int HOLD>
+PMD bool path_shade(const TraceParams &P, const SceneDev &S, PathState &st, const Hit &h, TProf &prof, Held &held);
 
-template <int MODE, class C>
-PMD bool path_step(const TraceParams &P, const SceneDev &S, int *stack, PathState &st, C &cen, TProf &prof) {
+template <int MODE, int HOLD, class C>
+PMD bool path_step(const TraceParams &P, const SceneDev &S, int *stack, PathState &st, C &cen, TProf &prof,
+                   Held &held) {
     Hit h;
     const bool hit = traverse<false, MODE>(S, st.ray, h, stack, TRACE_BLOCK, cen);
     prof.mark(1);
     if (!hit) return false;
-    return path_shade(P, S, st, h, prof);
+    return path_shade<HOLD>(P, S, st, h, prof, held);
 }
 
 /* the hit of a path's ray: specular continuation, or diffuse deposit +
- * Lambert bounce (photontracing.cu:119-183); false when the path ends */
-PMD bool path_shade(const TraceParams &P, const SceneDev &S, PathState &st, const Hit &h, TProf &prof) {
+ * Lambert bounce (photontracing.cu:119-183); false when the path ends.
+ * HOLD: the deposit goes to `held` (written at path end, held_write) */
+template <int HOLD>
+PMD bool path_shade(const TraceParams &P, const SceneDev &S, PathState &st, const Hit &h, TProf &prof, Held &held) {
     const uint32_t mpc = (uint32_t)P.mpc;
     Geo g = shade(S, st.ray, h);
     v3 hit_point = st.ray.o + h.t * st.ray.d;
@@ -337,19 +411,24 @@ PMD bool path_shade(const TraceParams &P, const SceneDev &S, PathState &st, cons
     v3 wo = -st.ray.d;
     if (st.nI >= 1) {
         const size_t slot = (size_t)(st.pid - (uint64_t)P.slot_path_base) * mpc + (st.nI - 1);
-        store_photon(P.slots + slot, hit_point, st.alpha, wo);
+        if (!HOLD) store_photon(P.slots + slot, hit_point, st.alpha, wo);
         st.stored = st.nI;
+        uint32_t key = 0xffffffffu, rank = 0u;
         if (P.bucket) { /* fused counting pass of the bucket build (pm_bucket.hip k_bucket_count) */
             const GridDesc &g = P.grid;
             const uint32_t cx = cell_axis(hit_point.x, g.gx, g.inv_cs, g.dx);
             const uint32_t cy = cell_axis(hit_point.y, g.gy, g.inv_cs, g.dy);
             const uint32_t cz = cell_axis(hit_point.z, g.gz, g.inv_cs, g.dz);
-            const uint32_t key = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx + cx;
-            P.key[slot] = key;
-            const uint32_t rank = atomicAdd(&P.count[key], 1u);
-            flush_rank(P, st);
-            st.prank = rank; st.pslot = (uint32_t)slot;
+            key = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx + cx;
+            rank = atomicAdd(&P.count[key], 1u);
+            if (!HOLD) {
+                P.key[slot] = key;
+                flush_rank(P, st);
+                st.prank = rank; st.pslot = (uint32_t)slot;
+            }
         }
+        /* HOLD: the returned rank is first read at the path's end */
+        if (HOLD) held_put(held, P, slot, st.nI - 1, hit_point, st.alpha, wo, key, rank);
     }
     prof.mark(4);
     if (st.nI >= mpc) return false;
@@ -370,7 +449,9 @@ PMD bool path_shade(const TraceParams &P, const SceneDev &S, PathState &st, cons
 
 /* a finished path's unused slots are invalid = zero (the reference leaves
  * them stale, DESIGN.md divergences); written here instead of a memset pass */
-PMD void finish_path(const TraceParams &P, PathState &st) {
+template <int HOLD = 0>
+PMD void finish_path(const TraceParams &P, PathState &st, const Held *held = nullptr) {
+    if (HOLD) { held_write(P, st.pid, *held, st.stored); return; }
     flush_rank(P, st);
     const uint32_t mpc = (uint32_t)P.mpc;
     pm_photon *slots = P.slots + (size_t)(st.pid - (uint64_t)P.slot_path_base) * mpc;
@@ -450,7 +531,8 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceParams P) {
         prof.mark(0);
         if (alive) {
             ++rays;
-            alive = path_step<MODE>(P, S, stack, st, cen, prof);
+            Held none;
+            alive = path_step<MODE, 0>(P, S, stack, st, cen, prof, none);
             if (!alive) {
                 if (COUNT) deposits += st.stored;
                 finish_path(P, st);
@@ -493,7 +575,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceParams P) {
  * at least refill_min lanes (or all) have finished, the wave hands them the
  * next paths of its pool (ballot + popcount ranks). With wave_paths == 64
  * every lane runs exactly one path and a wave lives as long as its longest. */
-template <int COUNT, int MODE>
+template <int COUNT, int MODE, int HOLD>
 __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
     extern __shared__ __attribute__((aligned(16))) int stk[];
     __shared__ uint32_t perm[28];
@@ -511,6 +593,9 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
     const int64_t wend = wbegin + P.wave_paths < P.path_count ? wbegin + P.wave_paths : P.path_count;
     int64_t cursor = wbegin; /* wave-uniform: next unassigned path of the pool */
     PathState st;
+    Held held;
+    if (HOLD) /* after the stacks and the (16-B padded) scene blob */
+        held.col = reinterpret_cast<uint32_t *>(stk + P.S.stack_depth * TRACE_BLOCK + (MODE != MODE_GLOBAL ? (int)((P.S.lds_bytes + 15u) / 4u & ~3u) : 0)) + tid;
     bool alive = false;
     prof.begin();
     while (true) {
@@ -519,8 +604,9 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
         if (cursor < wend && (nidle >= P.refill_min || nidle == 64)) {
             const int64_t mine = cursor + __popcll(idle & ((1ull << lane) - 1ull));
             if (!alive && mine < wend) {
+                if (HOLD) held_clear(held);
                 alive = emit_path(P, S, perm, (uint32_t)(P.path_begin + mine), st);
-                if (!alive) finish_path(P, st);
+                if (!alive) finish_path<HOLD>(P, st, &held);
             }
             cursor = cursor + nidle < wend ? cursor + nidle : wend;
         }
@@ -531,10 +617,10 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
         }
         if (alive) {
             ++rays;
-            alive = path_step<MODE>(P, S, stack, st, cen, prof);
+            alive = path_step<MODE, HOLD>(P, S, stack, st, cen, prof, held);
             if (!alive) {
                 if (COUNT) deposits += st.stored;
-                finish_path(P, st);
+                finish_path<HOLD>(P, st, &held);
             }
         }
         prof.mark(2);
@@ -563,7 +649,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
 constexpr int POOL_STEPS = 4, POOL_SHADE_MIN = PM_POOL_SHADE_MIN;
 enum { PHASE_DEAD = 0, PHASE_TRAV = 1, PHASE_SHADE = 2 };
 
-template <int COUNT>
+template <int COUNT, int HOLD>
 #ifdef PM_POOL_EU /* experiment: make variant VFLAGS=-DPM_POOL_EU=5 */
 #define POOL_OCC __attribute__((amdgpu_waves_per_eu(PM_POOL_EU, PM_POOL_EU)))
 #else
@@ -586,6 +672,8 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
     int64_t cursor = wbegin; /* wave-uniform: next unassigned path of the pool */
     PathState st;
     TravState tr;
+    Held held;
+    if (HOLD) held.col = reinterpret_cast<uint32_t *>(stk + P.S.stack_depth * TRACE_BLOCK) + tid; /* after the stacks */
     int phase = PHASE_DEAD;
     while (true) {
         const unsigned long long travm = __ballot(phase == PHASE_TRAV);
@@ -597,13 +685,13 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
         if (travm == 0ull || waiting >= POOL_SHADE_MIN) {
             if (phase == PHASE_SHADE) {
                 ++rays;
-                bool alive = tr.best.ref != 0xffffffffu && path_shade(P, S, st, tr.best, prof);
+                bool alive = tr.best.ref != 0xffffffffu && path_shade<HOLD>(P, S, st, tr.best, prof, held);
                 if (alive) {
                     trav_begin(st.ray, tr);
                     phase = PHASE_TRAV;
                 } else {
                     if (COUNT) deposits += st.stored;
-                    finish_path(P, st);
+                    finish_path<HOLD>(P, st, &held);
                     phase = PHASE_DEAD;
                 }
             }
@@ -611,11 +699,12 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
             if (cursor < wend) {
                 const int64_t mine = cursor + __popcll(dm & ((1ull << lane) - 1ull));
                 if (phase == PHASE_DEAD && mine < wend) {
+                    if (HOLD) held_clear(held);
                     if (emit_path(P, S, perm, (uint32_t)(P.path_begin + mine), st)) {
                         trav_begin(st.ray, tr);
                         phase = PHASE_TRAV;
                     } else {
-                        finish_path(P, st);
+                        finish_path<HOLD>(P, st, &held);
                     }
                 }
                 cursor = cursor + __popcll(dm) < wend ? cursor + __popcll(dm) : wend;
@@ -650,10 +739,61 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
     }
 
 /* resident waves of the pooled kernel per CU at this LDS size (0 if unknown) */
-int trace_pool_waves_per_cu(size_t lds) {
+int trace_pool_waves_per_cu(size_t lds, int hold) {
     int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0>, TRACE_BLOCK, lds) != hipSuccess) return 0;
+    if (hold) lds += (size_t)HOLD_WORDS * TRACE_BLOCK * 4;
+    const hipError_t e = hold ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0, 1>, TRACE_BLOCK, lds)
+                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0, 0>, TRACE_BLOCK, lds);
+    if (e != hipSuccess) return 0;
     return blocks * (TRACE_BLOCK / 64);
+}
+
+/* resident waves per CU of the per-lane kernel (scene mode of S) with or
+ * without the held deposits' LDS: the host keeps HOLD only when it costs no
+ * waves (C2: one occupancy round of 4,096 waves) */
+int trace_lane_waves_per_cu(const SceneDev &S, size_t lds, int hold) {
+    int blocks = 0;
+    hipError_t e;
+    if (hold) {
+        lds += ((size_t)S.lds_bytes + 15u) / 16u * 16u - S.lds_bytes + (size_t)HOLD_WORDS * TRACE_BLOCK * 4;
+        switch (scene_mode(S)) {
+        case MODE_BRUTE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_lane<0, MODE_BRUTE, 1>, TRACE_BLOCK, lds); break;
+        case MODE_LDS: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_lane<0, MODE_LDS, 1>, TRACE_BLOCK, lds); break;
+        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_lane<0, MODE_GLOBAL, 1>, TRACE_BLOCK, lds); break;
+        }
+    } else {
+        switch (scene_mode(S)) {
+        case MODE_BRUTE: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_lane<0, MODE_BRUTE, 0>, TRACE_BLOCK, lds); break;
+        case MODE_LDS: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_lane<0, MODE_LDS, 0>, TRACE_BLOCK, lds); break;
+        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_lane<0, MODE_GLOBAL, 0>, TRACE_BLOCK, lds); break;
+        }
+    }
+    return e == hipSuccess ? blocks * (TRACE_BLOCK / 64) : 0;
+}
+
+/* deposits held in registers and written per path (Held): the reference's
+ * 4 photons per path, a 16-B aligned slot buffer; env PM_TRACE_HOLD=0 (read
+ * by pm_api.cpp into TraceParams::hold) keeps the per-deposit stores */
+static bool trace_hold(const TraceParams &p) {
+    return p.hold && p.mpc == HOLD_MPC && ((uintptr_t)p.slots & 15u) == 0u;
+}
+
+template <int HOLD>
+static void launch_lane(const TraceParams &p, dim3 grid, size_t lds, int count, hipStream_t s) {
+    switch (scene_mode(p.S)) {
+    case MODE_BRUTE:
+        if (count) pm_launch((k_trace_lane<1, MODE_BRUTE, HOLD>), grid, dim3(TRACE_BLOCK), lds, s, p);
+        else pm_launch((k_trace_lane<0, MODE_BRUTE, HOLD>), grid, dim3(TRACE_BLOCK), lds, s, p);
+        break;
+    case MODE_LDS:
+        if (count) pm_launch((k_trace_lane<1, MODE_LDS, HOLD>), grid, dim3(TRACE_BLOCK), lds, s, p);
+        else pm_launch((k_trace_lane<0, MODE_LDS, HOLD>), grid, dim3(TRACE_BLOCK), lds, s, p);
+        break;
+    default:
+        if (count) pm_launch((k_trace_lane<1, MODE_GLOBAL, HOLD>), grid, dim3(TRACE_BLOCK), lds, s, p);
+        else pm_launch((k_trace_lane<0, MODE_GLOBAL, HOLD>), grid, dim3(TRACE_BLOCK), lds, s, p);
+        break;
+    }
 }
 
 hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s) {
@@ -664,15 +804,22 @@ hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s) {
         q.wave_paths = p.pool_paths;
         const int64_t waves = (p.path_count + q.wave_paths - 1) / q.wave_paths;
         const unsigned grid = (unsigned)((waves + TRACE_BLOCK / 64 - 1) / (TRACE_BLOCK / 64));
-        if (count) pm_launch(k_trace_pool<1>, dim3(grid), dim3(TRACE_BLOCK), lds, s, q);
-        else pm_launch(k_trace_pool<0>, dim3(grid), dim3(TRACE_BLOCK), lds, s, q);
+        const bool hold = trace_hold(p);
+        const size_t lds_h = lds + (hold ? (size_t)HOLD_WORDS * TRACE_BLOCK * 4 : 0);
+        if (count && hold) pm_launch((k_trace_pool<1, 1>), dim3(grid), dim3(TRACE_BLOCK), lds_h, s, q);
+        else if (count) pm_launch((k_trace_pool<1, 0>), dim3(grid), dim3(TRACE_BLOCK), lds, s, q);
+        else if (hold) pm_launch((k_trace_pool<0, 1>), dim3(grid), dim3(TRACE_BLOCK), lds_h, s, q);
+        else pm_launch((k_trace_pool<0, 0>), dim3(grid), dim3(TRACE_BLOCK), lds, s, q);
         return hipGetLastError();
     }
     if (p.per_block == 0) {
         if (p.wave_paths < 64 || p.refill_min < 1) return hipErrorInvalidValue;
         const int64_t waves = (p.path_count + p.wave_paths - 1) / p.wave_paths;
         const unsigned grid = (unsigned)((waves + TRACE_BLOCK / 64 - 1) / (TRACE_BLOCK / 64));
-        PM_LAUNCH_MODES(k_trace_lane, dim3(grid), dim3(TRACE_BLOCK), lds, s, p, count);
+        if (trace_hold(p))
+            launch_lane<1>(p, dim3(grid), lds + ((size_t)p.S.lds_bytes + 15u) / 16u * 16u - p.S.lds_bytes +
+                                              (size_t)HOLD_WORDS * TRACE_BLOCK * 4, count, s);
+        else launch_lane<0>(p, dim3(grid), lds, count, s);
         return hipGetLastError();
     }
     if (p.per_block < 0) return hipErrorInvalidValue;

@@ -47,6 +47,29 @@ def test_photon_trace_bitexact(cornell, paths, pass_index):
     assert_bitexact(gpu, ref, "photon slots")
 
 
+@pytest.mark.parametrize("hold", ["0", "1"])
+@pytest.mark.parametrize("scene", ["cornell", "soup"])
+def test_photon_trace_write_modes_bitexact(hold, scene, oracle_mod, hip_mod, monkeypatch):
+    """Slots and the fused bucket counts are the same whether a path's
+    deposits are written as they happen (PM_TRACE_HOLD=0) or held and written
+    once per path with 16-B stores (default): brute-force and BVH scenes,
+    every slot bit-exact vs the oracle, map photons == valid slots."""
+    monkeypatch.setenv("PM_TRACE_HOLD", hold)
+    sc = scenes.cornell_box(32, 32) if scene == "cornell" else scenes.triangle_soup(20000, 32, 32)
+    ctx, orc = make_pair(sc, oracle_mod, hip_mod)
+    try:
+        paths = 32768
+        p = RenderParams.defaults(paths_per_pass=paths)
+        ctx.trace_photons(p, 1, 0, paths)
+        gpu = ctx.download_slots(paths * 4)
+        ref = orc.trace_photons(p, 1, 0, paths)
+        assert_bitexact(gpu, ref, f"slots (hold={hold}, {scene})")
+        ctx.build_photon_map(p, paths * 4)
+        assert ctx.map_info()["valid"] == int((ref["bits"] & 1).sum()) > paths // 2
+    finally:
+        ctx.close()
+
+
 def test_photon_trace_sharded_equals_whole(cornell):
     """Global path ids: two shards traced separately == one launch (owner-writes)."""
     ctx, orc = cornell
@@ -178,7 +201,11 @@ def test_bucket_gather_kernels_agree(radius2, W, H, paths, oracle_mod, hip_mod, 
     wave-cooperative scalar-cache experiment and the per-lane kernel give
     bit-identical fused records and split partials. radius2 25 makes the
     unions of a tile exceed one LDS window (several windows); 400 exceeds the
-    grid's design radius for uploaded records -> the per-lane fallbacks."""
+    grid's design radius for uploaded records -> the per-lane fallbacks.
+    PM_CELL_SPAN 3..5: finer bucket cells (edge 2 r / (span - 1)), the tile
+    kernel's lanes reading span z-runs of span rows each. PM_REC_ORDER=1:
+    waves over the active records in cell order instead of pixel tiles (the
+    partials are by record, so they are compared too)."""
     torch = pytest.importorskip("torch")
     sc = scenes.cornell_box(W, H)
     orc = sc.load_into(oracle_mod.Oracle())
@@ -187,8 +214,13 @@ def test_bucket_gather_kernels_agree(radius2, W, H, paths, oracle_mod, hip_mod, 
     outs = {}
     for name, env in (("lane", {"PM_GATHER_KERNEL": "lane"}), ("tile", {"PM_GATHER_KERNEL": "tile"}),
                       ("tile_xcd", {"PM_GATHER_KERNEL": "tile", "PM_GATHER_XCD": "1"}),
-                      ("wave", {"PM_GATHER_KERNEL": "wave"})):
-        for k in ("PM_GATHER_KERNEL", "PM_GATHER_XCD"):
+                      ("wave", {"PM_GATHER_KERNEL": "wave"}),
+                      ("tile_span3", {"PM_GATHER_KERNEL": "tile", "PM_CELL_SPAN": "3"}),
+                      ("tile_span4", {"PM_GATHER_KERNEL": "tile", "PM_CELL_SPAN": "4"}),
+                      ("tile_span5", {"PM_GATHER_KERNEL": "tile", "PM_CELL_SPAN": "5"}),
+                      ("lane_span3", {"PM_GATHER_KERNEL": "lane", "PM_CELL_SPAN": "3"}),
+                      ("tile_order", {"PM_GATHER_KERNEL": "tile", "PM_REC_ORDER": "1"})):
+        for k in ("PM_GATHER_KERNEL", "PM_GATHER_XCD", "PM_CELL_SPAN", "PM_REC_ORDER"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -207,9 +239,72 @@ def test_bucket_gather_kernels_agree(radius2, W, H, paths, oracle_mod, hip_mod, 
             ctx.close()
     ref_rec, ref_part = outs["lane"]
     assert (ref_part[:, 0] > 0).sum() > 100
-    for name in ("tile", "tile_xcd", "wave"):
+    for name in ("tile", "tile_xcd", "wave", "tile_span3", "tile_span4", "tile_span5", "lane_span3", "tile_order"):
         assert np.array_equal(outs[name][1], ref_part), name
         assert_bitexact(outs[name][0], ref_rec, f"{name} vs per-lane gather")
+
+
+def test_adaptive_grid_radius_progressive(oracle_mod, hip_mod, monkeypatch):
+    """Progressive passes size the photon grid from the records' current
+    radii (a histogram binned by the fused gather, PM_GRID_QUANTILE; records
+    above the grid's radius scan their own cells): 8 passes with the grid
+    fixed at the initial radius (0), the default quantile and an aggressive
+    one (0.5: half the records scan per lane) give identical records, and
+    match the oracle's kd-tree passes (N', r^2 exact)."""
+    sc = scenes.caustic_scene(96, 72)
+    orc = sc.load_into(oracle_mod.Oracle())
+    p = RenderParams.defaults(paths_per_pass=32768, initial_radius2=25.0)
+    outs = {}
+    for q in ("0", "0.99", "0.5"):
+        monkeypatch.setenv("PM_GRID_QUANTILE", q)
+        ctx = sc.load_into(hip_mod.Context(0))
+        try:
+            ctx.eye_pass(p)
+            for k in range(8):
+                ctx.trace_photons(p, k, 0, p.paths_per_pass)
+                ctx.build_photon_map(p, p.paths_per_pass * 4)
+                ctx.gather(p)
+                ctx.synchronize()  # lets each histogram land before the next pass picks its grid
+            outs[q] = (ctx.download_records(), ctx.map_info())
+        finally:
+            ctx.close()
+    ref = orc.eye_pass(p)
+    for k in range(8):
+        orc.gather(orc.build_kdtree(orc.trace_photons(p, k, 0, p.paths_per_pass)), ref, p)
+    assert (ref["photon_count"] > 0).sum() > 1000
+    for q in ("0.99", "0.5"):
+        assert_bitexact(outs[q][0], outs["0"][0], f"records, grid quantile {q} vs fixed grid")
+    assert outs["0.5"][1]["cells"] > outs["0"][1]["cells"], "the grid did not follow the shrinking radii"
+    compare_gathered_records(outs["0"][0], ref, flux_rtol=5e-5)
+
+
+@pytest.mark.parametrize("order", ["0", "1", "-1"])
+def test_record_order_gather_soup(order, oracle_mod, hip_mod, monkeypatch):
+    """Incoherent tiles (a triangle soup: neighbouring pixels on unrelated
+    triangles): the fused gather over the active records in cell order
+    (PM_REC_ORDER=1, and the auto choice -1) gives the records of the tile
+    gather (0) bit for bit, and both match the oracle (M -> N', r^2 exact)."""
+    monkeypatch.setenv("PM_REC_ORDER", order)
+    sc = scenes.triangle_soup(50000, 160, 120)
+    ctx, orc = make_pair(sc, oracle_mod, hip_mod)
+    try:
+        p = RenderParams.defaults(paths_per_pass=65536, initial_radius2=25.0)
+        recs = orc.eye_pass(p)
+        slots = orc.trace_photons(p, 0, 0, 65536)
+        ctx.eye_pass(p)
+        ctx.trace_photons(p, 0, 0, 65536)
+        ctx.build_photon_map(p, 65536 * 4)
+        ctx.gather(p)
+        ctx.gather(p)  # a second pass over the same map: PPM state carried
+        got = ctx.download_records()
+        ref = recs.copy()
+        nodes = orc.build_kdtree(slots)
+        orc.gather(nodes, ref, p)
+        orc.gather(nodes, ref, p)
+        assert (ref["photon_count"] > 0).sum() > 1000
+        compare_gathered_records(got, ref)
+    finally:
+        ctx.close()
 
 
 def test_partial_plus_update_equals_fused(cornell):
