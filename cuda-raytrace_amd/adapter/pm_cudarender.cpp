@@ -5,6 +5,8 @@
  */
 #include "pm_cudarender.h"
 
+#include <cstdlib>
+
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -103,9 +105,33 @@ static DiskFrame disk_frame(const Shape &d) {
 }
 
 /* ------------------------------------------------------------ CudaRender */
+/* PM_DEVICES="0,1,...": one context over those devices of the node
+ * (pm_config::n_devices: photon shards, RCCL all-gather, 8-row bands per
+ * device), so the plugin pbrt loads renders on the whole node; unset: the
+ * one device given (PM_DEVICE in cudaapi.cpp). */
+static std::vector<int> device_list_env() {
+    std::vector<int> devs;
+    const char *e = std::getenv("PM_DEVICES");
+    if (!e) return devs;
+    std::string s(e);
+    size_t i = 0;
+    while (i < s.size()) {
+        size_t j = s.find(',', i);
+        if (j == std::string::npos) j = s.size();
+        if (j > i) devs.push_back(std::atoi(s.substr(i, j - i).c_str()));
+        i = j + 1;
+    }
+    return devs;
+}
+
 CudaRender::CudaRender(int device) {
     pm_config cfg{};
     cfg.device = device;
+    const std::vector<int> devs = device_list_env();
+    if (!devs.empty()) {
+        cfg.n_devices = (int)devs.size();
+        cfg.devices = devs.data();
+    }
     if (pm_create(&ctx_, &cfg) != PM_OK) throw Error(std::string("pm_create: ") + pm_last_error(nullptr));
 }
 

@@ -6,6 +6,7 @@
  * kernels and fails with PM_ERR_HIP when the device is unusable.
  */
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -48,7 +49,9 @@ struct HTri { int v[3]; int mesh; };
 struct Timer { hipEvent_t a = nullptr, b = nullptr; };
 struct TimerPool { std::vector<Timer> ev; size_t used = 0; };
 
+struct Group;
 struct Ctx {
+    Group *group = nullptr; /* non-null: a multi-device context (pm_config::n_devices), Group below */
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
@@ -182,12 +185,46 @@ struct Ctx {
         if (_e != hipSuccess) FAIL(c, PM_ERR_HIP, "%s: %s", #expr, hipGetErrorString(_e)); \
     } while (0)
 
-#define GETCTX(ptr)                                                  \
-    Ctx *c = (Ctx *)(ptr);                                           \
-    if (!c) FAIL((Ctx *)nullptr, PM_ERR_INVALID, "null context");    \
+#define GETCTX(ptr)                                                                                      \
+    Ctx *c = (Ctx *)(ptr);                                                                               \
+    if (!c) FAIL((Ctx *)nullptr, PM_ERR_INVALID, "null context");                                        \
+    if (c->group)                                                                                        \
+        FAIL(c, PM_ERR_INVALID, "%s: a multi-device context takes the scene calls, pm_render and "       \
+                                "pm_render_simple (the stage API needs one context per device)", __func__); \
     (void)hipSetDevice(c->device)
 
 hipStream_t pick(Ctx *c, void *s) { return s ? (hipStream_t)s : c->stream; }
+
+/* Single-process multi-device context (north_star: tiles and
+ * photon batches over the GPUs of one node, RCCL all-gather of the photon
+ * slots before the gather): one sub-context per device holds the whole
+ * scene and record set; pm_render shards the paths by global id, all-gathers
+ * the 40-B slots into every device's buffer (ncclAllGather over xGMI when the
+ * devices are distinct, peer copies otherwise), builds the same map on every
+ * device and gathers interleaved 8-row bands per device (pmrender/dist.py
+ * _bands: runs of bands dealt round-robin, about four per device). */
+struct Group {
+    std::vector<Ctx *> subs;
+    std::vector<int> devs;
+    std::vector<ncclComm_t> comms; /* empty: peer-copy exchange */
+    std::vector<hipEvent_t> ev;    /* per sub: end of its trace (peer-copy exchange) */
+};
+Group *group_of(void *ptr) { return ptr ? ((Ctx *)ptr)->group : nullptr; }
+int group_fail(void *ptr, Ctx *sub, int rc) {
+    Ctx *c = (Ctx *)ptr;
+    c->err = "device " + std::to_string(sub->device) + ": " + sub->err;
+    g_last_error = c->err;
+    return rc;
+}
+/* scene calls go to every device's context */
+#define GROUP_FWD(ptr, CALL)                                                                                  \
+    if (Group *g_ = group_of(ptr)) {                                                                          \
+        for (Ctx *sub : g_->subs) {                                                                           \
+            const int rc_ = (CALL);                                                                           \
+            if (rc_) return group_fail(ptr, sub, rc_);                                                        \
+        }                                                                                                     \
+        return PM_OK;                                                                                         \
+    }
 
 } // namespace
 thread_local pm::StageEvents *pm::g_stage = nullptr;
@@ -463,6 +500,51 @@ void pm_default_params(pm_render_params *p) {
 int pm_create(void **out, const pm_config *cfg) {
     if (!out) FAIL((Ctx *)nullptr, PM_ERR_INVALID, "null output pointer");
     *out = nullptr;
+    if (cfg && cfg->n_devices > 0) { /* multi-device context (Group) */
+        if (!cfg->devices || cfg->n_devices > 64) FAIL((Ctx *)nullptr, PM_ERR_INVALID, "bad device list");
+        Ctx *gc = new Ctx();
+        gc->group = new Group();
+        Group &G = *gc->group;
+        bool distinct = true;
+        for (int i = 0; i < cfg->n_devices; ++i) {
+            pm_config one{};
+            one.device = cfg->devices[i];
+            void *sub = nullptr;
+            if (pm_create(&sub, &one) != PM_OK) {
+                const std::string e = g_last_error;
+                pm_destroy(gc);
+                FAIL((Ctx *)nullptr, PM_ERR_HIP, "device %d: %s", cfg->devices[i], e.c_str());
+            }
+            for (int d : G.devs) distinct = distinct && d != one.device;
+            G.subs.push_back((Ctx *)sub);
+            G.devs.push_back(one.device);
+            hipEvent_t ev = nullptr;
+            (void)hipSetDevice(one.device);
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+                pm_destroy(gc);
+                FAIL((Ctx *)nullptr, PM_ERR_HIP, "hipEventCreate on device %d", one.device);
+            }
+            G.ev.push_back(ev);
+        }
+        gc->device = G.devs[0];
+        const char *re = getenv("PM_GROUP_RCCL"); /* 0: peer copies even on distinct devices */
+        if (distinct && !(re && atoi(re) == 0)) {
+            G.comms.resize(G.devs.size());
+            const ncclResult_t r = ncclCommInitAll(G.comms.data(), (int)G.devs.size(), G.devs.data());
+            if (r != ncclSuccess) {
+                G.comms.clear();
+                pm_destroy(gc);
+                FAIL((Ctx *)nullptr, PM_ERR_HIP, "ncclCommInitAll over %d devices: %s", cfg->n_devices, ncclGetErrorString(r));
+            }
+        } else if (distinct) {
+            for (int a : G.devs)
+                for (int b : G.devs)
+                    if (a != b) { (void)hipSetDevice(a); (void)hipDeviceEnablePeerAccess(b, 0); }
+            (void)hipGetLastError(); /* already-enabled peers are not errors here */
+        }
+        *out = gc;
+        return PM_OK;
+    }
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev == 0)
@@ -506,6 +588,14 @@ int pm_create(void **out, const pm_config *cfg) {
 void pm_destroy(void *ptr) {
     Ctx *c = (Ctx *)ptr;
     if (!c) return;
+    if (Group *g = c->group) {
+        for (ncclComm_t cm : g->comms) (void)ncclCommDestroy(cm);
+        for (size_t i = 0; i < g->ev.size(); ++i) { (void)hipSetDevice(g->devs[i]); (void)hipEventDestroy(g->ev[i]); }
+        for (Ctx *sub : g->subs) pm_destroy(sub);
+        delete g;
+        delete c;
+        return;
+    }
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (auto &kv : c->timers)
@@ -548,6 +638,7 @@ int pm_halton_permutation(uint32_t seed, uint32_t out[28]) {
 
 /* ------------------------------------------------------------------ scene */
 int pm_add_material(void *ptr, int type, const float rgb[3], int *out_id) {
+    GROUP_FWD(ptr, pm_add_material(sub, type, rgb, out_id));
     GETCTX(ptr);
     if (type != PM_MATTE && type != PM_MIRROR && type != PM_GLASS) FAIL(c, PM_ERR_INVALID, "bad material type %d", type);
     float r = rgb ? rgb[0] : 0.f, g = rgb ? rgb[1] : 0.f, b = rgb ? rgb[2] : 0.f;
@@ -559,6 +650,7 @@ int pm_add_material(void *ptr, int type, const float rgb[3], int *out_id) {
 
 int pm_add_trimesh(void *ptr, const float *P, int nverts, const int *idx, int ntris, const float *N, const float *uv,
                    int material, int light) {
+    GROUP_FWD(ptr, pm_add_trimesh(sub, P, nverts, idx, ntris, N, uv, material, light));
     GETCTX(ptr);
     if (!P || !idx || nverts <= 0 || ntris <= 0) FAIL(c, PM_ERR_INVALID, "empty or null mesh");
     if (material < 0 || material >= (int)c->materials.size()) FAIL(c, PM_ERR_INVALID, "bad material id %d", material);
@@ -579,6 +671,7 @@ int pm_add_trimesh(void *ptr, const float *P, int nverts, const int *idx, int nt
 }
 
 int pm_add_sphere(void *ptr, float radius, const float o2w[16], const float w2o[16], int material, int light) {
+    GROUP_FWD(ptr, pm_add_sphere(sub, radius, o2w, w2o, material, light));
     GETCTX(ptr);
     if (!o2w || !w2o || !(radius > 0.f)) FAIL(c, PM_ERR_INVALID, "bad sphere");
     if (material < 0 || material >= (int)c->materials.size()) FAIL(c, PM_ERR_INVALID, "bad material id %d", material);
@@ -594,6 +687,7 @@ int pm_add_sphere(void *ptr, float radius, const float o2w[16], const float w2o[
 /* derived uniforms as cudadisk.cpp:24-43 computes them */
 int pm_add_disk(void *ptr, const float o[3], const float x[3], const float y[3], const float z[3], float inner,
                 float phimax, int material, int light) {
+    GROUP_FWD(ptr, pm_add_disk(sub, o, x, y, z, inner, phimax, material, light));
     GETCTX(ptr);
     if (!o || !x || !y || !z) FAIL(c, PM_ERR_INVALID, "null disk vector");
     if (material < 0 || material >= (int)c->materials.size()) FAIL(c, PM_ERR_INVALID, "bad material id %d", material);
@@ -610,6 +704,7 @@ int pm_add_disk(void *ptr, const float o[3], const float x[3], const float y[3],
 }
 
 int pm_add_light_point(void *ptr, const float pos[3], const float I[3]) {
+    GROUP_FWD(ptr, pm_add_light_point(sub, pos, I));
     GETCTX(ptr);
     if (!pos || !I) FAIL(c, PM_ERR_INVALID, "null point light");
     LightDev L{};
@@ -625,6 +720,7 @@ int pm_add_light_point(void *ptr, const float pos[3], const float I[3]) {
 
 int pm_add_light_disk(void *ptr, const float o[3], const float p1[3], const float p2[3], const float n[3],
                       const float Le[3], float area, int nsamples) {
+    GROUP_FWD(ptr, pm_add_light_disk(sub, o, p1, p2, n, Le, area, nsamples));
     GETCTX(ptr);
     if (!o || !p1 || !p2 || !n || !Le) FAIL(c, PM_ERR_INVALID, "null disk light vector");
     int ns = std::max(1, nsamples);
@@ -642,6 +738,7 @@ int pm_add_light_disk(void *ptr, const float o[3], const float p1[3], const floa
 
 int pm_set_pinhole(void *ptr, const float eye[3], const float fwd[3], const float right[3], const float up[3], int W,
                    int H) {
+    GROUP_FWD(ptr, pm_set_pinhole(sub, eye, fwd, right, up, W, H));
     GETCTX(ptr);
     if (W <= 0 || H <= 0 || !eye || !fwd || !right || !up) FAIL(c, PM_ERR_INVALID, "bad pinhole camera");
     c->pinhole = 1; c->W = W; c->H = H;
@@ -651,6 +748,7 @@ int pm_set_pinhole(void *ptr, const float eye[3], const float fwd[3], const floa
 }
 
 int pm_set_eye_rays(void *ptr, const float *rays, int64_t nrays, const float *rand2d, int n2d) {
+    GROUP_FWD(ptr, pm_set_eye_rays(sub, rays, nrays, rand2d, n2d));
     GETCTX(ptr);
     if (!rays || nrays <= 0) FAIL(c, PM_ERR_INVALID, "no rays");
     c->pinhole = 0;
@@ -669,6 +767,7 @@ int pm_set_eye_rays(void *ptr, const float *rays, int64_t nrays, const float *ra
 }
 
 int pm_commit(void *ptr) {
+    GROUP_FWD(ptr, pm_commit(sub));
     GETCTX(ptr);
     if (c->lights.empty()) FAIL(c, PM_ERR_INVALID, "scene has no lights");
     const int64_t nt = (int64_t)c->tris.size(), nd = (int64_t)c->disks.size() / 5,
@@ -804,7 +903,7 @@ int pm_commit(void *ptr) {
      * node fetches per ray); env PM_BVH_WIDE=0 keeps the binary traversal,
      * PM_BVH4_LEAF sets the largest subtree folded into one leaf */
     size_t o_wnodes = 0;
-    int wide = 0, wide_stack = 0;
+    int wide = 0, wide_stack = 0, nodelets = 0;
     if (blob.size() > LDS_SCENE_MAX) {
         const char *we = getenv("PM_BVH_WIDE");
         if (!we || atoi(we) != 0) {
@@ -818,6 +917,12 @@ int pm_commit(void *ptr) {
             /* a leaf the quantized count cannot code (>= LEAF_TRIS primitives,
              * possible at build_bvh's depth limit) keeps the binary traversal,
              * like a tree whose stack bound exceeds BVH_STACK */
+            /* env PM_NODELETS=N: the pooled trace kernel keeps the first N nodes
+             * in LDS, the tree renumbered breadth-first so that they are its
+             * top levels (PM_BVH4_BFS=1 renumbers without nodelets) */
+            const char *nl = getenv("PM_NODELETS"), *bf = getenv("PM_BVH4_BFS");
+            nodelets = nl ? std::max(0, atoi(nl)) : 0;
+            if (nodelets > 0 || (bf && atoi(bf) != 0)) bvh4_bfs_order(w.nodes);
             const bool coded = !quant || quantize_bvh4(w.nodes, lt && atoi(lt) == 0 ? std::vector<uint32_t>() : bvh.refs, qn);
             if (coded && w.max_stack <= BVH_STACK) {
                 o_wnodes = quant ? put(qn.data(), qn.size() * sizeof(uint32_t))
@@ -854,6 +959,7 @@ int pm_commit(void *ptr) {
     S.stack_depth = std::min(BVH_STACK, std::max(2, c->bvh_depth + 2));
     S.wide = wide;
     S.wnodes = wide ? (const float4 *)(base + o_wnodes) : nullptr;
+    S.nodelets = wide == 2 ? (int)std::min<int64_t>(nodelets, c->bvh4_nodes) : 0;
     /* wide scenes traverse only the 4-wide tree (traverse() dispatches every
      * MODE_GLOBAL query to traverse4): its exact stack bound sizes the LDS
      * stacks, not the binary tree's depth — k_trace_pool's 256-thread blocks
@@ -1055,7 +1161,7 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
         if (waves <= 0) {
             int cus = 0;
             if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0) cus = 256;
-            const size_t lds = (size_t)c->S.stack_depth * TRACE_BLOCK * 4 + c->S.lds_bytes;
+            const size_t lds = (size_t)c->S.stack_depth * TRACE_BLOCK * 4 + c->S.lds_bytes + (size_t)c->S.nodelets * 64;
             int per_cu = trace_pool_waves_per_cu(lds, 0);
             if (T.hold && c->S.wide) { /* pooled kernel: the held deposits' LDS must not cost resident waves */
                 const int per_cu_h = trace_pool_waves_per_cu(lds, 1);
@@ -1415,7 +1521,166 @@ int pm_final(void *ptr, double emitted, int64_t rec_begin, int64_t rec_count, vo
 }
 
 /* ------------------------------------------------------------ whole render */
+/* the all-gather mode's record ranges of each device: 8-row bands (`unit`
+ * records each) in runs dealt round-robin, about four runs per device
+ * (pmrender/dist.py _bands) */
+static std::vector<std::vector<std::pair<int64_t, int64_t>>> device_bands(int64_t n, int64_t unit, int world) {
+    std::vector<std::vector<std::pair<int64_t, int64_t>>> owned(world);
+    const int64_t units = (n + unit - 1) / unit;
+    const int64_t runs = std::max<int64_t>(1, (units + (int64_t)world * 4 - 1) / ((int64_t)world * 4));
+    int k = 0;
+    for (int64_t u = 0; u < units; u += runs, ++k) {
+        const int64_t b = u * unit, e = std::min(n, (u + runs) * unit);
+        owned[k % world].push_back({b, e - b});
+    }
+    return owned;
+}
+
+/* one progressive render over the group's devices (Group): per pass every
+ * device traces its shard of the global paths into its own slot buffer at
+ * the shard's global slot offset, the shards are all-gathered (equal
+ * chunks, the last padded with invalid slots), every device builds the full
+ * map and gathers its bands; the final pass writes each device's bands into
+ * the host image. Bit-identical to one device rendering all the paths (the
+ * same valid photons in the map; exact, order-free gather sums). */
+static int group_render(Ctx *gc, const pm_render_params *p, float *out_rgb, pm_stats *st) {
+    Group &G = *gc->group;
+    const int n = (int)G.subs.size();
+    if (!p || !out_rgb) FAIL(gc, PM_ERR_INVALID, "null params / output");
+    if (p->passes < 1 || p->paths_per_pass < 1) FAIL(gc, PM_ERR_INVALID, "passes and paths_per_pass must be >= 1");
+    const int64_t P = p->paths_per_pass, mpc = p->max_photon_count;
+    const int64_t chunk = (P + n - 1) / n;                 /* paths per device (the last one may trace fewer) */
+    const int64_t total_slots = chunk * n * mpc;
+    const size_t chunk_bytes = (size_t)(chunk * mpc) * sizeof(pm_photon);
+    int rc;
+    auto sub_fail = [&](Ctx *sub, int code) { return group_fail(gc, sub, code); };
+    std::vector<pm_photon *> slots(n);
+    for (int d = 0; d < n; ++d) {
+        Ctx *c = G.subs[d];
+        (void)hipSetDevice(c->device);
+        if ((rc = pm_eye_pass(c, p, nullptr))) return sub_fail(c, rc);
+        if ((rc = pm_reserve_slots(c, total_slots, (void **)&slots[d]))) return sub_fail(c, rc);
+    }
+    Ctx *c0 = G.subs[0];
+    const int64_t nrec = c0->nrec;
+    const int64_t unit = c0->pinhole ? (int64_t)((c0->W + 7) / 8) * 64 : 512;
+    const auto bands = device_bands(nrec, unit, n);
+    int64_t nvalid = 0;
+    double t_trace = 0, t_build = 0, t_gather = 0;
+    for (int pass = 0; pass < p->passes; ++pass) {
+        for (int d = 0; d < n; ++d) {
+            Ctx *c = G.subs[d];
+            (void)hipSetDevice(c->device);
+            const int64_t b = d * chunk, cnt = std::max<int64_t>(0, std::min(chunk, P - b));
+            if (cnt > 0 && (rc = pm_trace_photons(c, p, pass, b, cnt, 0, nullptr))) return sub_fail(c, rc);
+            if (cnt < chunk) /* padding slots of a short shard: invalid */
+                HIPCHK(gc, hipMemsetAsync(slots[d] + (b + cnt) * mpc, 0, (size_t)((chunk - cnt) * mpc) * sizeof(pm_photon),
+                                          c->stream));
+            if (d == 0) t_trace += timer_ms(c, "trace");
+        }
+        /* all-gather of the shards: every buffer gets every device's chunk */
+        if (!G.comms.empty()) {
+            if (ncclGroupStart() != ncclSuccess) FAIL(gc, PM_ERR_HIP, "ncclGroupStart");
+            for (int d = 0; d < n; ++d) {
+                Ctx *c = G.subs[d];
+                (void)hipSetDevice(c->device);
+                const ncclResult_t r = ncclAllGather((const char *)slots[d] + d * chunk_bytes, slots[d], chunk_bytes,
+                                                     ncclUint8, G.comms[d], c->stream);
+                if (r != ncclSuccess) { (void)ncclGroupEnd(); FAIL(gc, PM_ERR_HIP, "ncclAllGather: %s", ncclGetErrorString(r)); }
+            }
+            if (ncclGroupEnd() != ncclSuccess) FAIL(gc, PM_ERR_HIP, "ncclGroupEnd");
+        } else if (n > 1) {
+            for (int d = 0; d < n; ++d) {
+                (void)hipSetDevice(G.subs[d]->device);
+                HIPCHK(gc, hipEventRecord(G.ev[d], G.subs[d]->stream));
+            }
+            for (int d = 0; d < n; ++d) {
+                Ctx *c = G.subs[d];
+                (void)hipSetDevice(c->device);
+                for (int q = 0; q < n; ++q) {
+                    if (q == d) continue;
+                    HIPCHK(gc, hipStreamWaitEvent(c->stream, G.ev[q], 0));
+                    HIPCHK(gc, hipMemcpyPeerAsync((char *)slots[d] + q * chunk_bytes, c->device,
+                                                  (const char *)slots[q] + q * chunk_bytes, G.subs[q]->device,
+                                                  chunk_bytes, c->stream));
+                }
+            }
+        }
+        for (int d = 0; d < n; ++d) {
+            Ctx *c = G.subs[d];
+            (void)hipSetDevice(c->device);
+            if ((rc = pm_build_photon_map(c, p, total_slots, nullptr))) {
+                if (rc == PM_ERR_NO_PHOTONS) FAIL(gc, PM_ERR_NO_PHOTONS, "0 valid photons (photonmappingrenderer.cpp:165-167)");
+                return sub_fail(c, rc);
+            }
+            if (d == 0) t_build += timer_ms(c, "build");
+        }
+        if (p->gather_structure == PM_GATHER_GRID) {
+            uint32_t nv = 0;
+            (void)hipSetDevice(c0->device);
+            HIPCHK(gc, hipMemcpyAsync(&nv, c0->d_cell_start.as<uint32_t>() + c0->grid.ncells, 4, hipMemcpyDeviceToHost, c0->stream));
+            HIPCHK(gc, hipStreamSynchronize(c0->stream));
+            nvalid = nv;
+        } else {
+            nvalid = c0->kd_count;
+        }
+        if (nvalid == 0) FAIL(gc, PM_ERR_NO_PHOTONS, "0 valid photons (photonmappingrenderer.cpp:165-167)");
+        for (int d = 0; d < n; ++d) {
+            Ctx *c = G.subs[d];
+            (void)hipSetDevice(c->device);
+            for (const auto &bc : bands[d]) {
+                if ((rc = pm_gather_range(c, p, bc.first, bc.second, nullptr))) return sub_fail(c, rc);
+                if (d == 0) t_gather += timer_ms(c, "gather");
+            }
+        }
+        /* the next pass overwrites the slot buffers the peers read */
+        for (int d = 0; d < n; ++d) { (void)hipSetDevice(G.subs[d]->device); HIPCHK(gc, hipStreamSynchronize(G.subs[d]->stream)); }
+    }
+    /* final radiance of each device's bands, straight into the host image */
+    const double emitted = (double)P * p->passes;
+    const int64_t nout = c0->pinhole ? (int64_t)c0->W * c0->H : nrec;
+    for (int d = 0; d < n; ++d) {
+        Ctx *c = G.subs[d];
+        (void)hipSetDevice(c->device);
+        if ((rc = materialize_reset(c, c->stream))) return sub_fail(c, rc);
+        HIPCHK(gc, c->d_out.ensure(nout * 3 * sizeof(float)));
+        for (const auto &bc : bands[d]) {
+            FinalParams F{};
+            F.R = recs(c);
+            F.knn = c->rec_estimator == PM_ESTIMATOR_KNN; F.materials = c->S.materials;
+            F.emitted = (float)emitted;
+            F.rec_begin = bc.first; F.rec_count = bc.second; F.raster = c->pinhole; F.W = c->W;
+            F.out = c->pinhole ? c->d_out.as<float>() : c->d_out.as<float>() + 3 * bc.first;
+            HIPCHK(gc, launch_final(F, c->stream));
+            int64_t o0 = bc.first, o1 = bc.first + bc.second; /* output elements of the band */
+            if (c->pinhole) {
+                const int64_t t0 = bc.first / unit, t1 = (bc.first + bc.second + unit - 1) / unit; /* tile rows */
+                o0 = std::min<int64_t>(8 * t0, c->H) * c->W;
+                o1 = std::min<int64_t>(8 * t1, c->H) * c->W;
+            }
+            if (o1 > o0)
+                HIPCHK(gc, hipMemcpyAsync(out_rgb + 3 * o0, c->d_out.as<float>() + 3 * o0, (size_t)(o1 - o0) * 3 * sizeof(float),
+                                          hipMemcpyDeviceToHost, c->stream));
+        }
+    }
+    for (int d = 0; d < n; ++d) { (void)hipSetDevice(G.subs[d]->device); HIPCHK(gc, hipStreamSynchronize(G.subs[d]->stream)); }
+    if (st) {
+        std::memset(st, 0, sizeof(*st));
+        st->paths_emitted = (int64_t)emitted;
+        st->photons_valid = nvalid;
+        std::vector<float4> pos(nrec);
+        (void)hipSetDevice(c0->device);
+        HIPCHK(gc, hipMemcpy(pos.data(), c0->d_pos.p, nrec * sizeof(float4), hipMemcpyDeviceToHost));
+        int64_t act = 0;
+        for (auto &q : pos) act += (fbits_h(q.w) & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) == 0;
+        st->gather_points = act;
+        st->ms_eye = timer_ms(c0, "eye"); st->ms_trace = t_trace; st->ms_build = t_build; st->ms_gather = t_gather;
+    }
+    return PM_OK;
+}
+
 int pm_render(void *ptr, const pm_render_params *p, float *out_rgb, pm_stats *st) {
+    if (group_of(ptr)) return group_render((Ctx *)ptr, p, out_rgb, st);
     GETCTX(ptr);
     int rc;
     if ((rc = check_params(c, p))) return rc;
@@ -1506,6 +1771,10 @@ int pm_simple_pass(void *ptr, const pm_render_params *p, void *d_out, void *stre
 }
 
 int pm_render_simple(void *ptr, const pm_render_params *p, float *out_rgb, pm_stats *st) {
+    if (Group *g_ = group_of(ptr)) { /* direct light only: one device renders it */
+        const int rc_ = pm_render_simple(g_->subs[0], p, out_rgb, st);
+        return rc_ ? group_fail(ptr, g_->subs[0], rc_) : PM_OK;
+    }
     GETCTX(ptr);
     if (!out_rgb) FAIL(c, PM_ERR_INVALID, "null output");
     const int64_t nout = c->pinhole ? (int64_t)c->W * c->H : c->nrays;
@@ -1525,6 +1794,7 @@ int pm_render_simple(void *ptr, const pm_render_params *p, float *out_rgb, pm_st
 
 /* ------------------------------------------------------- buffers / tests */
 int64_t pm_num_records(void *ptr) {
+    if (Group *g_ = group_of(ptr)) return pm_num_records(g_->subs[0]);
     Ctx *c = (Ctx *)ptr;
     return c ? num_records(c) : -1;
 }
@@ -1665,6 +1935,7 @@ int pm_map_info(void *ptr, int64_t out[4]) {
 }
 
 int pm_scene_info(void *ptr, int64_t out[7]) {
+    if (Group *g_ = group_of(ptr)) return pm_scene_info(g_->subs[0], out);
     GETCTX(ptr);
     if (!c->S.blob) FAIL(c, PM_ERR_INVALID, "no scene committed");
     const SceneDev &S = c->S;
@@ -1739,6 +2010,7 @@ int pm_set_stage_timing(void *ptr, const char *stages) {
 }
 
 int pm_synchronize(void *ptr) {
+    GROUP_FWD(ptr, pm_synchronize(sub));
     GETCTX(ptr);
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return PM_OK;

@@ -252,6 +252,35 @@ void collapse_bvh4(const BvhOut &bin, int leaf_prims, Bvh4Out &out) {
     out.max_stack = need + 1;
 }
 
+void bvh4_bfs_order(std::vector<float> &nodes) {
+    const size_t nn = nodes.size() / 32;
+    if (nn == 0) return;
+    std::vector<int> order, newid(nn, -1);
+    order.reserve(nn);
+    order.push_back(0);
+    newid[0] = 0;
+    for (size_t h = 0; h < order.size(); ++h) {
+        const float *n = &nodes[(size_t)order[h] * 32];
+        int codes[4], counts[4];
+        std::memcpy(codes, &n[24], sizeof(codes));
+        std::memcpy(counts, &n[28], sizeof(counts));
+        for (int k = 0; k < 4; ++k)
+            if (counts[k] == 0 && newid[codes[k]] < 0) { newid[codes[k]] = (int)order.size(); order.push_back(codes[k]); }
+    }
+    std::vector<float> out(order.size() * 32);
+    for (size_t i = 0; i < order.size(); ++i) {
+        float *n = &out[i * 32];
+        std::memcpy(n, &nodes[(size_t)order[i] * 32], 32 * sizeof(float));
+        int codes[4], counts[4];
+        std::memcpy(codes, &n[24], sizeof(codes));
+        std::memcpy(counts, &n[28], sizeof(counts));
+        for (int k = 0; k < 4; ++k)
+            if (counts[k] == 0) codes[k] = newid[codes[k]];
+        std::memcpy(&n[24], codes, sizeof(codes));
+    }
+    nodes.swap(out);
+}
+
 /* the device's decode of a quantized bound (traverse4 / trav_step) */
 static float qdecode(float o, uint32_t q, int e) { return o + (float)q * std::ldexp(1.0f, e); }
 

@@ -72,6 +72,9 @@ bool quantize_bvh4(const std::vector<float> &nodes, std::vector<uint32_t> &q);
  * tri_geo[s0 ..] directly, without loading the refs (one dependent load
  * less per leaf). */
 constexpr int LEAF_TRIS = 0x4000;
+/* renumbers collapse_bvh4's nodes (depth-first) breadth-first, root 0: the
+ * top levels become the first nodes (the LDS nodelets of k_trace_pool) */
+void bvh4_bfs_order(std::vector<float> &nodes);
 bool quantize_bvh4(const std::vector<float> &nodes, const std::vector<uint32_t> &refs, std::vector<uint32_t> &q);
 
 /* returns the number of nodes (= valid photons); nodes sized >= that */

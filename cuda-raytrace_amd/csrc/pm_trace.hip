@@ -674,6 +674,14 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
     TravState tr;
     Held held;
     if (HOLD) held.col = reinterpret_cast<uint32_t *>(stk + P.S.stack_depth * TRACE_BLOCK) + tid; /* after the stacks */
+    /* nodelets after the stacks (and the held deposits): the BVH's top levels */
+    const int n_lds = PM_BVH4_QUANT ? S.nodelets : 0;
+    uint4 *lnodes = reinterpret_cast<uint4 *>(stk + P.S.stack_depth * TRACE_BLOCK + (HOLD ? HOLD_WORDS * TRACE_BLOCK : 0));
+    if (n_lds > 0) {
+        const uint4 *g = reinterpret_cast<const uint4 *>(S.wnodes);
+        for (int i = tid; i < 4 * n_lds; i += TRACE_BLOCK) lnodes[i] = g[i];
+        __syncthreads();
+    }
     int phase = PHASE_DEAD;
     while (true) {
         const unsigned long long travm = __ballot(phase == PHASE_TRAV);
@@ -713,7 +721,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
         }
 #pragma unroll 1
         for (int k = 0; k < POOL_STEPS; ++k)
-            if (phase == PHASE_TRAV && !trav_step(S, st.ray, tr, stack, TRACE_BLOCK, cen)) phase = PHASE_SHADE;
+            if (phase == PHASE_TRAV && !trav_step(S, st.ray, tr, stack, TRACE_BLOCK, cen, lnodes, n_lds)) phase = PHASE_SHADE;
     }
     if (COUNT) {
         uint32_t nodes = 0, prims = 0;
@@ -739,7 +747,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
     }
 
 /* resident waves of the pooled kernel per CU at this LDS size (0 if unknown) */
-int trace_pool_waves_per_cu(size_t lds, int hold) {
+int trace_pool_waves_per_cu(size_t lds, int hold) { /* lds: stacks (+ nodelets) */
     int blocks = 0;
     if (hold) lds += (size_t)HOLD_WORDS * TRACE_BLOCK * 4;
     const hipError_t e = hold ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0, 1>, TRACE_BLOCK, lds)
@@ -805,11 +813,12 @@ hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s) {
         const int64_t waves = (p.path_count + q.wave_paths - 1) / q.wave_paths;
         const unsigned grid = (unsigned)((waves + TRACE_BLOCK / 64 - 1) / (TRACE_BLOCK / 64));
         const bool hold = trace_hold(p);
-        const size_t lds_h = lds + (hold ? (size_t)HOLD_WORDS * TRACE_BLOCK * 4 : 0);
+        const size_t lnl = (size_t)(PM_BVH4_QUANT ? p.S.nodelets : 0) * 64; /* nodelet bytes */
+        const size_t lds_h = lds + (hold ? (size_t)HOLD_WORDS * TRACE_BLOCK * 4 : 0) + lnl;
         if (count && hold) pm_launch((k_trace_pool<1, 1>), dim3(grid), dim3(TRACE_BLOCK), lds_h, s, q);
-        else if (count) pm_launch((k_trace_pool<1, 0>), dim3(grid), dim3(TRACE_BLOCK), lds, s, q);
+        else if (count) pm_launch((k_trace_pool<1, 0>), dim3(grid), dim3(TRACE_BLOCK), lds + lnl, s, q);
         else if (hold) pm_launch((k_trace_pool<0, 1>), dim3(grid), dim3(TRACE_BLOCK), lds_h, s, q);
-        else pm_launch((k_trace_pool<0, 0>), dim3(grid), dim3(TRACE_BLOCK), lds, s, q);
+        else pm_launch((k_trace_pool<0, 0>), dim3(grid), dim3(TRACE_BLOCK), lds + lnl, s, q);
         return hipGetLastError();
     }
     if (p.per_block == 0) {

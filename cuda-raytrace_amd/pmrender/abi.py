@@ -30,6 +30,16 @@ RECORD_DTYPE = np.dtype([
 assert RECORD_DTYPE.itemsize == 64
 
 
+class PMConfig(ctypes.Structure):
+    """include/pm_api.h pm_config (32 B)."""
+    _fields_ = [
+        ("device", ctypes.c_int),
+        ("n_devices", ctypes.c_int),
+        ("devices", ctypes.POINTER(ctypes.c_int)),
+        ("reserved", ctypes.c_int * 4),
+    ]
+
+
 class RenderParams(ctypes.Structure):
     """pm_render_params; defaults are the reference's hard-coded constants."""
     _fields_ = [

@@ -9,7 +9,7 @@ import os
 
 import numpy as np
 
-from .abi import (PHOTON_DTYPE, RECORD_DTYPE, PM_ERR_NO_PHOTONS, RenderParams, Stats, f32, fptr, iptr,
+from .abi import (PHOTON_DTYPE, RECORD_DTYPE, PM_ERR_NO_PHOTONS, PMConfig, RenderParams, Stats, f32, fptr, iptr,
                   record_pixels)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -125,15 +125,23 @@ def kdtree_build_host(slots):
 class Context:
     """One renderer context on one HIP device (cudarender.cpp's gContext)."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, devices=None):
+        """devices: a list of device ordinals -> one multi-device context
+        (pm_config::n_devices: scene calls, render() and render_simple()
+        only; photon shards + RCCL all-gather + 8-row bands per device)."""
         self.lib = load_library()
         h = ctypes.c_void_p()
-        cfg = (ctypes.c_int * 8)(device, 0, 0, 0, 0, 0, 0, 0)
-        rc = self.lib.pm_create(ctypes.byref(h), ctypes.cast(cfg, ctypes.c_void_p))
+        cfg = PMConfig(device=device)
+        if devices is not None:
+            self._devlist = (ctypes.c_int * len(devices))(*devices)
+            cfg.n_devices = len(devices)
+            cfg.devices = ctypes.cast(self._devlist, ctypes.POINTER(ctypes.c_int))
+        rc = self.lib.pm_create(ctypes.byref(h), ctypes.byref(cfg))
         if rc != 0:
             raise PMError(rc, self.lib.pm_last_error(None).decode())
         self.h = h
         self.device = device
+        self.devices = list(devices) if devices is not None else [device]
         self.width = self.height = 0
         self.pinhole = False
 

@@ -107,8 +107,16 @@ typedef struct pm_record {
 } pm_record;
 
 typedef struct pm_config {
-    int device;          /* HIP device ordinal */
-    int reserved[7];
+    int device;          /* HIP device ordinal (n_devices == 0) */
+    /* n_devices > 0: one context over devices[0 .. n_devices) of this node
+     * (photon paths sharded by global id, RCCL all-gather of
+     * the slots, interleaved 8-row bands per device). It takes the scene
+     * calls, pm_render and pm_render_simple; the stage API needs one context
+     * per device (one process per GPU, pmrender/dist.py). The reference is
+     * single-context (cudarender.cpp:14), so this is new surface. */
+    int n_devices;
+    const int *devices;
+    int reserved[4];
 } pm_config;
 
 /* Render parameters. Defaults (pm_default_params) are the reference's

@@ -57,12 +57,17 @@ def test_pod_layouts(tmp_path):
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "pm_api.h"\nint main(void){printf("%zu %zu %zu %zu %zu %zu",'
                    'sizeof(pm_photon), sizeof(pm_record), sizeof(pm_render_params), sizeof(pm_stats),'
-                   'offsetof(pm_render_params, paths_per_pass), offsetof(pm_render_params, gather_structure));return 0;}\n')
+                   'offsetof(pm_render_params, paths_per_pass), offsetof(pm_render_params, gather_structure));'
+                   'printf(" %zu %zu %zu", sizeof(pm_config), offsetof(pm_config, n_devices), offsetof(pm_config, devices));'
+                   'return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    from pmrender.abi import PMConfig
     assert got == [PHOTON_DTYPE.itemsize, RECORD_DTYPE.itemsize, ctypes.sizeof(RenderParams), ctypes.sizeof(Stats),
-                   RenderParams.paths_per_pass.offset, RenderParams.gather_structure.offset]
+                   RenderParams.paths_per_pass.offset, RenderParams.gather_structure.offset,
+                   ctypes.sizeof(PMConfig), PMConfig.n_devices.offset, PMConfig.devices.offset]
+    assert ctypes.sizeof(PMConfig) == 32         # the round-2 pm_config size (int device + 7 reserved ints)
     assert PHOTON_DTYPE.itemsize == 40           # CudaPhoton, photonmapping.h:32-41
 
 
