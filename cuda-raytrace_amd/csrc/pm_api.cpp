@@ -9,10 +9,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <random>
 #include <string>
 #include <vector>
@@ -126,6 +128,8 @@ struct Ctx {
     int kd_stack = KD_STACK;        /* kd gather stack entries (env PM_KD_STACK, tests only) */
     bool trace_pool = true;         /* pooled trace kernel for 4-wide BVH scenes (env PM_TRACE_POOL=0 disables) */
     bool trace_hold = true;         /* deposits written once per path (env PM_TRACE_HOLD=0: per deposit) */
+    bool path_sort = false;         /* pooled kernel: paths by first-ray direction (env PM_PATH_SORT=1) */
+    DevBuf d_porder, d_pscratch;
     int64_t pool_waves = 0;         /* pooled kernel: waves per launch (env PM_POOL_WAVES; 0 = one occupancy round) */
     int gather_kernel = PM_GK_TILE; /* bucket gather kernel (env PM_GATHER_KERNEL=tile|lane|wave) */
     bool gather_xcd = false;        /* tile gather: contiguous tile ranges per XCD (env PM_GATHER_XCD=1) */
@@ -566,6 +570,7 @@ int pm_create(void **out, const pm_config *cfg) {
     if (const char *e = getenv("PM_REC_ORDER")) c->rec_order_mode = atoi(e);
     if (const char *e = getenv("PM_TRACE_POOL")) c->trace_pool = atoi(e) != 0;
     if (const char *e = getenv("PM_TRACE_HOLD")) c->trace_hold = atoi(e) != 0;
+    if (const char *e = getenv("PM_PATH_SORT")) c->path_sort = atoi(e) != 0;
     if (const char *e = getenv("PM_POOL_WAVES")) c->pool_waves = std::max(1LL, atoll(e));
     if (const char *e = getenv("PM_TILE_LIST")) c->tile_list = atoi(e) != 0;
     if (const char *e = getenv("PM_KD_STACK")) c->kd_stack = std::max(1, std::min(KD_STACK, atoi(e)));
@@ -607,7 +612,8 @@ void pm_destroy(void *ptr) {
                       &c->d_dl, &c->d_slots, &c->d_count, &c->d_scratch, &c->d_vflags, &c->d_vrank, &c->d_vlist, &c->d_vsums,
                       &c->d_cell_start, &c->d_pha, &c->d_phb,
                       &c->d_kd, &c->d_out, &c->d_counters, &c->d_tiles, &c->d_tile_flags, &c->d_tile_count,
-                      &c->d_r2hist, &c->d_order, &c->d_ocount, &c->d_ostart, &c->d_oscratch, &c->d_ostats};
+                      &c->d_r2hist, &c->d_order, &c->d_ocount, &c->d_ostart, &c->d_oscratch, &c->d_ostats,
+                      &c->d_porder, &c->d_pscratch};
     for (DevBuf *b : bufs) b->release();
     if (c->tile_event) (void)hipEventDestroy(c->tile_event);
     if (c->r2_event) (void)hipEventDestroy(c->r2_event);
@@ -778,28 +784,40 @@ int pm_commit(void *ptr) {
     for (int64_t i = 0; i < nd; ++i) c->disks[5 * i + 4].w = ibits((int)(nt + i));
     for (int64_t i = 0; i < ns; ++i) c->spheres[4 * i + 3].w = ibits((int)(nt + nd + i));
 
-    std::vector<BuildPrim> prims;
-    prims.reserve(nt + nd + ns);
+    const auto t_commit0 = std::chrono::steady_clock::now();
+    std::vector<BuildPrim> prims(nt);
     float blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    auto add_box = [&](float lo[3], float hi[3], uint32_t ref) {
+    auto make_box = [](const float lo[3], const float hi[3], uint32_t ref) {
         BuildPrim bp;
         for (int a = 0; a < 3; ++a) {
-            blo[a] = std::min(blo[a], lo[a]); bhi[a] = std::max(bhi[a], hi[a]);
             float pad = 1e-4f * std::max(1.0f, std::max(fabsf(lo[a]), fabsf(hi[a])));
             bp.lo[a] = lo[a] - pad; bp.hi[a] = hi[a] + pad;
         }
         bp.ref = ref;
-        prims.push_back(bp);
+        return bp;
+    };
+    auto add_box = [&](float lo[3], float hi[3], uint32_t ref) {
+        for (int a = 0; a < 3; ++a) { blo[a] = std::min(blo[a], lo[a]); bhi[a] = std::max(bhi[a], hi[a]); }
+        prims.push_back(make_box(lo, hi, ref));
     };
     const float *V = c->P.data();
-    for (int64_t t = 0; t < nt; ++t) {
-        const HTri &tr = c->tris[t];
-        float lo[3], hi[3];
-        for (int a = 0; a < 3; ++a) {
-            float v0 = V[3 * tr.v[0] + a], v1 = V[3 * tr.v[1] + a], v2 = V[3 * tr.v[2] + a];
-            lo[a] = std::min(v0, std::min(v1, v2)); hi[a] = std::max(v0, std::max(v1, v2));
-        }
-        add_box(lo, hi, (PRIM_TRI << 30) | (uint32_t)t);
+    { /* triangle boxes in parallel chunks; the scene box merged per chunk */
+        std::mutex mu;
+        parallel_for(nt, [&](int64_t t0, int64_t t1) {
+            float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (int64_t t = t0; t < t1; ++t) {
+                const HTri &tr = c->tris[t];
+                float lo[3], hi[3];
+                for (int a = 0; a < 3; ++a) {
+                    float v0 = V[3 * tr.v[0] + a], v1 = V[3 * tr.v[1] + a], v2 = V[3 * tr.v[2] + a];
+                    lo[a] = std::min(v0, std::min(v1, v2)); hi[a] = std::max(v0, std::max(v1, v2));
+                    clo[a] = std::min(clo[a], lo[a]); chi[a] = std::max(chi[a], hi[a]);
+                }
+                prims[t] = make_box(lo, hi, (PRIM_TRI << 30) | (uint32_t)t);
+            }
+            std::lock_guard<std::mutex> g(mu);
+            for (int a = 0; a < 3; ++a) { blo[a] = std::min(blo[a], clo[a]); bhi[a] = std::max(bhi[a], chi[a]); }
+        });
     }
     for (int64_t i = 0; i < nd; ++i) {
         const float4 *d = &c->disks[5 * i];
@@ -828,7 +846,16 @@ int pm_commit(void *ptr) {
     BvhCost cost;
     if (const char *e = getenv("PM_BVH_LEAF_MAX")) cost.leaf_max = std::max(1, atoi(e));
     if (const char *e = getenv("PM_BVH_CTRAV")) cost.c_trav = (float)atof(e);
+    /* env PM_COMMIT_TIMES=1: the host build's phases on stderr (setup-time study) */
+    const bool ptimes = getenv("PM_COMMIT_TIMES") != nullptr;
+    auto tnow = [] { return std::chrono::steady_clock::now(); };
+    auto tms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const auto t_build0 = tnow();
     build_bvh(prims, BVH_STACK - 2, bvh, cost);
+    if (ptimes) fprintf(stderr, "pm_commit: %zu prims (boxes %.1f ms), SAH build %.1f ms\n", prims.size(),
+                        tms(t_commit0, t_build0), tms(t_build0, tnow()));
     c->bvh_depth = bvh.depth;
     if (bvh.depth >= BVH_STACK) FAIL(c, PM_ERR_INVALID, "BVH too deep (%d)", bvh.depth);
 
@@ -848,32 +875,40 @@ int pm_commit(void *ptr) {
     }
     std::vector<uint32_t> slot_of(nt);
     for (size_t k = 0; k < tri_order.size(); ++k) slot_of[tri_order[k]] = (uint32_t)k;
-    for (uint32_t &ref : bvh.refs)
-        if ((ref >> 30) == PRIM_TRI) ref = (PRIM_TRI << 30) | slot_of[ref & 0x3fffffffu];
+    parallel_for((int64_t)bvh.refs.size(), [&](int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i) {
+            uint32_t &ref = bvh.refs[i];
+            if ((ref >> 30) == PRIM_TRI) ref = (PRIM_TRI << 30) | slot_of[ref & 0x3fffffffu];
+        }
+    });
 
     /* per-triangle precomputed (p0, e0, e1, n) for the intersector and the
-     * normalized shading frame for hits */
-    std::vector<float4> tri_geo, tri_shade;
-    std::vector<int4> tri_info;
-    std::vector<uint32_t> tri_id;
-    tri_geo.reserve(3 * nt); tri_shade.reserve(2 * nt); tri_info.reserve(nt); tri_id.reserve(nt);
-    for (uint32_t t : tri_order) {
-        const HTri &tr = c->tris[t];
-        const HMesh &m = c->meshes[tr.mesh];
-        const float *p0 = V + 3 * tr.v[0], *p1 = V + 3 * tr.v[1], *p2 = V + 3 * tr.v[2];
-        float e0[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
-        float e1[3] = {p0[0] - p2[0], p0[1] - p2[1], p0[2] - p2[2]};
-        float n[3] = {e1[1] * e0[2] - e1[2] * e0[1], e1[2] * e0[0] - e1[0] * e0[2], e1[0] * e0[1] - e1[1] * e0[0]};
-        tri_geo.push_back(f4(p0[0], p0[1], p0[2], e0[0]));
-        tri_geo.push_back(f4(e0[1], e0[2], e1[0], e1[1]));
-        tri_geo.push_back(f4(e1[2], n[0], n[1], n[2]));
-        float ns[3], dpdu[3];
-        tri_frame(p0, p1, p2, m.has_uv ? &c->UV[0] : nullptr, tr.v, n, ns, dpdu);
-        tri_shade.push_back(f4(ns[0], ns[1], ns[2], bits_f((uint32_t)m.material | (m.has_n ? 0x80000000u : 0u))));
-        tri_shade.push_back(f4(dpdu[0], dpdu[1], dpdu[2], bits_f((uint32_t)m.light)));
-        tri_info.push_back(make_int4(tr.v[0], tr.v[1], tr.v[2], tr.mesh));
-        tri_id.push_back(t);
-    }
+     * normalized shading frame for hits (in parallel chunks of storage slots) */
+    const int64_t nst = (int64_t)tri_order.size();
+    std::vector<float4> tri_geo(3 * nst), tri_shade(2 * nst);
+    std::vector<int4> tri_info(nst);
+    std::vector<uint32_t> tri_id(nst);
+    parallel_for(nst, [&](int64_t k0, int64_t k1) {
+        for (int64_t k = k0; k < k1; ++k) {
+            const uint32_t t = tri_order[k];
+            const HTri &tr = c->tris[t];
+            const HMesh &m = c->meshes[tr.mesh];
+            const float *p0 = V + 3 * tr.v[0], *p1 = V + 3 * tr.v[1], *p2 = V + 3 * tr.v[2];
+            float e0[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
+            float e1[3] = {p0[0] - p2[0], p0[1] - p2[1], p0[2] - p2[2]};
+            float n[3] = {e1[1] * e0[2] - e1[2] * e0[1], e1[2] * e0[0] - e1[0] * e0[2], e1[0] * e0[1] - e1[1] * e0[0]};
+            tri_geo[3 * k + 0] = f4(p0[0], p0[1], p0[2], e0[0]);
+            tri_geo[3 * k + 1] = f4(e0[1], e0[2], e1[0], e1[1]);
+            tri_geo[3 * k + 2] = f4(e1[2], n[0], n[1], n[2]);
+            float ns[3], dpdu[3];
+            tri_frame(p0, p1, p2, m.has_uv ? &c->UV[0] : nullptr, tr.v, n, ns, dpdu);
+            tri_shade[2 * k + 0] = f4(ns[0], ns[1], ns[2], bits_f((uint32_t)m.material | (m.has_n ? 0x80000000u : 0u)));
+            tri_shade[2 * k + 1] = f4(dpdu[0], dpdu[1], dpdu[2], bits_f((uint32_t)m.light));
+            tri_info[k] = make_int4(tr.v[0], tr.v[1], tr.v[2], tr.mesh);
+            tri_id[k] = t;
+        }
+    });
+    if (ptimes) fprintf(stderr, "pm_commit: triangle records done at %.1f ms\n", tms(t_commit0, tnow()));
     std::vector<float4> norms(c->N.size() / 3);
     for (size_t i = 0; i < norms.size(); ++i) norms[i] = f4(c->N[3 * i], c->N[3 * i + 1], c->N[3 * i + 2], 0.f);
     std::vector<float4> nodes4(bvh.nodes.size() / 4);
@@ -882,6 +917,11 @@ int pm_commit(void *ptr) {
     /* one blob of 16-B aligned sections: the same offsets address it in HBM
      * and, for scenes that fit (SceneDev::lds_bytes), in each block's LDS copy */
     std::vector<unsigned char> blob;
+    /* one reservation for every section (no regrowth copies of a 250 MB blob) */
+    blob.reserve(16 * 16 + nodes4.size() * sizeof(float4) + bvh.refs.size() * 4 + tri_geo.size() * sizeof(float4) +
+                 tri_shade.size() * sizeof(float4) + tri_id.size() * 4 + tri_info.size() * sizeof(int4) +
+                 norms.size() * sizeof(float4) + (c->disks.size() + c->spheres.size() + c->materials.size()) * sizeof(float4) +
+                 c->lights.size() * sizeof(LightDev) + (size_t)(bvh.nodes.size() / 16 + 1) * 64 * 2);
     auto put = [&](const void *src, size_t n) -> size_t {
         size_t off = (blob.size() + 15) & ~(size_t)15;
         blob.resize(off + n, 0);
@@ -909,7 +949,9 @@ int pm_commit(void *ptr) {
         if (!we || atoi(we) != 0) {
             const char *le = getenv("PM_BVH4_LEAF");
             Bvh4Out w;
+            const auto t_c0 = tnow();
             collapse_bvh4(bvh, le ? atoi(le) : 1, w);
+            if (ptimes) fprintf(stderr, "pm_commit: collapse %.1f ms\n", tms(t_c0, tnow()));
             /* node format fixed at build time (pm_device.h PM_BVH4_QUANT) */
             std::vector<uint32_t> qn;
             const bool quant = PM_BVH4_QUANT != 0;
@@ -923,7 +965,9 @@ int pm_commit(void *ptr) {
             const char *nl = getenv("PM_NODELETS"), *bf = getenv("PM_BVH4_BFS");
             nodelets = nl ? std::max(0, atoi(nl)) : 0;
             if (nodelets > 0 || (bf && atoi(bf) != 0)) bvh4_bfs_order(w.nodes);
+            const auto t_q0 = tnow();
             const bool coded = !quant || quantize_bvh4(w.nodes, lt && atoi(lt) == 0 ? std::vector<uint32_t>() : bvh.refs, qn);
+            if (ptimes) fprintf(stderr, "pm_commit: quantize %.1f ms\n", tms(t_q0, tnow()));
             if (coded && w.max_stack <= BVH_STACK) {
                 o_wnodes = quant ? put(qn.data(), qn.size() * sizeof(uint32_t))
                                  : put(w.nodes.data(), w.nodes.size() * sizeof(float));
@@ -936,7 +980,10 @@ int pm_commit(void *ptr) {
     }
     blob.resize(std::max<size_t>((blob.size() + 15) & ~(size_t)15, 16), 0);
     int rc;
+    const auto t_u0 = tnow();
     if ((rc = upload(c, c->d_scene, blob))) return rc;
+    if (ptimes) fprintf(stderr, "pm_commit: upload %.1f ms (%zu bytes), total %.1f ms\n", tms(t_u0, tnow()), blob.size(),
+                        tms(t_commit0, tnow()));
 
     SceneDev &S = c->S;
     const char *base = c->d_scene.as<char>();
@@ -1196,6 +1243,12 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
         T.count = c->d_count.as<uint32_t>();
         T.key = c->d_scratch.as<uint32_t>();
         T.rank = c->d_scratch.as<uint32_t>() + end_slot;
+    }
+    if (c->path_sort && T.pool_paths > 0 && c->S.wide) {
+        HIPCHK(c, c->d_porder.ensure((size_t)path_count * 4));
+        HIPCHK(c, c->d_pscratch.ensure(path_order_scratch_words(path_count) * 4));
+        HIPCHK(c, launch_path_order(T, c->d_pscratch.as<uint32_t>(), c->d_porder.as<uint32_t>(), s));
+        T.order = c->d_porder.as<uint32_t>();
     }
     timer_begin(c, "trace", s);
     /* the kernel writes all path_count * mpc slots: deposits, then zeros */

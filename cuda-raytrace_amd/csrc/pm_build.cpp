@@ -4,8 +4,12 @@
 #include "pm_build.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <thread>
 
 namespace pm {
 
@@ -28,12 +32,41 @@ struct Box {
 
 inline float centroid(const BuildPrim &p, int a) { return 0.5f * (p.lo[a] + p.hi[a]); }
 
+/* host threads for the builders: this process's CPU share (OMP_NUM_THREADS,
+ * 16 per GPU on the MI355X boxes), else the hardware's, at most 32 */
+int build_threads() {
+    static const int t = [] {
+        const char *e = std::getenv("PM_BUILD_THREADS");
+        if (!e) e = std::getenv("OMP_NUM_THREADS");
+        int n = e ? std::atoi(e) : (int)std::thread::hardware_concurrency();
+        return std::max(1, std::min(32, n));
+    }();
+    return t;
+}
+/* f(chunk, begin, end) over [b, e) in `parts` contiguous chunks, in parallel */
+void parallel_chunks(int b, int e, int parts, const std::function<void(int, int, int)> &f) {
+    if (parts <= 1) { f(0, b, e); return; }
+    std::vector<std::thread> th;
+    const int n = e - b;
+    for (int k = 0; k < parts; ++k) {
+        const int cb = b + (int)((int64_t)n * k / parts), ce = b + (int)((int64_t)n * (k + 1) / parts);
+        th.emplace_back(f, k, cb, ce);
+    }
+    for (auto &t : th) t.join();
+}
+/* ranges this large bin in parallel (the top levels, where few subtrees
+ * run at once); the merge of per-chunk bins is exact (counts, min / max) */
+constexpr int PAR_BIN_MIN = 1 << 16;
+/* ranges this large build their left subtree in another thread */
+constexpr int SUBTREE_TASK_MIN = 1 << 14;
+
 struct BvhBuilder {
     std::vector<BuildPrim> &P;
     std::vector<float> &nodes;
     int max_depth;
     BvhCost cost;
     int depth_seen = 0;
+    int threads = 1; /* binning threads for large ranges */
 
     int alloc() {
         int id = (int)(nodes.size() / 16);
@@ -53,39 +86,78 @@ struct BvhBuilder {
     /* binned SAH; returns split position or -1 for "make a leaf" */
     int find_split(int b, int e) {
         int n = e - b;
-        Box cb;
-        for (int i = b; i < e; ++i) {
-            float c[3] = {centroid(P[i], 0), centroid(P[i], 1), centroid(P[i], 2)};
-            cb.grow(c, c);
+        const int parts = n >= PAR_BIN_MIN ? std::min(threads, n / (PAR_BIN_MIN / 4)) : 1;
+        Box cb, full;
+        if (parts == 1) {
+            for (int i = b; i < e; ++i) {
+                float c[3] = {centroid(P[i], 0), centroid(P[i], 1), centroid(P[i], 2)};
+                cb.grow(c, c);
+                full.grow(P[i].lo, P[i].hi);
+            }
+        } else {
+            std::vector<Box> pc(parts), pf(parts);
+            parallel_chunks(b, e, parts, [&](int k, int cb0, int ce0) {
+                for (int i = cb0; i < ce0; ++i) {
+                    float c[3] = {centroid(P[i], 0), centroid(P[i], 1), centroid(P[i], 2)};
+                    pc[k].grow(c, c);
+                    pf[k].grow(P[i].lo, P[i].hi);
+                }
+            });
+            for (int k = 0; k < parts; ++k) { cb.grow(pc[k]); full.grow(pf[k]); }
         }
-        Box full;
-        for (int i = b; i < e; ++i) full.grow(P[i].lo, P[i].hi);
         float best_cost = INFINITY;
         int best_axis = -1, best_bin = -1;
+        /* the three axes' bins in one pass over the range */
+        Box bins[3][NBINS];
+        int cnt[3][NBINS] = {{0}};
+        float k3[3];
+        for (int a = 0; a < 3; ++a) { const float ext = cb.hi[a] - cb.lo[a]; k3[a] = ext > 0.f ? NBINS / ext : 0.f; }
+        if (parts == 1) {
+            for (int a = 0; a < 3; ++a) {
+                if (!(k3[a] > 0.f)) continue;
+                for (int i = b; i < e; ++i) {
+                    int bi = (int)((centroid(P[i], a) - cb.lo[a]) * k3[a]);
+                    bi = std::min(NBINS - 1, std::max(0, bi));
+                    cnt[a][bi]++;
+                    bins[a][bi].grow(P[i].lo, P[i].hi);
+                }
+            }
+        } else {
+            struct Part { Box bins[3][NBINS]; int cnt[3][NBINS]; };
+            std::vector<Part> pp(parts);
+            parallel_chunks(b, e, parts, [&](int k, int cb0, int ce0) {
+                Part &q = pp[k];
+                std::memset(q.cnt, 0, sizeof(q.cnt));
+                for (int a = 0; a < 3; ++a)
+                    for (int i2 = 0; i2 < NBINS; ++i2) q.bins[a][i2] = Box();
+                for (int i = cb0; i < ce0; ++i)
+                    for (int a = 0; a < 3; ++a) {
+                        if (!(k3[a] > 0.f)) continue;
+                        int bi = (int)((centroid(P[i], a) - cb.lo[a]) * k3[a]);
+                        bi = std::min(NBINS - 1, std::max(0, bi));
+                        q.cnt[a][bi]++;
+                        q.bins[a][bi].grow(P[i].lo, P[i].hi);
+                    }
+            });
+            for (int k = 0; k < parts; ++k)
+                for (int a = 0; a < 3; ++a)
+                    for (int i2 = 0; i2 < NBINS; ++i2) { cnt[a][i2] += pp[k].cnt[a][i2]; bins[a][i2].grow(pp[k].bins[a][i2]); }
+        }
         for (int a = 0; a < 3; ++a) {
             float ext = cb.hi[a] - cb.lo[a];
             if (!(ext > 0.f)) continue;
-            Box bins[NBINS];
-            int cnt[NBINS] = {0};
-            float k = NBINS / ext;
-            for (int i = b; i < e; ++i) {
-                int bi = (int)((centroid(P[i], a) - cb.lo[a]) * k);
-                bi = std::min(NBINS - 1, std::max(0, bi));
-                cnt[bi]++;
-                bins[bi].grow(P[i].lo, P[i].hi);
-            }
             float rarea[NBINS];
             int rcnt[NBINS];
             Box acc;
             int c = 0;
             for (int i = NBINS - 1; i > 0; --i) {
-                acc.grow(bins[i]); c += cnt[i];
+                acc.grow(bins[a][i]); c += cnt[a][i];
                 rarea[i] = acc.half_area(); rcnt[i] = c;
             }
             Box lacc;
             int lc = 0;
             for (int i = 0; i < NBINS - 1; ++i) {
-                lacc.grow(bins[i]); lc += cnt[i];
+                lacc.grow(bins[a][i]); lc += cnt[a][i];
                 if (lc == 0 || rcnt[i + 1] == 0) continue;
                 float cost = lacc.half_area() * lc + rarea[i + 1] * rcnt[i + 1];
                 if (cost < best_cost) { best_cost = cost; best_axis = a; best_bin = i; }
@@ -116,9 +188,23 @@ struct BvhBuilder {
         return m;
     }
 
+    Box range_box(int b, int e) const {
+        const int parts = e - b >= PAR_BIN_MIN ? std::min(threads, (e - b) / (PAR_BIN_MIN / 4)) : 1;
+        if (parts == 1) {
+            Box box;
+            for (int i = b; i < e; ++i) box.grow(P[i].lo, P[i].hi);
+            return box;
+        }
+        std::vector<Box> pb(parts);
+        parallel_chunks(b, e, parts, [&](int k, int cb0, int ce0) {
+            for (int i = cb0; i < ce0; ++i) pb[k].grow(P[i].lo, P[i].hi);
+        });
+        Box box;
+        for (auto &x : pb) box.grow(x);
+        return box;
+    }
     void child(int b, int e, int depth, int &code, int &count, Box &box) {
-        box = Box();
-        for (int i = b; i < e; ++i) box.grow(P[i].lo, P[i].hi);
+        box = range_box(b, e);
         int split = -1;
         if (e - b > 1 && depth < max_depth) split = find_split(b, e);
         if (split < 0) { code = ~b; count = e - b; return; }
@@ -126,11 +212,44 @@ struct BvhBuilder {
         depth_seen = std::max(depth_seen, depth + 1);
         Box lb, rb;
         int lc, lcnt, rc, rcnt;
-        child(b, split, depth + 1, lc, lcnt, lb);
-        child(split, e, depth + 1, rc, rcnt, rb);
+        if (threads > 1 && e - b >= SUBTREE_TASK_MIN) {
+            /* the left subtree in its own builder and thread, numbered as the
+             * serial recursion numbers it: its nodes follow this node, the
+             * right subtree's follow them (identical tree and ids) */
+            std::vector<float> lnodes;
+            BvhBuilder L{P, lnodes, max_depth, cost, 0, std::max(1, threads / 2)};
+            std::thread t([&] { L.child(b, split, depth + 1, lc, lcnt, lb); });
+            BvhBuilder R{P, rnodes_scratch(), max_depth, cost, 0, std::max(1, threads - threads / 2)};
+            R.child(split, e, depth + 1, rc, rcnt, rb);
+            t.join();
+            const int lbase = (int)(nodes.size() / 16), nl = (int)(lnodes.size() / 16);
+            append(lnodes, lbase);
+            append(R.nodes, lbase + nl);
+            if (lcnt == 0) lc += lbase;
+            if (rcnt == 0) rc += lbase + nl;
+            depth_seen = std::max({depth_seen, L.depth_seen, R.depth_seen});
+            R.nodes.clear();
+        } else {
+            child(b, split, depth + 1, lc, lcnt, lb);
+            child(split, e, depth + 1, rc, rcnt, rb);
+        }
         write_node(id, lb, lc, lcnt, rb, rc, rcnt);
         code = id; count = 0;
     }
+    /* a subtree's nodes (ids from 0) appended at id base: internal child ids shift */
+    void append(const std::vector<float> &sub, int base) {
+        const size_t off = nodes.size();
+        nodes.insert(nodes.end(), sub.begin(), sub.end());
+        for (size_t i = off; i < nodes.size(); i += 16) {
+            int ints[4];
+            std::memcpy(ints, &nodes[i + 12], sizeof(ints));
+            for (int k = 0; k < 2; ++k)
+                if (ints[2 + k] == 0) ints[k] += base;
+            std::memcpy(&nodes[i + 12], ints, sizeof(ints));
+        }
+    }
+    std::vector<float> own_scratch;
+    std::vector<float> &rnodes_scratch() { own_scratch.clear(); return own_scratch; }
 };
 
 } // namespace
@@ -281,9 +400,12 @@ void bvh4_bfs_order(std::vector<float> &nodes) {
     nodes.swap(out);
 }
 
-/* the device's decode of a quantized bound (traverse4 / trav_step) */
-static float qdecode(float o, uint32_t q, int e) { return o + (float)q * std::ldexp(1.0f, e); }
+/* the device's decode of a quantized bound (traverse4 / trav_step): o + q * 2^e,
+ * the power of two s = 2^e passed exactly */
+static float qdecode(float o, uint32_t q, float s) { return o + (float)q * s; }
 
+static bool quantize_nodes(const std::vector<float> &nodes, const std::vector<uint32_t> &refs, std::vector<uint32_t> &q,
+                           int i0, int i1);
 bool quantize_bvh4(const std::vector<float> &nodes, std::vector<uint32_t> &q) {
     return quantize_bvh4(nodes, std::vector<uint32_t>(), q);
 }
@@ -291,7 +413,16 @@ bool quantize_bvh4(const std::vector<float> &nodes, std::vector<uint32_t> &q) {
 bool quantize_bvh4(const std::vector<float> &nodes, const std::vector<uint32_t> &refs, std::vector<uint32_t> &q) {
     const size_t nn = nodes.size() / 32;
     q.assign(nn * 16, 0u);
-    for (size_t i = 0; i < nn; ++i) {
+    std::atomic<bool> ok{true};
+    /* nodes encode independently: chunks of nodes in parallel */
+    const int parts = nn >= 4096 ? build_threads() : 1;
+    parallel_chunks(0, (int)nn, parts, [&](int, int i0, int i1) { if (!quantize_nodes(nodes, refs, q, i0, i1)) ok = false; });
+    return ok;
+}
+
+static bool quantize_nodes(const std::vector<float> &nodes, const std::vector<uint32_t> &refs, std::vector<uint32_t> &q,
+                           int i0, int i1) {
+    for (size_t i = (size_t)i0; i < (size_t)i1; ++i) {
         const float *n = &nodes[i * 32];
         int codes[4], counts[4];
         std::memcpy(codes, &n[24], sizeof(codes));
@@ -304,9 +435,18 @@ bool quantize_bvh4(const std::vector<float> &nodes, const std::vector<uint32_t> 
                 if (counts[k] != -1) { lo = std::min(lo, n[4 * a + k]); hi = std::max(hi, n[4 * (3 + a) + k]); }
             if (!(lo <= hi)) lo = hi = 0.f; /* no children (empty scene root) */
             const double ext = (double)hi - (double)lo;
+            /* the smallest e >= -126 with 255 * 2^e >= ext (a linear search
+             * from -126 cost ~400 ldexp calls per node) */
             int e = -126;
+            if (ext > 0.0) {
+                int ex = 0;
+                (void)std::frexp(ext / 255.0, &ex);
+                e = std::max(-126, std::min(127, ex - 1));
+                while (e > -126 && std::ldexp(255.0, e - 1) >= ext) --e;
+            }
             while (e < 127 && std::ldexp(255.0, e) < ext) ++e;
             const double s = std::ldexp(1.0, e);
+            const float sf = std::ldexp(1.0f, e);
             std::memcpy(&w[a], &lo, 4);
             ebytes |= (uint32_t)(e + 128) << (8 * a);
             uint32_t ql = 0, qh = 0;
@@ -316,9 +456,9 @@ bool quantize_bvh4(const std::vector<float> &nodes, const std::vector<uint32_t> 
                     const float clo = n[4 * a + k], chi = n[4 * (3 + a) + k];
                     bl = (uint32_t)std::min(255.0, std::max(0.0, std::floor(((double)clo - lo) / s)));
                     bh = (uint32_t)std::min(255.0, std::max(0.0, std::ceil(((double)chi - lo) / s)));
-                    while (bl > 0 && qdecode(lo, bl, e) > clo) --bl;
-                    while (bh < 255 && qdecode(lo, bh, e) < chi) ++bh;
-                    if (qdecode(lo, bl, e) > clo || qdecode(lo, bh, e) < chi) return false;
+                    while (bl > 0 && qdecode(lo, bl, sf) > clo) --bl;
+                    while (bh < 255 && qdecode(lo, bh, sf) < chi) ++bh;
+                    if (qdecode(lo, bl, sf) > clo || qdecode(lo, bh, sf) < chi) return false;
                 }
                 ql |= bl << (8 * k);
                 qh |= bh << (8 * k);
@@ -343,10 +483,19 @@ bool quantize_bvh4(const std::vector<float> &nodes, const std::vector<uint32_t> 
     return true;
 }
 
+int host_threads() { return build_threads(); }
+void parallel_for(int64_t n, const std::function<void(int64_t, int64_t)> &f, int64_t min_per_thread) {
+    const int parts = (int)std::max<int64_t>(1, std::min<int64_t>(build_threads(), n / std::max<int64_t>(1, min_per_thread)));
+    if (parts <= 1) { f(0, n); return; }
+    std::vector<std::thread> th;
+    for (int k = 0; k < parts; ++k) th.emplace_back(f, n * k / parts, n * (k + 1) / parts);
+    for (auto &t : th) t.join();
+}
+
 void build_bvh(std::vector<BuildPrim> &prims, int max_depth, BvhOut &out, const BvhCost &cost) {
     out.nodes.clear();
     out.refs.clear();
-    BvhBuilder B{prims, out.nodes, max_depth, cost};
+    BvhBuilder B{prims, out.nodes, max_depth, cost, 0, (int)prims.size() >= SUBTREE_TASK_MIN ? build_threads() : 1};
     int n = (int)prims.size();
     Box empty;
     if (n == 0) {

@@ -14,6 +14,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <functional>
 #include <vector>
 
 #include "../../include/pm_api.h"
@@ -38,6 +39,12 @@ struct BvhCost {
     int leaf_max = 1;
 };
 void build_bvh(std::vector<BuildPrim> &prims, int max_depth, BvhOut &out, const BvhCost &cost = BvhCost());
+
+/* host threads of the builders (PM_BUILD_THREADS, else OMP_NUM_THREADS, else
+ * the hardware's; at most 32) and a parallel loop over [0, n) in contiguous
+ * chunks of at least min_per_thread: f(begin, end) */
+int host_threads();
+void parallel_for(int64_t n, const std::function<void(int64_t, int64_t)> &f, int64_t min_per_thread = 1 << 15);
 
 /* 4-wide BVH collapsed from the binary one (each node takes its binary
  * node's children and opens the largest internal child until it has four):

@@ -99,6 +99,9 @@ struct TraceParams {
     int bucket;
     GridDesc grid;
     uint32_t *count, *key, *rank;
+    /* pooled kernel: non-null -> pool position i traces path path_begin +
+     * order[i] (launch_path_order: paths sorted by first-ray direction) */
+    const uint32_t *order;
     /* per-lane / pooled kernels: a path's deposits held in registers and
      * written once per path (pm_trace.hip Held; used when mpc == 4 and the
      * slot buffer is 16-B aligned) */
@@ -194,6 +197,9 @@ hipError_t launch_simple(const EyeParams &p, float *out, hipStream_t s);
 /* writes every slot of its paths (deposits, then zeros); count: census */
 /* resident waves of k_trace_pool per CU with `lds` bytes of dynamic LDS per block */
 int trace_pool_waves_per_cu(size_t lds, int hold);
+size_t scan_scratch_words(int64_t n);
+size_t path_order_scratch_words(int64_t n);
+hipError_t launch_path_order(const TraceParams &p, uint32_t *scratch, uint32_t *order, hipStream_t s);
 int trace_lane_waves_per_cu(const SceneDev &S, size_t lds, int hold);
 /* adaptive-grid histogram: sum the R2_COPIES copies into host-mapped
  * out[R2_BINS] with plain stores (no copy engine) and zero the copies */

@@ -708,7 +708,8 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
                 const int64_t mine = cursor + __popcll(dm & ((1ull << lane) - 1ull));
                 if (phase == PHASE_DEAD && mine < wend) {
                     if (HOLD) held_clear(held);
-                    if (emit_path(P, S, perm, (uint32_t)(P.path_begin + mine), st)) {
+                    const uint32_t pid = P.order ? (uint32_t)P.path_begin + P.order[mine] : (uint32_t)(P.path_begin + mine);
+                    if (emit_path(P, S, perm, pid, st)) {
                         trav_begin(st.ray, tr);
                         phase = PHASE_TRAV;
                     } else {
@@ -754,6 +755,56 @@ int trace_pool_waves_per_cu(size_t lds, int hold) { /* lds: stacks (+ nodelets) 
                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0, 0>, TRACE_BLOCK, lds);
     if (e != hipSuccess) return 0;
     return blocks * (TRACE_BLOCK / 64);
+}
+
+/* Path order for the pooled kernel (env PM_PATH_SORT): the launch's paths
+ * counting-sorted by the direction of their first ray (octahedral map,
+ * PATH_KEY_RES^2 cells), so that a wave's pool starts its rays in similar
+ * directions from the light (and their hit points, and the subtrees they
+ * visit, cluster). Keys: one emission per path (the same Halton sample and
+ * Sample_L the trace recomputes). */
+constexpr int PATH_KEY_RES = 64;
+__global__ __launch_bounds__(256) void k_path_key(TraceParams P, uint32_t *count, uint32_t *key, uint32_t *rank) {
+    __shared__ uint32_t perm[28];
+    if (threadIdx.x < 28) perm[threadIdx.x] = P.perm[threadIdx.x];
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= P.path_count) return;
+    PathState st;
+    const bool ok = emit_path(P, P.S, perm, (uint32_t)(P.path_begin + i), st);
+    uint32_t k = 0u;
+    if (ok) {
+        const v3 d = st.ray.d;
+        const float l1 = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
+        float u = d.x / l1, v = d.z / l1;
+        if (d.y < 0.f) { const float uu = (1.f - fabsf(v)) * (u < 0.f ? -1.f : 1.f); v = (1.f - fabsf(u)) * (v < 0.f ? -1.f : 1.f); u = uu; }
+        const int iu = min(PATH_KEY_RES - 1, max(0, (int)((u * 0.5f + 0.5f) * PATH_KEY_RES)));
+        const int iv = min(PATH_KEY_RES - 1, max(0, (int)((v * 0.5f + 0.5f) * PATH_KEY_RES)));
+        k = (uint32_t)(iv * PATH_KEY_RES + iu);
+    }
+    key[i] = k;
+    rank[i] = atomicAdd(&count[k], 1u);
+}
+__global__ __launch_bounds__(256) void k_path_fill(int64_t n, const uint32_t *key, const uint32_t *rank,
+                                                   const uint32_t *start, uint32_t *order) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) order[start[key[i]] + rank[i]] = (uint32_t)i;
+}
+size_t path_order_scratch_words(int64_t n) {
+    return (size_t)(2 * n) + 2 * ((size_t)PATH_KEY_RES * PATH_KEY_RES + 1) + scan_scratch_words(PATH_KEY_RES * PATH_KEY_RES + 1);
+}
+hipError_t launch_path_order(const TraceParams &p, uint32_t *scratch, uint32_t *order, hipStream_t s) {
+    const int64_t n = p.path_count;
+    if (n <= 0) return hipSuccess;
+    const int64_t nk = (int64_t)PATH_KEY_RES * PATH_KEY_RES + 1;
+    uint32_t *key = scratch, *rank = scratch + n, *count = scratch + 2 * n, *start = count + nk, *sums = start + nk;
+    hipError_t e = hipMemsetAsync(count, 0, (size_t)nk * 4, s);
+    if (e != hipSuccess) return e;
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    pm_launch(k_path_key, dim3(grid), dim3(256), 0, s, p, count, key, rank);
+    if ((e = launch_exclusive_scan(count, nk, start, sums, s)) != hipSuccess) return e;
+    pm_launch(k_path_fill, dim3(grid), dim3(256), 0, s, n, key, rank, start, order);
+    return hipGetLastError();
 }
 
 /* resident waves per CU of the per-lane kernel (scene mode of S) with or

@@ -19,9 +19,26 @@ def test_quantized_boxes_contain_float_boxes(tmp_path, nprims, mode):
     all-triangle leaves (~first storage slot); a leaf of >= LEAF_TRIS
     primitives is rejected (the scene then keeps the binary traversal)."""
     exe = tmp_path / "qcheck"
-    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", CSRC, "-I", os.path.join(ROOT, "include"),
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-ffp-contract=off", "-I", CSRC, "-I", os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "tests", "native", "bvh4_quant_check.cpp"), os.path.join(CSRC, "pm_build.cpp"),
                     "-o", str(exe)], check=True, timeout=300)
     r = subprocess.run([str(exe), str(nprims)] + ([mode] if mode else []), capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "bad 0" in r.stdout
+
+
+def test_threaded_build_is_the_serial_tree(tmp_path):
+    """The SAH build bins large ranges and builds left subtrees in threads
+    (PM_BUILD_THREADS / OMP_NUM_THREADS): the binary nodes, refs and the
+    quantized 4-wide nodes are bit-identical to the single-threaded build."""
+    exe = tmp_path / "bcheck"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-ffp-contract=off", "-I", CSRC, "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "native", "bvh_build_check.cpp"), os.path.join(CSRC, "pm_build.cpp"),
+                    "-o", str(exe)], check=True, timeout=300)
+    outs = []
+    for t in ("1", "4"):
+        r = subprocess.run([str(exe), "200000"], capture_output=True, text=True, timeout=300,
+                           env={**os.environ, "PM_BUILD_THREADS": t})
+        assert r.returncode == 0, r.stderr
+        outs.append(r.stdout.strip())
+    assert outs[0] == outs[1] and "hash" in outs[0]

@@ -47,14 +47,17 @@ def test_photon_trace_bitexact(cornell, paths, pass_index):
     assert_bitexact(gpu, ref, "photon slots")
 
 
-@pytest.mark.parametrize("hold", ["0", "1"])
+@pytest.mark.parametrize("hold,sort", [("0", "0"), ("1", "0"), ("0", "1")])
 @pytest.mark.parametrize("scene", ["cornell", "soup"])
-def test_photon_trace_write_modes_bitexact(hold, scene, oracle_mod, hip_mod, monkeypatch):
+def test_photon_trace_write_modes_bitexact(hold, sort, scene, oracle_mod, hip_mod, monkeypatch):
     """Slots and the fused bucket counts are the same whether a path's
     deposits are written as they happen (PM_TRACE_HOLD=0) or held and written
-    once per path with 16-B stores (default): brute-force and BVH scenes,
-    every slot bit-exact vs the oracle, map photons == valid slots."""
+    once per path with 16-B stores, and whether the pooled BVH kernel takes
+    its paths in id order or sorted by first-ray direction (PM_PATH_SORT=1):
+    brute-force and BVH scenes, every slot bit-exact vs the oracle, map
+    photons == valid slots."""
     monkeypatch.setenv("PM_TRACE_HOLD", hold)
+    monkeypatch.setenv("PM_PATH_SORT", sort)
     sc = scenes.cornell_box(32, 32) if scene == "cornell" else scenes.triangle_soup(20000, 32, 32)
     ctx, orc = make_pair(sc, oracle_mod, hip_mod)
     try:
