@@ -100,12 +100,21 @@ def load_pmc_traffic(kernel_prefix, config):
     FETCH x2 correction; tools/pmc_traffic.py) of this kernel from the
     committed profile — only if it was measured on these exact HIP sources
     and this config; else (None, reason)."""
-    path = os.path.join(ROOT, "profiles", "r02", "pmc_traffic_%s.json" % config)
-    if not os.path.exists(path):
+    sha = kernel_src_sha()
+    path, d = None, None
+    for rnd in ("r03", "r02"):      # the newest committed profile of these sources
+        cand = os.path.join(ROOT, "profiles", rnd, "pmc_traffic_%s.json" % config)
+        if os.path.exists(cand):
+            with open(cand) as f:
+                dd = json.load(f)
+            if path is None:
+                path, d = cand, dd
+            if dd.get("kernel_src_sha") == sha:
+                path, d = cand, dd
+                break
+    if path is None:
         return None, "no committed PMC profile for this config"
-    with open(path) as f:
-        d = json.load(f)
-    if d.get("kernel_src_sha") != kernel_src_sha():
+    if d.get("kernel_src_sha") != sha:
         return None, "committed PMC profile is from other HIP sources (%s)" % d.get("kernel_src_sha")
     k = d.get("kernels", {}).get(kernel_prefix)
     if not k:
@@ -168,6 +177,9 @@ def cpu_baseline(scene, params, threads, cfg):
         "cores": threads,
         "kind": "port",
         "host_cpus": os.cpu_count(),
+        "threads_note": "the oracle runs std::thread over this process's CPU share (OMP_NUM_THREADS: 16 per GPU "
+                        "on the MI355X box), not hardware_concurrency(): the box's other CPUs belong to the other "
+                        "GPUs' jobs, so host_cpus threads would not be a clean measurement",
         "cpu_model": cpu_model(),
         "sample": f"{passes} full {cfg.upper()} passes on the host with {threads} threads (this process's CPU share; "
                   f"the host has {os.cpu_count()}) — each: trace {params.paths_per_pass} paths + pbrt kd-tree "
