@@ -141,7 +141,7 @@ struct Ctx {
      * the grid_quantile of the records' radii (the rest scan per lane).
      * Staleness is safe (radii only shrink); anything that can raise a
      * radius (eye pass, reset, upload, set_radius2, split / partial updates)
-     * invalidates it. env PM_GRID_QUANTILE (default 0.95; <= 0 disables). */
+     * invalidates it. env PM_GRID_QUANTILE (default 0.9; <= 0 disables). */
     /* gather order (incoherent scenes, launch_record_order): active records
      * in cell order, built once per eye pass; env PM_REC_ORDER = 1 always,
      * -1 auto (when > 20 % of the active tiles do not fit one LDS group),
@@ -159,7 +159,7 @@ struct Ctx {
     bool r2_valid = false;     /* the last landed / in-flight histogram describes the records */
     float r2_hist_init = 0.f;  /* the r^2 its bins are relative to */
     float design_r2 = 0.f;     /* grid radius^2 of the current photon map (0: initial_radius2) */
-    double grid_quantile = 0.95;
+    double grid_quantile = 0.9; /* C5 step (same box, 3 runs each): 0.95 0.82-0.85 ms, 0.9 0.784-0.790, 0.8 0.826 */
     /* leading words of d_count known to be zero (the bucket scan clears the
      * counters it reads); valid while d_count.p == count_zero_ptr */
     size_t count_zero_words = 0;

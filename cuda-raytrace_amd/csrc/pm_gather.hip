@@ -368,9 +368,9 @@ constexpr uint32_t GROUP_R = PM_GROUP_R;
 constexpr int GROUP_MIN = PM_GROUP_MIN, GROUP_MIN_SPARSE = PM_GROUP_MIN_SPARSE;
 constexpr uint32_t SPARSE_CELLS = 20;
 #ifndef PM_TILE_UMAX
-#define PM_TILE_UMAX 1024
+#define PM_TILE_UMAX 512
 #endif
-constexpr int TILE_UMAX = PM_TILE_UMAX; /* C5: no cap 2.88 ms, 2048 0.44, 1024 0.41, 512 0.43 (per lane 0.42) */
+constexpr int TILE_UMAX = PM_TILE_UMAX; /* C5 (r02 grid): no cap 2.88 ms, 2048 0.44, 1024 0.41, 512 0.43; adaptive grid (r03): 2048 0.268, 1024 0.24, 512 0.205; C2 unchanged */
 static_assert(2 * GROUP_R + 2 <= 8, "group rows exceed the 64-lane row map");
 /* the updated radii of a wave into the adaptive-grid histogram
  * (GatherParams::r2hist): one atomic per distinct bin of the wave (a tile's
