@@ -17,6 +17,7 @@
 #include <mutex>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pm_build.h"
@@ -478,6 +479,188 @@ int check_params(Ctx *c, const pm_render_params *p) {
     return PM_OK;
 }
 
+/* where pm_commit put each section of the scene blob */
+struct SceneLayout {
+    size_t o_nodes = 0, o_refs = 0, o_geo = 0, o_shade = 0, o_tid = 0, o_info = 0, o_norms = 0, o_disks = 0,
+           o_spheres = 0, o_mats = 0, o_lights = 0, o_wnodes = 0, bytes = 0;
+    int64_t n_nodes = 0, n_refs = 0, n_tris = 0;
+    bool id_order = false;
+    int wide = 0, wide_stack = 0, nodelets = 0;
+};
+
+/* per triangle t: (p0, e0, e1, n) for the intersector, the normalized
+ * shading frame for hits, vertex ids + mesh */
+void tri_record(const Ctx *c, uint32_t t, float4 *geo, float4 *shade, int4 *info) {
+    const float *V = c->P.data();
+    const HTri &tr = c->tris[t];
+    const HMesh &m = c->meshes[tr.mesh];
+    const float *p0 = V + 3 * tr.v[0], *p1 = V + 3 * tr.v[1], *p2 = V + 3 * tr.v[2];
+    float e0[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
+    float e1[3] = {p0[0] - p2[0], p0[1] - p2[1], p0[2] - p2[2]};
+    float n[3] = {e1[1] * e0[2] - e1[2] * e0[1], e1[2] * e0[0] - e1[0] * e0[2], e1[0] * e0[1] - e1[1] * e0[0]};
+    geo[0] = f4(p0[0], p0[1], p0[2], e0[0]);
+    geo[1] = f4(e0[1], e0[2], e1[0], e1[1]);
+    geo[2] = f4(e1[2], n[0], n[1], n[2]);
+    float ns[3], dpdu[3];
+    tri_frame(p0, p1, p2, m.has_uv ? &c->UV[0] : nullptr, tr.v, n, ns, dpdu);
+    shade[0] = f4(ns[0], ns[1], ns[2], bits_f((uint32_t)m.material | (m.has_n ? 0x80000000u : 0u)));
+    shade[1] = f4(dpdu[0], dpdu[1], dpdu[2], bits_f((uint32_t)m.light));
+    *info = make_int4(tr.v[0], tr.v[1], tr.v[2], tr.mesh);
+}
+
+std::vector<float4> vertex_normals(const Ctx *c) {
+    std::vector<float4> norms(c->N.size() / 3);
+    for (size_t i = 0; i < norms.size(); ++i) norms[i] = f4(c->N[3 * i], c->N[3 * i + 1], c->N[3 * i + 2], 0.f);
+    return norms;
+}
+
+/* PLOC neighbour radius (env PM_PLOC_RADIUS, 1..32). C3 trace per 1M paths
+ * on the host-built PLOC tree (same box): r 1 5.87 ms, 2 4.70, 3 4.50, 4
+ * 4.58–4.63, 8 5.12, 16 5.73; the binned-SAH tree 4.50–4.51 */
+int ploc_radius() {
+    const char *e = getenv("PM_PLOC_RADIUS");
+    return e ? std::max(1, std::min(32, atoi(e))) : 3;
+}
+
+/* env PM_BVH_BUILD: "gpu" (the device PLOC build, pm_bvh_gpu.hip), "host"
+ * (the binned-SAH host build), "ploc-host" (the device's algorithm on the
+ * host: A/B and test oracle); unset or "auto": the device for scenes of at
+ * least PM_BVH_GPU_MIN (65,536) primitives, whose host build dominated the
+ * scene setup (C3: 0.28 s SAH of a 0.51 s commit) */
+bool gpu_bvh_wanted(int64_t nprims) {
+    const char *b = getenv("PM_BVH_BUILD");
+    const std::string m = b ? b : "auto";
+    int64_t gmin = 1 << 16;
+    if (const char *e = getenv("PM_BVH_GPU_MIN")) gmin = std::max<int64_t>(2, atoll(e));
+    const bool want = m == "gpu" ? nprims >= 2 : (m == "auto" && nprims >= gmin);
+    if (!want || PM_BVH4_QUANT == 0) return false;
+    /* the host path's experiment knobs for the 4-wide tree are host-only */
+    for (const char *k : {"PM_BVH_WIDE", "PM_BVH4_LEAF", "PM_NODELETS", "PM_BVH4_BFS", "PM_LEAF_TRIS", "PM_BVH_LEAF_MAX"})
+        if (getenv(k)) return false;
+    return true;
+}
+
+struct TmpBuf : DevBuf {
+    ~TmpBuf() { release(); }
+};
+
+/* the scene blob with the BVH built on the device: boxes from the host's
+ * parallel pass uploaded, gpu_bvh_build writes the 4-wide nodes and refs in
+ * place, the triangle records (computed on the host in triangle-id order
+ * while the device builds) are uploaded and permuted into storage order.
+ * built = false: the caller runs the host build (the device tree exceeded a
+ * limit the traversal has, or the build failed — reported on stderr) */
+int commit_gpu_bvh(Ctx *c, const std::vector<BuildPrim> &prims, int64_t nt, SceneLayout &L, bool &built, bool ptimes) {
+    built = false;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+    const int n = (int)prims.size();
+    GpuBvhIn in{};
+    in.n = n;
+    in.radius = ploc_radius();
+    ploc_morton_frame(prims, in.frame_lo, in.frame_scale);
+    std::vector<float4> geo(3 * (size_t)nt), shade(2 * (size_t)nt);
+    std::vector<int4> info((size_t)nt);
+    struct Joiner {
+        std::thread t;
+        ~Joiner() { if (t.joinable()) t.join(); }
+    } records;
+    records.t = std::thread([&] {
+        parallel_for(nt, [&](int64_t k0, int64_t k1) {
+            for (int64_t k = k0; k < k1; ++k) tri_record(c, (uint32_t)k, &geo[3 * k], &shade[2 * k], &info[k]);
+        });
+    });
+    std::vector<float4> hb(2 * (size_t)n);
+    parallel_for(n, [&](int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i) {
+            const BuildPrim &p = prims[i];
+            hb[2 * i] = f4(p.lo[0], p.lo[1], p.lo[2], bits_f(p.ref));
+            hb[2 * i + 1] = f4(p.hi[0], p.hi[1], p.hi[2], 0.f);
+        }
+    });
+    TmpBuf d_box, d_tord, d_src;
+    HIPCHK(c, d_box.ensure(hb.size() * sizeof(float4)));
+    HIPCHK(c, hipMemcpy(d_box.p, hb.data(), hb.size() * sizeof(float4), hipMemcpyHostToDevice));
+    in.box = d_box.as<float4>();
+    /* blob sections in pm_commit's order; no binary tree (a 16-B placeholder) */
+    const std::vector<float4> norms = vertex_normals(c);
+    size_t off = 0;
+    auto sect = [&](size_t bytes) { const size_t o = (off + 15) & ~(size_t)15; off = o + bytes; return o; };
+    L.o_nodes = sect(16);
+    L.o_refs = sect(4 * (size_t)n);
+    L.o_geo = sect(48 * (size_t)nt);
+    L.o_shade = sect(32 * (size_t)nt);
+    L.o_tid = sect(4 * (size_t)nt);
+    L.o_info = sect(16 * (size_t)nt);
+    L.o_norms = sect(norms.size() * sizeof(float4));
+    L.o_disks = sect(c->disks.size() * sizeof(float4));
+    L.o_spheres = sect(c->spheres.size() * sizeof(float4));
+    L.o_mats = sect(c->materials.size() * sizeof(float4));
+    L.o_lights = sect(c->lights.size() * sizeof(LightDev));
+    L.o_wnodes = sect(64 * (size_t)(n - 1));
+    /* never LDS-resident: the LDS modes traverse the binary tree this path does not build */
+    L.bytes = std::max<size_t>((off + 15) & ~(size_t)15, (size_t)LDS_SCENE_MAX + 16);
+    HIPCHK(c, c->d_scene.ensure(L.bytes));
+    char *base = c->d_scene.as<char>();
+    HIPCHK(c, hipMemsetAsync(base + L.o_nodes, 0, 16, c->stream));
+    auto put = [&](size_t o, const void *src, size_t bytes) {
+        return bytes ? hipMemcpyAsync(base + o, src, bytes, hipMemcpyHostToDevice, c->stream) : hipSuccess;
+    };
+    HIPCHK(c, put(L.o_norms, norms.data(), norms.size() * sizeof(float4)));
+    HIPCHK(c, put(L.o_disks, c->disks.data(), c->disks.size() * sizeof(float4)));
+    HIPCHK(c, put(L.o_spheres, c->spheres.data(), c->spheres.size() * sizeof(float4)));
+    HIPCHK(c, put(L.o_mats, c->materials.data(), c->materials.size() * sizeof(float4)));
+    HIPCHK(c, put(L.o_lights, c->lights.data(), c->lights.size() * sizeof(LightDev)));
+    HIPCHK(c, d_tord.ensure(4 * (size_t)std::max<int64_t>(nt, 1)));
+    GpuBvhOut out;
+    out.wnodes = reinterpret_cast<uint4 *>(base + L.o_wnodes);
+    out.refs = reinterpret_cast<uint32_t *>(base + L.o_refs);
+    out.tri_order = d_tord.as<uint32_t>();
+    out.max_nodes = n - 1;
+    const double t_up = ms();
+    const hipError_t e = gpu_bvh_build(in, out, c->stream);
+    const double t_build = ms();
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        fprintf(stderr, "pm_commit: device BVH build failed (%s); host build\n", hipGetErrorString(e));
+        return PM_OK;
+    }
+    if (out.max_stack > BVH_STACK || out.n_tris != nt) {
+        fprintf(stderr, "pm_commit: device BVH stack bound %d (limit %d), %lld triangles; host build\n", out.max_stack,
+                BVH_STACK, (long long)out.n_tris);
+        return PM_OK;
+    }
+    records.t.join();
+    const double t_rec = ms();
+    HIPCHK(c, d_src.ensure(96 * (size_t)std::max<int64_t>(nt, 1)));
+    float4 *src_geo = d_src.as<float4>(), *src_shade = src_geo + 3 * nt;
+    int4 *src_info = reinterpret_cast<int4 *>(src_shade + 2 * nt);
+    HIPCHK(c, hipMemcpyAsync(src_geo, geo.data(), geo.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(src_shade, shade.data(), shade.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(src_info, info.data(), info.size() * sizeof(int4), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_tri_permute(d_tord.as<uint32_t>(), nt, src_geo, src_shade, src_info,
+                                 reinterpret_cast<float4 *>(base + L.o_geo), reinterpret_cast<float4 *>(base + L.o_shade),
+                                 reinterpret_cast<uint32_t *>(base + L.o_tid), reinterpret_cast<int4 *>(base + L.o_info),
+                                 c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (ptimes)
+        fprintf(stderr, "pm_commit: device build: boxes up %.1f ms, PLOC + collapse %.1f ms (%d rounds, %lld nodes, depth %d, "
+                        "stack %d), records %.1f ms, permute %.1f ms\n", t_up, t_build - t_up, out.rounds,
+                (long long)out.nodes, out.depth, out.max_stack, t_rec, ms());
+    c->bvh_depth = out.depth;
+    c->bvh4_nodes = out.nodes;
+    c->bvh4_depth = out.depth;
+    L.n_nodes = out.nodes;
+    L.n_refs = n;
+    L.n_tris = nt;
+    L.id_order = false;
+    L.wide = 2;
+    L.wide_stack = out.max_stack;
+    L.nodelets = 0;
+    built = true;
+    return PM_OK;
+}
+
 } // namespace
 
 extern "C" {
@@ -842,176 +1025,183 @@ int pm_commit(void *ptr) {
         }
         add_box(lo, hi, (PRIM_SPHERE << 30) | (uint32_t)i);
     }
-    BvhOut bvh;
-    BvhCost cost;
-    if (const char *e = getenv("PM_BVH_LEAF_MAX")) cost.leaf_max = std::max(1, atoi(e));
-    if (const char *e = getenv("PM_BVH_CTRAV")) cost.c_trav = (float)atof(e);
-    /* env PM_COMMIT_TIMES=1: the host build's phases on stderr (setup-time study) */
+    /* env PM_COMMIT_TIMES=1: the build's phases on stderr (setup-time study) */
     const bool ptimes = getenv("PM_COMMIT_TIMES") != nullptr;
     auto tnow = [] { return std::chrono::steady_clock::now(); };
     auto tms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
         return std::chrono::duration<double, std::milli>(b - a).count();
     };
-    const auto t_build0 = tnow();
-    build_bvh(prims, BVH_STACK - 2, bvh, cost);
-    if (ptimes) fprintf(stderr, "pm_commit: %zu prims (boxes %.1f ms), SAH build %.1f ms\n", prims.size(),
-                        tms(t_commit0, t_build0), tms(t_build0, tnow()));
-    c->bvh_depth = bvh.depth;
-    if (bvh.depth >= BVH_STACK) FAIL(c, PM_ERR_INVALID, "BVH too deep (%d)", bvh.depth);
-
-    /* tiny LDS scenes skip the BVH (MODE_BRUTE); env PM_TRACE_BRUTE_MAX
-     * overrides the limit (0 = never). Their triangles are stored in global-id
-     * order (brute_isect's tie-break relies on it), others in leaf order. */
-    const char *brute_env = getenv("PM_TRACE_BRUTE_MAX");
-    const int brute_max = brute_env ? atoi(brute_env) : BRUTE_MAX_PRIMS;
-    const bool id_order = (int64_t)bvh.refs.size() <= brute_max;
-    std::vector<uint32_t> tri_order; /* triangle ids in storage order */
-    tri_order.reserve(nt);
-    if (id_order) {
-        for (int64_t t = 0; t < nt; ++t) tri_order.push_back((uint32_t)t);
-    } else {
-        for (uint32_t ref : bvh.refs)
-            if ((ref >> 30) == PRIM_TRI) tri_order.push_back(ref & 0x3fffffffu);
+    SceneLayout L;
+    int rc;
+    bool built = false;
+    if (gpu_bvh_wanted((int64_t)prims.size())) {
+        if ((rc = commit_gpu_bvh(c, prims, nt, L, built, ptimes))) return rc;
+        if (ptimes && built) fprintf(stderr, "pm_commit: device build, total %.1f ms\n", tms(t_commit0, tnow()));
     }
-    std::vector<uint32_t> slot_of(nt);
-    for (size_t k = 0; k < tri_order.size(); ++k) slot_of[tri_order[k]] = (uint32_t)k;
-    parallel_for((int64_t)bvh.refs.size(), [&](int64_t i0, int64_t i1) {
-        for (int64_t i = i0; i < i1; ++i) {
-            uint32_t &ref = bvh.refs[i];
-            if ((ref >> 30) == PRIM_TRI) ref = (PRIM_TRI << 30) | slot_of[ref & 0x3fffffffu];
+    if (!built) {
+        L = SceneLayout();
+        BvhOut bvh;
+        BvhCost cost;
+        if (const char *e = getenv("PM_BVH_LEAF_MAX")) cost.leaf_max = std::max(1, atoi(e));
+        if (const char *e = getenv("PM_BVH_CTRAV")) cost.c_trav = (float)atof(e);
+        const auto t_build0 = tnow();
+        /* env PM_BVH_BUILD=ploc-host: the device builder's PLOC tree built on
+         * the host (A/B of the tree quality; PM_PLOC_RADIUS) */
+        const char *bb = getenv("PM_BVH_BUILD");
+        if (bb && std::strcmp(bb, "ploc-host") == 0 && prims.size() > 1) {
+            PlocTree pt;
+            build_ploc(prims, ploc_radius(), pt);
+            ploc_to_bvh(prims, pt, bvh);
+        } else {
+            build_bvh(prims, BVH_STACK - 2, bvh, cost);
         }
-    });
+        if (ptimes) fprintf(stderr, "pm_commit: %zu prims (boxes %.1f ms), host build %.1f ms\n", prims.size(),
+                            tms(t_commit0, t_build0), tms(t_build0, tnow()));
+        c->bvh_depth = bvh.depth;
+        if (bvh.depth >= BVH_STACK) FAIL(c, PM_ERR_INVALID, "BVH too deep (%d)", bvh.depth);
 
-    /* per-triangle precomputed (p0, e0, e1, n) for the intersector and the
-     * normalized shading frame for hits (in parallel chunks of storage slots) */
-    const int64_t nst = (int64_t)tri_order.size();
-    std::vector<float4> tri_geo(3 * nst), tri_shade(2 * nst);
-    std::vector<int4> tri_info(nst);
-    std::vector<uint32_t> tri_id(nst);
-    parallel_for(nst, [&](int64_t k0, int64_t k1) {
-        for (int64_t k = k0; k < k1; ++k) {
-            const uint32_t t = tri_order[k];
-            const HTri &tr = c->tris[t];
-            const HMesh &m = c->meshes[tr.mesh];
-            const float *p0 = V + 3 * tr.v[0], *p1 = V + 3 * tr.v[1], *p2 = V + 3 * tr.v[2];
-            float e0[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
-            float e1[3] = {p0[0] - p2[0], p0[1] - p2[1], p0[2] - p2[2]};
-            float n[3] = {e1[1] * e0[2] - e1[2] * e0[1], e1[2] * e0[0] - e1[0] * e0[2], e1[0] * e0[1] - e1[1] * e0[0]};
-            tri_geo[3 * k + 0] = f4(p0[0], p0[1], p0[2], e0[0]);
-            tri_geo[3 * k + 1] = f4(e0[1], e0[2], e1[0], e1[1]);
-            tri_geo[3 * k + 2] = f4(e1[2], n[0], n[1], n[2]);
-            float ns[3], dpdu[3];
-            tri_frame(p0, p1, p2, m.has_uv ? &c->UV[0] : nullptr, tr.v, n, ns, dpdu);
-            tri_shade[2 * k + 0] = f4(ns[0], ns[1], ns[2], bits_f((uint32_t)m.material | (m.has_n ? 0x80000000u : 0u)));
-            tri_shade[2 * k + 1] = f4(dpdu[0], dpdu[1], dpdu[2], bits_f((uint32_t)m.light));
-            tri_info[k] = make_int4(tr.v[0], tr.v[1], tr.v[2], tr.mesh);
-            tri_id[k] = t;
+        /* tiny LDS scenes skip the BVH (MODE_BRUTE); env PM_TRACE_BRUTE_MAX
+         * overrides the limit (0 = never). Their triangles are stored in global-id
+         * order (brute_isect's tie-break relies on it), others in leaf order. */
+        const char *brute_env = getenv("PM_TRACE_BRUTE_MAX");
+        const int brute_max = brute_env ? atoi(brute_env) : BRUTE_MAX_PRIMS;
+        const bool id_order = (int64_t)bvh.refs.size() <= brute_max;
+        std::vector<uint32_t> tri_order; /* triangle ids in storage order */
+        tri_order.reserve(nt);
+        if (id_order) {
+            for (int64_t t = 0; t < nt; ++t) tri_order.push_back((uint32_t)t);
+        } else {
+            for (uint32_t ref : bvh.refs)
+                if ((ref >> 30) == PRIM_TRI) tri_order.push_back(ref & 0x3fffffffu);
         }
-    });
-    if (ptimes) fprintf(stderr, "pm_commit: triangle records done at %.1f ms\n", tms(t_commit0, tnow()));
-    std::vector<float4> norms(c->N.size() / 3);
-    for (size_t i = 0; i < norms.size(); ++i) norms[i] = f4(c->N[3 * i], c->N[3 * i + 1], c->N[3 * i + 2], 0.f);
-    std::vector<float4> nodes4(bvh.nodes.size() / 4);
-    std::memcpy(nodes4.data(), bvh.nodes.data(), bvh.nodes.size() * sizeof(float));
+        std::vector<uint32_t> slot_of(nt);
+        for (size_t k = 0; k < tri_order.size(); ++k) slot_of[tri_order[k]] = (uint32_t)k;
+        parallel_for((int64_t)bvh.refs.size(), [&](int64_t i0, int64_t i1) {
+            for (int64_t i = i0; i < i1; ++i) {
+                uint32_t &ref = bvh.refs[i];
+                if ((ref >> 30) == PRIM_TRI) ref = (PRIM_TRI << 30) | slot_of[ref & 0x3fffffffu];
+            }
+        });
 
-    /* one blob of 16-B aligned sections: the same offsets address it in HBM
-     * and, for scenes that fit (SceneDev::lds_bytes), in each block's LDS copy */
-    std::vector<unsigned char> blob;
-    /* one reservation for every section (no regrowth copies of a 250 MB blob) */
-    blob.reserve(16 * 16 + nodes4.size() * sizeof(float4) + bvh.refs.size() * 4 + tri_geo.size() * sizeof(float4) +
-                 tri_shade.size() * sizeof(float4) + tri_id.size() * 4 + tri_info.size() * sizeof(int4) +
-                 norms.size() * sizeof(float4) + (c->disks.size() + c->spheres.size() + c->materials.size()) * sizeof(float4) +
-                 c->lights.size() * sizeof(LightDev) + (size_t)(bvh.nodes.size() / 16 + 1) * 64 * 2);
-    auto put = [&](const void *src, size_t n) -> size_t {
-        size_t off = (blob.size() + 15) & ~(size_t)15;
-        blob.resize(off + n, 0);
-        if (n) std::memcpy(&blob[off], src, n);
-        return off;
-    };
-    const size_t o_nodes = put(nodes4.data(), nodes4.size() * sizeof(float4));
-    const size_t o_refs = put(bvh.refs.data(), bvh.refs.size() * sizeof(uint32_t));
-    const size_t o_geo = put(tri_geo.data(), tri_geo.size() * sizeof(float4));
-    const size_t o_shade = put(tri_shade.data(), tri_shade.size() * sizeof(float4));
-    const size_t o_tid = put(tri_id.data(), tri_id.size() * sizeof(uint32_t));
-    const size_t o_info = put(tri_info.data(), tri_info.size() * sizeof(int4));
-    const size_t o_norms = put(norms.data(), norms.size() * sizeof(float4));
-    const size_t o_disks = put(c->disks.data(), c->disks.size() * sizeof(float4));
-    const size_t o_spheres = put(c->spheres.data(), c->spheres.size() * sizeof(float4));
-    const size_t o_mats = put(c->materials.data(), c->materials.size() * sizeof(float4));
-    const size_t o_lights = put(c->lights.data(), c->lights.size() * sizeof(LightDev));
-    /* scenes traversed from HBM also get the 4-wide BVH (half the dependent
-     * node fetches per ray); env PM_BVH_WIDE=0 keeps the binary traversal,
-     * PM_BVH4_LEAF sets the largest subtree folded into one leaf */
-    size_t o_wnodes = 0;
-    int wide = 0, wide_stack = 0, nodelets = 0;
-    if (blob.size() > LDS_SCENE_MAX) {
-        const char *we = getenv("PM_BVH_WIDE");
-        if (!we || atoi(we) != 0) {
-            const char *le = getenv("PM_BVH4_LEAF");
-            Bvh4Out w;
-            const auto t_c0 = tnow();
-            collapse_bvh4(bvh, le ? atoi(le) : 1, w);
-            if (ptimes) fprintf(stderr, "pm_commit: collapse %.1f ms\n", tms(t_c0, tnow()));
-            /* node format fixed at build time (pm_device.h PM_BVH4_QUANT) */
-            std::vector<uint32_t> qn;
-            const bool quant = PM_BVH4_QUANT != 0;
-            const char *lt = getenv("PM_LEAF_TRIS"); /* 0: every leaf through its refs (A/B knob) */
-            /* a leaf the quantized count cannot code (>= LEAF_TRIS primitives,
-             * possible at build_bvh's depth limit) keeps the binary traversal,
-             * like a tree whose stack bound exceeds BVH_STACK */
-            /* env PM_NODELETS=N: the pooled trace kernel keeps the first N nodes
-             * in LDS, the tree renumbered breadth-first so that they are its
-             * top levels (PM_BVH4_BFS=1 renumbers without nodelets) */
-            const char *nl = getenv("PM_NODELETS"), *bf = getenv("PM_BVH4_BFS");
-            nodelets = nl ? std::max(0, atoi(nl)) : 0;
-            if (nodelets > 0 || (bf && atoi(bf) != 0)) bvh4_bfs_order(w.nodes);
-            const auto t_q0 = tnow();
-            const bool coded = !quant || quantize_bvh4(w.nodes, lt && atoi(lt) == 0 ? std::vector<uint32_t>() : bvh.refs, qn);
-            if (ptimes) fprintf(stderr, "pm_commit: quantize %.1f ms\n", tms(t_q0, tnow()));
-            if (coded && w.max_stack <= BVH_STACK) {
-                o_wnodes = quant ? put(qn.data(), qn.size() * sizeof(uint32_t))
-                                 : put(w.nodes.data(), w.nodes.size() * sizeof(float));
-                wide = quant ? 2 : 1;
-                wide_stack = w.max_stack;
-                c->bvh4_nodes = (int64_t)(w.nodes.size() / 32);
-                c->bvh4_depth = w.depth;
+        /* per-triangle precomputed (p0, e0, e1, n) for the intersector and the
+         * normalized shading frame for hits (in parallel chunks of storage slots) */
+        const int64_t nst = (int64_t)tri_order.size();
+        std::vector<float4> tri_geo(3 * nst), tri_shade(2 * nst);
+        std::vector<int4> tri_info(nst);
+        std::vector<uint32_t> tri_id(nst);
+        parallel_for(nst, [&](int64_t k0, int64_t k1) {
+            for (int64_t k = k0; k < k1; ++k) {
+                tri_record(c, tri_order[k], &tri_geo[3 * k], &tri_shade[2 * k], &tri_info[k]);
+                tri_id[k] = tri_order[k];
+            }
+        });
+        if (ptimes) fprintf(stderr, "pm_commit: triangle records done at %.1f ms\n", tms(t_commit0, tnow()));
+        const std::vector<float4> norms = vertex_normals(c);
+        std::vector<float4> nodes4(bvh.nodes.size() / 4);
+        std::memcpy(nodes4.data(), bvh.nodes.data(), bvh.nodes.size() * sizeof(float));
+
+        /* one blob of 16-B aligned sections: the same offsets address it in HBM
+         * and, for scenes that fit (SceneDev::lds_bytes), in each block's LDS copy */
+        std::vector<unsigned char> blob;
+        /* one reservation for every section (no regrowth copies of a 250 MB blob) */
+        blob.reserve(16 * 16 + nodes4.size() * sizeof(float4) + bvh.refs.size() * 4 + tri_geo.size() * sizeof(float4) +
+                     tri_shade.size() * sizeof(float4) + tri_id.size() * 4 + tri_info.size() * sizeof(int4) +
+                     norms.size() * sizeof(float4) + (c->disks.size() + c->spheres.size() + c->materials.size()) * sizeof(float4) +
+                     c->lights.size() * sizeof(LightDev) + (size_t)(bvh.nodes.size() / 16 + 1) * 64 * 2);
+        auto put = [&](const void *src, size_t n) -> size_t {
+            size_t off = (blob.size() + 15) & ~(size_t)15;
+            blob.resize(off + n, 0);
+            if (n) std::memcpy(&blob[off], src, n);
+            return off;
+        };
+        L.o_nodes = put(nodes4.data(), nodes4.size() * sizeof(float4));
+        L.o_refs = put(bvh.refs.data(), bvh.refs.size() * sizeof(uint32_t));
+        L.o_geo = put(tri_geo.data(), tri_geo.size() * sizeof(float4));
+        L.o_shade = put(tri_shade.data(), tri_shade.size() * sizeof(float4));
+        L.o_tid = put(tri_id.data(), tri_id.size() * sizeof(uint32_t));
+        L.o_info = put(tri_info.data(), tri_info.size() * sizeof(int4));
+        L.o_norms = put(norms.data(), norms.size() * sizeof(float4));
+        L.o_disks = put(c->disks.data(), c->disks.size() * sizeof(float4));
+        L.o_spheres = put(c->spheres.data(), c->spheres.size() * sizeof(float4));
+        L.o_mats = put(c->materials.data(), c->materials.size() * sizeof(float4));
+        L.o_lights = put(c->lights.data(), c->lights.size() * sizeof(LightDev));
+        /* scenes traversed from HBM also get the 4-wide BVH (half the dependent
+         * node fetches per ray); env PM_BVH_WIDE=0 keeps the binary traversal,
+         * PM_BVH4_LEAF sets the largest subtree folded into one leaf */
+        if (blob.size() > LDS_SCENE_MAX) {
+            const char *we = getenv("PM_BVH_WIDE");
+            if (!we || atoi(we) != 0) {
+                const char *le = getenv("PM_BVH4_LEAF");
+                Bvh4Out w;
+                const auto t_c0 = tnow();
+                collapse_bvh4(bvh, le ? atoi(le) : 1, w);
+                if (ptimes) fprintf(stderr, "pm_commit: collapse %.1f ms\n", tms(t_c0, tnow()));
+                /* node format fixed at build time (pm_device.h PM_BVH4_QUANT) */
+                std::vector<uint32_t> qn;
+                const bool quant = PM_BVH4_QUANT != 0;
+                const char *lt = getenv("PM_LEAF_TRIS"); /* 0: every leaf through its refs (A/B knob) */
+                /* a leaf the quantized count cannot code (>= LEAF_TRIS primitives,
+                 * possible at build_bvh's depth limit) keeps the binary traversal,
+                 * like a tree whose stack bound exceeds BVH_STACK */
+                /* env PM_NODELETS=N: the pooled trace kernel keeps the first N nodes
+                 * in LDS, the tree renumbered breadth-first so that they are its
+                 * top levels (PM_BVH4_BFS=1 renumbers without nodelets) */
+                const char *nl = getenv("PM_NODELETS"), *bf = getenv("PM_BVH4_BFS");
+                const int nodelets = nl ? std::max(0, atoi(nl)) : 0;
+                if (nodelets > 0 || (bf && atoi(bf) != 0)) bvh4_bfs_order(w.nodes);
+                const auto t_q0 = tnow();
+                const bool coded = !quant || quantize_bvh4(w.nodes, lt && atoi(lt) == 0 ? std::vector<uint32_t>() : bvh.refs, qn);
+                if (ptimes) fprintf(stderr, "pm_commit: quantize %.1f ms\n", tms(t_q0, tnow()));
+                if (coded && w.max_stack <= BVH_STACK) {
+                    L.o_wnodes = quant ? put(qn.data(), qn.size() * sizeof(uint32_t))
+                                       : put(w.nodes.data(), w.nodes.size() * sizeof(float));
+                    L.wide = quant ? 2 : 1;
+                    L.wide_stack = w.max_stack;
+                    L.nodelets = nodelets;
+                    c->bvh4_nodes = (int64_t)(w.nodes.size() / 32);
+                    c->bvh4_depth = w.depth;
+                }
             }
         }
+        blob.resize(std::max<size_t>((blob.size() + 15) & ~(size_t)15, 16), 0);
+        const auto t_u0 = tnow();
+        if ((rc = upload(c, c->d_scene, blob))) return rc;
+        if (ptimes) fprintf(stderr, "pm_commit: upload %.1f ms (%zu bytes), total %.1f ms\n", tms(t_u0, tnow()), blob.size(),
+                            tms(t_commit0, tnow()));
+        L.bytes = blob.size();
+        L.n_nodes = (int64_t)nodes4.size() / 4;
+        L.n_refs = (int64_t)bvh.refs.size();
+        L.n_tris = (int64_t)tri_info.size();
+        L.id_order = id_order;
     }
-    blob.resize(std::max<size_t>((blob.size() + 15) & ~(size_t)15, 16), 0);
-    int rc;
-    const auto t_u0 = tnow();
-    if ((rc = upload(c, c->d_scene, blob))) return rc;
-    if (ptimes) fprintf(stderr, "pm_commit: upload %.1f ms (%zu bytes), total %.1f ms\n", tms(t_u0, tnow()), blob.size(),
-                        tms(t_commit0, tnow()));
 
     SceneDev &S = c->S;
     const char *base = c->d_scene.as<char>();
     S.blob = base;
-    S.blob_bytes = (uint32_t)std::min<size_t>(blob.size(), 0xffffffffu);
-    S.lds_bytes = blob.size() <= LDS_SCENE_MAX ? (uint32_t)blob.size() : 0u;
-    S.nodes = (const float4 *)(base + o_nodes); S.refs = (const uint32_t *)(base + o_refs);
-    S.tri_geo = (const float4 *)(base + o_geo); S.tri_shade = (const float4 *)(base + o_shade);
-    S.tri_id = (const uint32_t *)(base + o_tid); S.tri_info = (const int4 *)(base + o_info);
-    S.norms = (const float4 *)(base + o_norms); S.disks = (const float4 *)(base + o_disks);
-    S.spheres = (const float4 *)(base + o_spheres); S.materials = (const float4 *)(base + o_mats);
-    S.lights = (const LightDev *)(base + o_lights);
-    S.n_lights = (int)c->lights.size(); S.n_nodes = (int)nodes4.size() / 4;
-    S.n_refs = (int)bvh.refs.size();
-    S.n_tris = (int)tri_info.size(); S.n_disks = (int)nd; S.n_spheres = (int)ns;
+    S.blob_bytes = (uint32_t)std::min<size_t>(L.bytes, 0xffffffffu);
+    S.lds_bytes = L.bytes <= LDS_SCENE_MAX ? (uint32_t)L.bytes : 0u;
+    S.nodes = (const float4 *)(base + L.o_nodes); S.refs = (const uint32_t *)(base + L.o_refs);
+    S.tri_geo = (const float4 *)(base + L.o_geo); S.tri_shade = (const float4 *)(base + L.o_shade);
+    S.tri_id = (const uint32_t *)(base + L.o_tid); S.tri_info = (const int4 *)(base + L.o_info);
+    S.norms = (const float4 *)(base + L.o_norms); S.disks = (const float4 *)(base + L.o_disks);
+    S.spheres = (const float4 *)(base + L.o_spheres); S.materials = (const float4 *)(base + L.o_mats);
+    S.lights = (const LightDev *)(base + L.o_lights);
+    S.n_lights = (int)c->lights.size(); S.n_nodes = (int)L.n_nodes;
+    S.n_refs = (int)L.n_refs;
+    S.n_tris = (int)L.n_tris; S.n_disks = (int)nd; S.n_spheres = (int)ns;
     S.tri_geo_g = S.tri_geo; S.tri_id_g = S.tri_id;
-    S.brute = (S.lds_bytes > 0 && id_order) ? 1 : 0;
+    S.brute = (S.lds_bytes > 0 && L.id_order) ? 1 : 0;
     /* a push happens only when descending a level, so depth + 1 entries suffice;
      * sizing the LDS stack by the actual tree keeps occupancy VGPR-bound */
     S.stack_depth = std::min(BVH_STACK, std::max(2, c->bvh_depth + 2));
-    S.wide = wide;
-    S.wnodes = wide ? (const float4 *)(base + o_wnodes) : nullptr;
-    S.nodelets = wide == 2 ? (int)std::min<int64_t>(nodelets, c->bvh4_nodes) : 0;
+    S.wide = L.wide;
+    S.wnodes = L.wide ? (const float4 *)(base + L.o_wnodes) : nullptr;
+    S.nodelets = L.wide == 2 ? (int)std::min<int64_t>(L.nodelets, c->bvh4_nodes) : 0;
     /* wide scenes traverse only the 4-wide tree (traverse() dispatches every
      * MODE_GLOBAL query to traverse4): its exact stack bound sizes the LDS
      * stacks, not the binary tree's depth — k_trace_pool's 256-thread blocks
      * then fit four per CU (its VGPR occupancy) instead of three */
-    if (wide) S.stack_depth = std::min(BVH_STACK, std::max(2, wide_stack + 1));
+    if (L.wide) S.stack_depth = std::min(BVH_STACK, std::max(2, L.wide_stack + 1));
     for (int a = 0; a < 3; ++a) { c->bbox_lo[a] = blo[a]; c->bbox_hi[a] = bhi[a]; }
     double em = 0.0, kd = 1.0;
     for (const LightDev &L : c->lights) {
@@ -1995,6 +2185,31 @@ int pm_scene_info(void *ptr, int64_t out[7]) {
     out[0] = S.n_tris; out[1] = S.n_disks; out[2] = S.n_spheres; out[3] = S.n_nodes; out[4] = c->bvh_depth;
     out[5] = scene_mode(S) == MODE_BRUTE ? 2 : scene_mode(S) == MODE_LDS ? 1 : 0;
     out[6] = S.blob_bytes;
+    return PM_OK;
+}
+
+int pm_scene_section(void *ptr, int section, void *out, int64_t max_bytes, int64_t *bytes) {
+    if (Group *g_ = group_of(ptr)) return pm_scene_section(g_->subs[0], section, out, max_bytes, bytes);
+    GETCTX(ptr);
+    if (!c->S.blob) FAIL(c, PM_ERR_INVALID, "no scene committed");
+    const SceneDev &S = c->S;
+    const void *src = nullptr;
+    int64_t n = 0;
+    switch (section) {
+    case PM_SCENE_REFS: src = S.refs; n = 4 * (int64_t)S.n_refs; break;
+    case PM_SCENE_TRI_GEO: src = S.tri_geo; n = 48 * (int64_t)S.n_tris; break;
+    case PM_SCENE_TRI_SHADE: src = S.tri_shade; n = 32 * (int64_t)S.n_tris; break;
+    case PM_SCENE_TRI_ID: src = S.tri_id; n = 4 * (int64_t)S.n_tris; break;
+    case PM_SCENE_TRI_INFO: src = S.tri_info; n = 16 * (int64_t)S.n_tris; break;
+    case PM_SCENE_BVH4: src = S.wnodes; n = S.wide ? (S.wide == 2 ? 64 : 128) * c->bvh4_nodes : 0; break;
+    default: FAIL(c, PM_ERR_INVALID, "unknown scene section %d", section);
+    }
+    if (bytes) *bytes = n;
+    if (out && n > 0) {
+        if (max_bytes < n) FAIL(c, PM_ERR_INVALID, "scene section needs %lld bytes", (long long)n);
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipMemcpy(out, src, (size_t)n, hipMemcpyDeviceToHost));
+    }
     return PM_OK;
 }
 

@@ -550,6 +550,196 @@ void build_bvh(std::vector<BuildPrim> &prims, int max_depth, BvhOut &out, const 
     for (size_t i = 0; i < prims.size(); ++i) out.refs[i] = prims[i].ref;
 }
 
+/* ------------------------------------------------------------------ PLOC */
+void ploc_morton_frame(const std::vector<BuildPrim> &prims, float lo[3], float scale[3]) {
+    float hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int a = 0; a < 3; ++a) lo[a] = INFINITY;
+    for (const BuildPrim &p : prims)
+        for (int a = 0; a < 3; ++a) {
+            const float c = centroid(p, a);
+            lo[a] = std::min(lo[a], c); hi[a] = std::max(hi[a], c);
+        }
+    for (int a = 0; a < 3; ++a) {
+        if (!(lo[a] <= hi[a])) lo[a] = hi[a] = 0.f;
+        const float ext = hi[a] - lo[a];
+        scale[a] = ext > 0.f ? 1024.f / ext : 0.f;
+    }
+}
+static inline uint32_t expand10(uint32_t v) { /* 10 bits -> every third bit */
+    v = (v | (v << 16)) & 0x030000ffu;
+    v = (v | (v << 8)) & 0x0300f00fu;
+    v = (v | (v << 4)) & 0x030c30c3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+uint32_t ploc_morton(const BuildPrim &p, const float lo[3], const float scale[3]) {
+    uint32_t q[3];
+    for (int a = 0; a < 3; ++a) {
+        const float u = (centroid(p, a) - lo[a]) * scale[a];
+        q[a] = u >= 1023.f ? 1023u : u > 0.f ? (uint32_t)u : 0u;
+    }
+    return (expand10(q[0]) << 2) | (expand10(q[1]) << 1) | expand10(q[2]);
+}
+
+namespace {
+struct PBox { float lo[3], hi[3]; };
+inline float union_area(const PBox &a, const PBox &b) {
+    const float dx = std::max(a.hi[0], b.hi[0]) - std::min(a.lo[0], b.lo[0]);
+    const float dy = std::max(a.hi[1], b.hi[1]) - std::min(a.lo[1], b.lo[1]);
+    const float dz = std::max(a.hi[2], b.hi[2]) - std::min(a.lo[2], b.lo[2]);
+    return dx * dy + dy * dz + dz * dx;
+}
+} // namespace
+
+void build_ploc(const std::vector<BuildPrim> &prims, int radius, PlocTree &t) {
+    const int n = (int)prims.size();
+    t = PlocTree();
+    if (n == 0) return;
+    radius = std::max(1, radius);
+    ploc_morton_frame(prims, t.frame_lo, t.frame_scale);
+    std::vector<uint64_t> keys((size_t)n);
+    parallel_for(n, [&](int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i)
+            keys[i] = ((uint64_t)ploc_morton(prims[i], t.frame_lo, t.frame_scale) << 32) | (uint64_t)i;
+    });
+    std::sort(keys.begin(), keys.end());
+    t.order.resize((size_t)n);
+    for (int i = 0; i < n; ++i) t.order[i] = (uint32_t)(keys[i] & 0xffffffffu);
+    t.left.resize((size_t)std::max(0, n - 1));
+    t.right.resize((size_t)std::max(0, n - 1));
+    t.box.resize((size_t)std::max(0, n - 1) * 6);
+    std::vector<int> id((size_t)n), nid((size_t)n), nn((size_t)n);
+    std::vector<PBox> box((size_t)n), nbox((size_t)n);
+    for (int i = 0; i < n; ++i) {
+        const BuildPrim &p = prims[t.order[i]];
+        id[i] = i;
+        for (int a = 0; a < 3; ++a) { box[i].lo[a] = p.lo[a]; box[i].hi[a] = p.hi[a]; }
+    }
+    int nc = n, created = 0;
+    while (nc > 1) {
+        parallel_for(nc, [&](int64_t i0, int64_t i1) {
+            for (int64_t i = i0; i < i1; ++i) {
+                const int j0 = (int)std::max<int64_t>(0, i - radius), j1 = (int)std::min<int64_t>(nc - 1, i + radius);
+                float best = INFINITY;
+                int bj = -1;
+                for (int j = j0; j <= j1; ++j) {
+                    if (j == i) continue;
+                    const float a = union_area(box[i], box[j]);
+                    if (bj < 0 || a < best) { best = a; bj = j; }
+                }
+                nn[i] = bj;
+            }
+        }, 1 << 12);
+        int m = 0;
+        for (int i = 0; i < nc; ++i) {
+            const int j = nn[i];
+            const bool mutual = nn[j] == i;
+            if (mutual && i > j) continue; /* merged into cluster j */
+            if (mutual) {
+                const int k = created++;
+                t.left[k] = id[i]; t.right[k] = id[j];
+                PBox u;
+                for (int a = 0; a < 3; ++a) {
+                    u.lo[a] = std::min(box[i].lo[a], box[j].lo[a]);
+                    u.hi[a] = std::max(box[i].hi[a], box[j].hi[a]);
+                }
+                std::memcpy(&t.box[(size_t)k * 6], &u, sizeof(u));
+                nid[m] = n + k; nbox[m] = u;
+            } else {
+                nid[m] = id[i]; nbox[m] = box[i];
+            }
+            ++m;
+        }
+        id.swap(nid);
+        box.swap(nbox);
+        nc = m;
+        ++t.rounds;
+    }
+    t.root = id[0];
+}
+
+void ploc_to_bvh(const std::vector<BuildPrim> &prims, const PlocTree &t, BvhOut &out) {
+    out.nodes.clear();
+    out.refs.clear();
+    const int n = (int)prims.size();
+    Box empty;
+    auto leaf_box = [&](int p) {
+        Box b;
+        b.grow(prims[t.order[p]].lo, prims[t.order[p]].hi);
+        return b;
+    };
+    auto node_box = [&](int id) {
+        if (id < n) return leaf_box(id);
+        Box b;
+        b.grow(&t.box[(size_t)(id - n) * 6], &t.box[(size_t)(id - n) * 6 + 3]);
+        return b;
+    };
+    auto write = [&](int at, const Box &lb, int lc, int lcnt, const Box &rb, int rc, int rcnt) {
+        float *nd = &out.nodes[(size_t)at * 16];
+        for (int a = 0; a < 3; ++a) { nd[a] = lb.lo[a]; nd[3 + a] = lb.hi[a]; nd[6 + a] = rb.lo[a]; nd[9 + a] = rb.hi[a]; }
+        int ints[4] = {lc, rc, lcnt, rcnt};
+        std::memcpy(&nd[12], ints, sizeof(ints));
+    };
+    if (n <= 1) {
+        out.nodes.assign(16, 0.f);
+        if (n == 0) write(0, empty, ~0, -1, empty, ~0, -1);
+        else write(0, leaf_box(0), ~0, 1, empty, ~0, -1);
+        out.depth = 1;
+    } else {
+        /* breadth-first over the internal nodes from the root */
+        std::vector<int> q;
+        q.reserve((size_t)n - 1);
+        q.push_back(t.root);
+        std::vector<int> level(1, 0);
+        out.nodes.assign((size_t)(n - 1) * 16, 0.f);
+        int depth = 0;
+        for (size_t h = 0; h < q.size(); ++h) {
+            const int k = q[h] - n, lv = level[h];
+            depth = std::max(depth, lv + 1);
+            const int ch[2] = {t.left[k], t.right[k]};
+            int code[2], cnt[2];
+            for (int s = 0; s < 2; ++s) {
+                if (ch[s] < n) { code[s] = ~ch[s]; cnt[s] = 1; }
+                else { code[s] = (int)q.size(); cnt[s] = 0; q.push_back(ch[s]); level.push_back(lv + 1); }
+            }
+            write((int)h, node_box(ch[0]), code[0], cnt[0], node_box(ch[1]), code[1], cnt[1]);
+        }
+        out.depth = depth;
+    }
+    out.refs.resize((size_t)n);
+    for (int p = 0; p < n; ++p) out.refs[p] = prims[t.order[p]].ref;
+}
+
+double bvh4_sah_cost(const std::vector<float> &nodes, double c_node, double c_prim) {
+    const size_t nn = nodes.size() / 32;
+    if (nn == 0) return 0.0;
+    auto area = [](double dx, double dy, double dz) { return dx < 0 || dy < 0 || dz < 0 ? 0.0 : dx * dy + dy * dz + dz * dx; };
+    double root = 0.0, total = 0.0;
+    {
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int k = 0; k < 4; ++k) {
+            int cnt;
+            std::memcpy(&cnt, &nodes[28 + k], 4);
+            if (cnt == -1) continue;
+            for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], (double)nodes[4 * a + k]); hi[a] = std::max(hi[a], (double)nodes[4 * (3 + a) + k]); }
+        }
+        root = area(hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]);
+    }
+    if (root <= 0.0) return 0.0;
+    total = c_node * root;
+    for (size_t i = 0; i < nn; ++i) {
+        const float *nd = &nodes[i * 32];
+        for (int k = 0; k < 4; ++k) {
+            int cnt;
+            std::memcpy(&cnt, &nd[28 + k], 4);
+            if (cnt == -1) continue;
+            const double a = area((double)nd[12 + k] - nd[k], (double)nd[16 + k] - nd[4 + k], (double)nd[20 + k] - nd[8 + k]);
+            total += cnt == 0 ? c_node * a : c_prim * a * cnt;
+        }
+    }
+    return total / root;
+}
+
 int64_t build_kdtree_pbrt(const pm_photon *slots, int64_t nslots, std::vector<pm_photon> &nodes) {
     std::vector<pm_photon> ph;
     ph.reserve((size_t)nslots);

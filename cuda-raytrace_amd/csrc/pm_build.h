@@ -84,6 +84,39 @@ constexpr int LEAF_TRIS = 0x4000;
 void bvh4_bfs_order(std::vector<float> &nodes);
 bool quantize_bvh4(const std::vector<float> &nodes, const std::vector<uint32_t> &refs, std::vector<uint32_t> &q);
 
+/* PLOC (parallel locally-ordered clustering, Meister & Bittner 2018), the
+ * GPU builder's algorithm (pm_bvh_gpu.hip) restated on the host — the
+ * device tree's test oracle and the A/B path of PM_BVH_BUILD=ploc-host.
+ *  1. primitives sorted by the 30-bit Morton code of their box centroid in
+ *     the centroid bounds (ploc_morton: q = (c - lo) * scale per axis, scale =
+ *     1024 / extent, clamped to 1023), ties by primitive index;
+ *  2. rounds over the cluster list (initially the sorted leaves): every
+ *     cluster takes as nearest neighbour the cluster within `radius` list
+ *     positions whose union box has the smallest surface area (ties: the
+ *     lower position — a strict order on pairs, so the global minimum pair
+ *     is always mutual); mutual pairs merge into a new internal node at the
+ *     lower position (ids in creation order: n + k, ranked by position
+ *     within a round), the higher one leaves, the list keeps its order.
+ * Leaf ids are Morton positions p (< n), internal ids n + k; the root is
+ * the last node created. */
+struct PlocTree {
+    std::vector<uint32_t> order;  /* primitive index at Morton position p */
+    std::vector<int32_t> left, right;
+    std::vector<float> box;       /* internal node k: lo[3] hi[3] */
+    int root = -1;                /* node id (-1: no primitives) */
+    int rounds = 0;
+    float frame_lo[3] = {0, 0, 0}, frame_scale[3] = {0, 0, 0};
+};
+void ploc_morton_frame(const std::vector<BuildPrim> &prims, float lo[3], float scale[3]);
+uint32_t ploc_morton(const BuildPrim &p, const float lo[3], const float scale[3]);
+void build_ploc(const std::vector<BuildPrim> &prims, int radius, PlocTree &t);
+/* the PLOC tree in build_bvh's layout (breadth-first, root 0, leaves of one
+ * primitive at Morton positions, refs in Morton order) */
+void ploc_to_bvh(const std::vector<BuildPrim> &prims, const PlocTree &t, BvhOut &out);
+/* surface-area cost of a 4-wide tree (pm_build.h node layout): sum over
+ * nodes of area(node box) * c_node + over leaves area * prims, / root area */
+double bvh4_sah_cost(const std::vector<float> &nodes, double c_node = 1.0, double c_prim = 1.0);
+
 /* returns the number of nodes (= valid photons); nodes sized >= that */
 int64_t build_kdtree_pbrt(const pm_photon *slots, int64_t nslots, std::vector<pm_photon> &nodes);
 

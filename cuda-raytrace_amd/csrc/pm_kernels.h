@@ -241,4 +241,31 @@ hipError_t launch_record_view(const RecordsDev &R, uint32_t *flags, uint32_t *ra
                               hipStream_t s);
 hipError_t launch_reset_records(const RecordsDev &R, float r2init, hipStream_t s);
 
+/* scene BVH on the device (pm_bvh_gpu.hip): PLOC over the primitive boxes
+ * (box: 2 float4 per primitive, (lo.xyz, ref bits) (hi.xyz, 0); Morton frame
+ * of pm_build.h ploc_morton_frame), collapsed into quantized 4-wide nodes —
+ * the tree pm_build.h build_ploc + ploc_to_bvh + collapse_bvh4 +
+ * bvh4_bfs_order + quantize_bvh4 produce on the host, bit for bit. Outputs:
+ * wnodes (<= max_nodes nodes of 4 uint4, breadth-first), refs (n, Morton
+ * order; triangles as PRIM_TRI << 30 | storage slot) and tri_order (storage
+ * slot -> triangle id, triangles in Morton order). Blocks on the stream. */
+struct GpuBvhIn {
+    const float4 *box;
+    int n;
+    float frame_lo[3], frame_scale[3];
+    int radius;
+};
+struct GpuBvhOut {
+    uint4 *wnodes;
+    uint32_t *refs, *tri_order;
+    int64_t max_nodes;
+    int64_t nodes = 0, n_tris = 0;
+    int depth = 0, max_stack = 0, rounds = 0;
+};
+hipError_t gpu_bvh_build(const GpuBvhIn &in, GpuBvhOut &out, hipStream_t s);
+/* triangle records computed in triangle-id order -> storage order */
+hipError_t launch_tri_permute(const uint32_t *tri_order, int64_t nst, const float4 *src_geo, const float4 *src_shade,
+                              const int4 *src_info, float4 *geo, float4 *shade, uint32_t *tid, int4 *info,
+                              hipStream_t s);
+
 } // namespace pm

@@ -78,6 +78,7 @@ def load_library(path=None):
         "pm_gather_counters": (c_int, [vp, ctypes.POINTER(i64)]),
         "pm_trace_counters": (c_int, [vp, ctypes.POINTER(i64)]),
         "pm_scene_info": (c_int, [vp, ctypes.POINTER(i64)]),
+        "pm_scene_section": (c_int, [vp, c_int, vp, i64, ctypes.POINTER(i64)]),
         "pm_map_info": (c_int, [vp, ctypes.POINTER(i64)]),
         "pm_trace_profile": (c_int, [vp, ctypes.POINTER(i64), c_int]),
         "pm_set_counting": (c_int, [vp, c_int]),
@@ -376,6 +377,19 @@ class Context:
         v = [int(x) for x in out]
         return {"triangles": v[0], "disks": v[1], "spheres": v[2], "bvh_nodes": v[3], "bvh_depth": v[4],
                 "mode": ("bvh-hbm", "bvh-lds", "brute")[v[5]], "bytes": v[6]}
+
+    SCENE_SECTIONS = {"refs": (0, np.uint32), "tri_geo": (1, np.float32), "tri_shade": (2, np.float32),
+                      "tri_id": (3, np.uint32), "tri_info": (4, np.int32), "bvh4": (5, np.uint32)}
+
+    def scene_section(self, name):
+        """One section of the committed scene blob as the kernels read it (pm_scene_section)."""
+        sec, dt = self.SCENE_SECTIONS[name]
+        n = ctypes.c_int64()
+        self._chk(self.lib.pm_scene_section(self.h, sec, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value // 4, dtype=dt)
+        if n.value:
+            self._chk(self.lib.pm_scene_section(self.h, sec, out.ctypes.data, n.value, ctypes.byref(n)))
+        return out
 
     def map_info(self):
         """dict: structure (PM_GATHER_*, -1 none), valid photons, slots, grid cells of the current photon map."""

@@ -301,6 +301,18 @@ int pm_trace_counters(void *ctx, int64_t out[4]);
  * [2] spheres, [3] BVH nodes, [4] BVH depth, [5] traversal mode (0 BVH in
  * HBM, 1 BVH in LDS, 2 brute force over an LDS-sized scene), [6] scene bytes */
 int pm_scene_info(void *ctx, int64_t out[7]);
+/* diagnostics: one section of the committed scene as the kernels read it
+ * (refs; per storage slot the triangle records geo 48 B, shade 32 B, id,
+ * info 16 B; the 4-wide nodes, 64 B quantized or 128 B float). *bytes = its
+ * size; out may be null to query it, else max_bytes must hold it. Lets a
+ * test compare the device-built tree with its host restatement. */
+#define PM_SCENE_REFS 0
+#define PM_SCENE_TRI_GEO 1
+#define PM_SCENE_TRI_SHADE 2
+#define PM_SCENE_TRI_ID 3
+#define PM_SCENE_TRI_INFO 4
+#define PM_SCENE_BVH4 5
+int pm_scene_section(void *ctx, int section, void *out, int64_t max_bytes, int64_t *bytes);
 /* the current photon map (pm_build_photon_map; the reference's
  * CreatePhotonMap, photonmappingrenderer.cpp:150-180): [0] structure
  * (PM_GATHER_GRID / PM_GATHER_KDTREE, -1 none), [1] valid photons in it,

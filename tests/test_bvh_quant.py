@@ -42,3 +42,23 @@ def test_threaded_build_is_the_serial_tree(tmp_path):
         assert r.returncode == 0, r.stderr
         outs.append(r.stdout.strip())
     assert outs[0] == outs[1] and "hash" in outs[0]
+
+
+@pytest.mark.parametrize("radius", ["1", "3", "8"])
+def test_ploc_host_tree_is_valid_and_thread_independent(tmp_path, radius):
+    """pm_build.cpp build_ploc (the device builder's host restatement,
+    csrc/pm_bvh_gpu.hip): a valid binary tree over every primitive in Morton
+    order, internal boxes the exact unions of their children, the 4-wide
+    collapse quantizable — and the same tree for 1 and 4 threads (only the
+    nearest-neighbour search runs in parallel)."""
+    exe = tmp_path / "pcheck"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-ffp-contract=off", "-I", CSRC, "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "native", "ploc_check.cpp"), os.path.join(CSRC, "pm_build.cpp"),
+                    "-o", str(exe)], check=True, timeout=300)
+    outs = []
+    for t in ("1", "4"):
+        r = subprocess.run([str(exe), "60000", radius], capture_output=True, text=True, timeout=300,
+                           env={**os.environ, "PM_BUILD_THREADS": t})
+        assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
+        outs.append(r.stdout.strip())
+    assert outs[0] == outs[1]
