@@ -90,7 +90,7 @@ struct Ctx {
     int64_t slots_used = 0;
     /* photon buckets */
     DevBuf d_count, d_cell_start, d_scratch, d_pha, d_phb;
-    struct { bool valid = false; int64_t n = 0; GridDesc grid{}; float r2 = 0.f; } fused; /* counts made by the last trace */
+    struct { bool valid = false; int64_t n = 0; GridDesc grid{}; float r2 = 0.f; int64_t key_np = 0; int mpc = 1; } fused; /* counts made by the last trace (keys plane-major when key_np > 0) */
     GridDesc grid{};
     float grid_r2 = 0.f; /* radius^2 the photon map's grid is designed for */
     int64_t bvh4_nodes = 0; /* 4-wide BVH of an HBM scene (0: binary traversal) */
@@ -132,6 +132,7 @@ struct Ctx {
     bool path_sort = false;         /* pooled kernel: paths by first-ray direction (env PM_PATH_SORT=1) */
     DevBuf d_porder, d_pscratch;
     int64_t pool_waves = 0;         /* pooled kernel: waves per launch (env PM_POOL_WAVES; 0 = one occupancy round) */
+    bool key_planes = true;         /* fused bucket keys / ranks plane-major (env PM_KEY_PLANES) */
     int gather_kernel = PM_GK_TILE; /* bucket gather kernel (env PM_GATHER_KERNEL=tile|lane|wave) */
     bool gather_xcd = false;        /* tile gather: contiguous tile ranges per XCD (env PM_GATHER_XCD=1) */
     int cell_span = 2;              /* PPM grid: cells per axis of a query box (env PM_CELL_SPAN 2..5) */
@@ -755,6 +756,7 @@ int pm_create(void **out, const pm_config *cfg) {
     if (const char *e = getenv("PM_TRACE_HOLD")) c->trace_hold = atoi(e) != 0;
     if (const char *e = getenv("PM_PATH_SORT")) c->path_sort = atoi(e) != 0;
     if (const char *e = getenv("PM_POOL_WAVES")) c->pool_waves = std::max(1LL, atoll(e));
+    if (const char *e = getenv("PM_KEY_PLANES")) c->key_planes = atoi(e) != 0;
     if (const char *e = getenv("PM_TILE_LIST")) c->tile_list = atoi(e) != 0;
     if (const char *e = getenv("PM_KD_STACK")) c->kd_stack = std::max(1, std::min(KD_STACK, atoi(e)));
     if (const char *e = getenv("PM_STAGE_TIMERS")) if (atoi(e) == 0) c->timed_stages.clear();
@@ -1433,6 +1435,9 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
         T.count = c->d_count.as<uint32_t>();
         T.key = c->d_scratch.as<uint32_t>();
         T.rank = c->d_scratch.as<uint32_t>() + end_slot;
+        /* plane-major keys / ranks (env PM_KEY_PLANES=0: slot order); the held
+         * deposits write a path's four keys as one 16-B store in slot order */
+        T.key_np = c->key_planes && !T.hold ? path_count : 0;
     }
     if (c->path_sort && T.pool_paths > 0 && c->S.wide) {
         HIPCHK(c, c->d_porder.ensure((size_t)path_count * 4));
@@ -1444,7 +1449,7 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
     /* the kernel writes all path_count * mpc slots: deposits, then zeros */
     HIPCHK(c, launch_trace(T, c->counting, s));
     timer_end(c, "trace", s);
-    if (fuse) { c->fused.valid = true; c->fused.n = end_slot; c->fused.grid = T.grid; c->count_zero_words = 0; }
+    if (fuse) { c->fused.valid = true; c->fused.n = end_slot; c->fused.grid = T.grid; c->fused.key_np = T.key_np; c->fused.mpc = (int)mpc; c->count_zero_words = 0; }
     /* traced photons carry the scene's signs (scene_nonneg); slots outside
      * the traced range keep theirs, so the flag is reset only when this
      * trace rewrote every slot in use */
@@ -1497,7 +1502,7 @@ int pm_build_photon_map(void *ptr, const pm_render_params *p, int64_t n_slots, v
     timer_begin(c, "build", s);
     HIPCHK(c, launch_bucket_build(c->d_slots.as<pm_photon>(), n_slots, g, c->d_count.as<uint32_t>(),
                                   c->d_cell_start.as<uint32_t>(), c->d_scratch.as<uint32_t>(), c->d_pha.as<float4>(),
-                                  c->d_phb.as<float4>(), counted, s));
+                                  c->d_phb.as<float4>(), counted, s, counted ? c->fused.key_np : 0, c->fused.mpc));
     /* the scan left the counters zeroed */
     c->count_zero_words = (size_t)g.ncells + 1;
     c->count_zero_ptr = c->d_count.p;

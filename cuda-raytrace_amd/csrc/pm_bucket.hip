@@ -160,12 +160,14 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_down(const uint32_t *in, in
 
 __global__ __launch_bounds__(256) void k_bucket_fill(const pm_photon *slots, int64_t n, const uint32_t *key,
                                                      const uint32_t *rank, const uint32_t *cell_start, float4 *ph_a,
-                                                     float4 *ph_b) {
+                                                     float4 *ph_b, int64_t key_np, int mpc) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    const uint32_t k = key[i];
+    /* keys / ranks of the trace's fused count may be plane-major (TraceParams::key_np) */
+    const int64_t ki = key_np > 0 ? (i % mpc) * key_np + i / mpc : i;
+    const uint32_t k = key[ki];
     if (k == 0xffffffffu) return;
-    const uint32_t dst = cell_start[k] + rank[i];
+    const uint32_t dst = cell_start[k] + rank[ki];
     const float2 *q = reinterpret_cast<const float2 *>(slots + i);
     const float2 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4];
     /* a = (bits, p.x) b = (p.y, p.z) c = (alpha.x, alpha.y) d = (alpha.z, wi.x) e = (wi.y, wi.z) */
@@ -200,7 +202,9 @@ size_t bucket_scratch_words(int64_t n_slots, uint32_t ncells) {
 }
 
 hipError_t launch_bucket_build(const pm_photon *slots, int64_t n, GridDesc g, uint32_t *count, uint32_t *cell_start,
-                               uint32_t *scratch, float4 *ph_a, float4 *ph_b, bool counted, hipStream_t s) {
+                               uint32_t *scratch, float4 *ph_a, float4 *ph_b, bool counted, hipStream_t s,
+                               int64_t key_np, int mpc) {
+    if (!counted || key_np * mpc != n) key_np = 0; /* k_bucket_count writes slot order */
     const int64_t nc = (int64_t)g.ncells + 1; /* last counter stays 0 -> cell_start[ncells] = total */
     uint32_t *key = scratch, *rank = scratch + n, *sums = scratch + 2 * n;
     if (n > 0 && !counted)
@@ -212,7 +216,7 @@ hipError_t launch_bucket_build(const pm_photon *slots, int64_t n, GridDesc g, ui
     pm_launch(k_scan_down, dim3(ntile), dim3(SCAN_BLOCK), 0, s, count, nc, sums, cell_start, count);
     if (n > 0)
         pm_launch(k_bucket_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slots, n, key, rank,
-                           cell_start, ph_a, ph_b);
+                           cell_start, ph_a, ph_b, key_np, mpc > 0 ? mpc : 1);
     return hipGetLastError();
 }
 

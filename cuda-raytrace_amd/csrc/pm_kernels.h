@@ -106,6 +106,8 @@ struct TraceParams {
      * written once per path (pm_trace.hip Held; used when mpc == 4 and the
      * slot buffer is 16-B aligned) */
     int hold;
+    /* fused counting: keys / ranks plane-major (deposit k of path i at k * key_np + i) when > 0, else at the slot index */
+    int64_t key_np;
 };
 
 struct GatherParams {
@@ -212,7 +214,8 @@ hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s);
  * otherwise count must arrive zeroed. count leaves zeroed (cleared by the scan). */
 size_t bucket_scratch_words(int64_t n_slots, uint32_t ncells);
 hipError_t launch_bucket_build(const pm_photon *slots, int64_t n, GridDesc g, uint32_t *count, uint32_t *cell_start,
-                               uint32_t *scratch, float4 *ph_a, float4 *ph_b, bool counted, hipStream_t s);
+                               uint32_t *scratch, float4 *ph_a, float4 *ph_b, bool counted, hipStream_t s,
+                               int64_t key_np = 0, int mpc = 1);
 /* gather: structure 0 grid, 1 kd; mode 0 fused PPM, 1 partial */
 hipError_t launch_gather(const GatherParams &p, int structure, int partial, int count, hipStream_t s);
 /* kNN estimator (pbrt LPhoton) over the photon buckets, fused record update */

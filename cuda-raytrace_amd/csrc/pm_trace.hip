@@ -260,6 +260,14 @@ struct PathState {
     uint32_t prank;
 };
 constexpr uint32_t PSLOT_NONE = 0xffffffffu;
+/* where the fused bucket count keeps deposit k of path pid: plane-major
+ * (k * key_np + path) when key_np > 0, so that the lanes of a wave — paths
+ * next to each other — store their keys and ranks into the same lines
+ * instead of one 4-B store per 16-B path block; else the slot index */
+PMD size_t key_index(const TraceParams &P, uint32_t pid, uint32_t k) {
+    const size_t path = (size_t)(pid - (uint64_t)P.slot_path_base);
+    return P.key_np > 0 ? (size_t)k * (size_t)P.key_np + path : path * (size_t)P.mpc + k;
+}
 PMD void flush_rank(const TraceParams &P, PathState &st) {
     if (st.pslot != PSLOT_NONE) { P.rank[st.pslot] = st.prank; st.pslot = PSLOT_NONE; }
 }
@@ -422,9 +430,10 @@ PMD bool path_shade(const TraceParams &P, const SceneDev &S, PathState &st, cons
             key = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx + cx;
             rank = atomicAdd(&P.count[key], 1u);
             if (!HOLD) {
-                P.key[slot] = key;
+                const size_t ki = key_index(P, st.pid, st.nI - 1);
+                P.key[ki] = key;
                 flush_rank(P, st);
-                st.prank = rank; st.pslot = (uint32_t)slot;
+                st.prank = rank; st.pslot = (uint32_t)ki;
             }
         }
         /* HOLD: the returned rank is first read at the path's end */
@@ -459,7 +468,7 @@ PMD void finish_path(const TraceParams &P, PathState &st, const Held *held = nul
     for (uint32_t k = st.stored; k < mpc; ++k) {
         float2 *q = reinterpret_cast<float2 *>(slots + k);
         q[0] = z; q[1] = z; q[2] = z; q[3] = z; q[4] = z;
-        if (P.bucket) P.key[(size_t)(st.pid - (uint64_t)P.slot_path_base) * mpc + k] = 0xffffffffu;
+        if (P.bucket) P.key[key_index(P, st.pid, k)] = 0xffffffffu;
     }
 }
 
@@ -646,7 +655,10 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
 #ifndef PM_POOL_SHADE_MIN
 #define PM_POOL_SHADE_MIN 16
 #endif
-constexpr int POOL_STEPS = 4, POOL_SHADE_MIN = PM_POOL_SHADE_MIN;
+#ifndef PM_POOL_STEPS
+#define PM_POOL_STEPS 4
+#endif
+constexpr int POOL_STEPS = PM_POOL_STEPS, POOL_SHADE_MIN = PM_POOL_SHADE_MIN;
 enum { PHASE_DEAD = 0, PHASE_TRAV = 1, PHASE_SHADE = 2 };
 
 template <int COUNT, int HOLD>
