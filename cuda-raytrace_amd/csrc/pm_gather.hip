@@ -236,11 +236,25 @@ __global__ __launch_bounds__(GATHER_BLOCK, 8) void k_gather_grid(GatherParams P)
 #define PM_TILE_CAP 128
 #endif
 constexpr int TILE_CAP = PM_TILE_CAP; /* photons per LDS window (two per lane) */
+/* PM_TILE_PAIRS (default): positions stored by aligned pairs, 32 B per pair
+ * (x0 x1 y0 y1 | z0 z1 . .), so a pair test reads one ds_read_b128 and one
+ * ds_read_b64 at immediate offsets (no per-pair address arithmetic) straight
+ * into the register pairs of the packed math; runs start at even positions
+ * (an odd start masks its first bit). 0: SoA x / y / z with ds_read2. */
+#ifndef PM_TILE_PAIRS
+#define PM_TILE_PAIRS 1
+#endif
 struct TileLds {
+#if PM_TILE_PAIRS
+    /* TILE_CAP + 2 pairs: a run's aligned pairs reach at most one pair past
+     * 2 x TILE_CAP positions' half (lanes beyond their run, masked) */
+    float4 pr[2 * (TILE_CAP + 2)];
+#else
     /* positions SoA, so that a pair of neighbouring photons is one ds_read2;
      * 2 x TILE_CAP entries: the test loop reads up to TILE_CAP past a run's
      * start (lanes beyond their run) without wrapping the index */
     float x[2 * TILE_CAP], y[2 * TILE_CAP], z[2 * TILE_CAP];
+#endif
     float4 b[TILE_CAP]; /* alpha.rgb, wi.y */
     float w[TILE_CAP];  /* wi.x */
     float c[TILE_CAP];  /* wi.z */
@@ -449,6 +463,7 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
     R.shade(P);
     const v3 fvs = R.fv * sc;
     const f2 px2 = {R.p.x, R.p.x}, py2 = {R.p.y, R.p.y}, pz2 = {R.p.z, R.p.z};
+    const f2 r2v = {R.r2, R.r2};
     /* Groups: the first pending lane leads; every pending lane whose box
      * starts within GR cells of the leader's on each axis joins. A group's
      * union box is at most (2 GR + KR)^3 cells (<= 8 x 8 rows), so it always
@@ -532,6 +547,33 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
                 else if (pre < T0 && pre + len > T0) T.mark[0] = lane; /* row running into the window */
             }
             wave_lds_sync();
+            const float *phb = reinterpret_cast<const float *>(P.ph_b);
+#if PM_TILE_PAIRS
+            static_assert(H == 2, "paired staging: two positions per lane");
+            {
+                /* lane l stages positions 2 l and 2 l + 1, a whole pair: one
+                 * 16-B and one 8-B LDS write instead of three scattered words
+                 * per position (bank conflicts) */
+                const int2 m2 = *reinterpret_cast<const int2 *>(&T.mark[2 * lane]);
+                const int incl = wave_incl_max_i32(max(m2.x, m2.y));
+                const int prev = __shfl(incl, (lane + 63) & 63);
+                const int u0 = max(lane == 0 ? -1 : prev, m2.x), u1 = incl;
+                const uint32_t q0 = 2u * (uint32_t)lane;
+                const uint32_t gi0 = T0 + q0 + (uint32_t)__shfl((int)gofs, u0);
+                const uint32_t gi1 = T0 + q0 + 1u + (uint32_t)__shfl((int)gofs, u1);
+                /* positions at or beyond n re-read position 0's photon (n >= 1) and are never read */
+                const uint32_t g0 = (uint32_t)__builtin_amdgcn_readlane((int)gi0, 0);
+                const uint32_t j0 = q0 < n ? gi0 : g0, j1 = q0 + 1u < n ? gi1 : g0;
+                const float4 pa0 = P.ph_a[j0], pa1 = P.ph_a[j1];
+                const float4 qa0 = P.ph_b[2 * (size_t)j0], qa1 = P.ph_b[2 * (size_t)j1];
+                const float ca0 = phb[8 * (size_t)j0 + 4], ca1 = phb[8 * (size_t)j1 + 4];
+                T.pr[2 * lane] = make_float4(pa0.x, pa1.x, pa0.y, pa1.y);
+                *reinterpret_cast<f2 *>(&T.pr[2 * lane + 1]) = f2{pa0.z, pa1.z};
+                *reinterpret_cast<f2 *>(&T.w[q0]) = f2{pa0.w, pa1.w};
+                T.b[q0] = qa0; T.b[q0 + 1] = qa1;
+                *reinterpret_cast<f2 *>(&T.c[q0]) = f2{ca0, ca1};
+            }
+#else
             int u[H];
             u[0] = wave_incl_max_i32(T.mark[lane]);
             if (H == 2) u[H - 1] = max(wave_incl_max_i32(T.mark[lane + 64 * (H - 1)]), __builtin_amdgcn_readlane(u[0], 63));
@@ -540,7 +582,6 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
             for (int h = 0; h < H; ++h) gi[h] = T0 + 64u * h + (uint32_t)lane + (uint32_t)__shfl((int)gofs, u[h]);
             /* every load in flight, then the LDS writes; positions at or beyond
              * n re-read position 0's photon (n >= 1) and are never read */
-            const float *phb = reinterpret_cast<const float *>(P.ph_b);
             const uint32_t g0 = (uint32_t)__builtin_amdgcn_readlane((int)gi[0], 0);
             float4 pa[H], qa[H];
             float ca[H];
@@ -552,15 +593,48 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
 #pragma unroll
             for (int h = 0; h < H; ++h) {
                 const int q = lane + 64 * h;
-                T.x[q] = pa[h].x; T.y[q] = pa[h].y; T.z[q] = pa[h].z; T.w[q] = pa[h].w;
+                T.x[q] = pa[h].x; T.y[q] = pa[h].y; T.z[q] = pa[h].z;
+                T.w[q] = pa[h].w;
                 T.b[q] = qa[h]; T.c[q] = ca[h];
             }
+#endif
             wave_lds_sync();
             /* 3. each run of this lane within the window: LDS positions [base,
              * base + m). Tested two photons per packed instruction, 32
              * positions at a time, into hit masks; the hits of all runs are
              * then summed in one loop with every lane busy (max over lanes of
              * its hits per chunk, not one masked pass per photon any lane hits). */
+#if PM_TILE_PAIRS
+            /* the pairs from even position a + v0: cnt (<= 32) positions, bits 2j / 2j + 1 of pair j;
+             * positions outside [lo_bit, hi_bit) of this chunk are another run's or the window's */
+            auto test32p = [&](uint32_t a, uint32_t v0, uint32_t cnt, uint32_t lo_bit, uint32_t hi_bit) {
+                const float4 *pp = &T.pr[a + v0]; /* pair (a + v0) / 2: two float4 each */
+                uint32_t bits = 0u;
+                const uint32_t np = (cnt + 1u) >> 1;
+#pragma unroll 4
+                for (uint32_t j = 0; j < np; ++j) {
+                    const float4 xy = pp[2 * j];
+                    const f2 zz = *reinterpret_cast<const f2 *>(&pp[2 * j + 1]);
+                    const f2 ddx = px2 - f2{xy.x, xy.y}, ddy = py2 - f2{xy.z, xy.w}, ddz = pz2 - zz;
+                    const f2 d2 = (ddx * ddx + ddy * ddy) + ddz * ddz;
+                    /* d2 < r^2 is the sign of min(d2, FLT_MAX) - r^2: exact
+                     * for finite d2 (a difference of unequal floats is never
+                     * 0, d2 >= +0), and a NaN d2 (non-finite photon or record
+                     * coordinates; its sign bit is arbitrary — the packed
+                     * subtract negates an operand) becomes FLT_MAX, false as
+                     * the comparison is; shifted in with one alignbit per
+                     * photon; the first pair ends in the top bits: reversed
+                     * below */
+                    const f2 df = f2{fminf(d2.x, 0x1.fffffep127f), fminf(d2.y, 0x1.fffffep127f)} - r2v;
+                    bits = __builtin_amdgcn_alignbit(bits, __float_as_uint(df.x), 31u);
+                    bits = __builtin_amdgcn_alignbit(bits, __float_as_uint(df.y), 31u);
+                }
+                bits = __builtin_bitreverse32(bits) >> (32u - 2u * np);
+                const uint32_t hi_m = hi_bit >= 32u ? 0xffffffffu : (1u << hi_bit) - 1u;
+                return bits & hi_m & ~((1u << lo_bit) - 1u);
+            };
+#endif
+#if !PM_TILE_PAIRS
             auto test32 = [&](uint32_t base, uint32_t v0, uint32_t cnt, uint32_t m) {
                 const float *xs = T.x + base + v0, *ys = T.y + base + v0, *zs = T.z + base + v0;
                 uint32_t bits = 0u;
@@ -577,6 +651,7 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
                 const uint32_t left = m > v0 ? m - v0 : 0u;
                 return bits & (left >= 32u ? 0xffffffffu : (1u << left) - 1u);
             };
+#endif
             auto hit = [&](uint32_t t) {
                 const float4 qb4 = T.b[t];
                 const v3 wi = mk(T.w[t], qb4.w, T.c[t]);
@@ -596,6 +671,11 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
                 const uint32_t lo = max(sK[k], T0), hi = min(eK[k], T0 + n);
                 mK[k] = hi > lo ? hi - lo : 0u;
                 baseK[k] = mK[k] ? lo - T0 : 0u; /* < TILE_CAP */
+#if PM_TILE_PAIRS
+                /* from the even position below the run: one more position when it starts odd */
+                mK[k] += mK[k] ? (baseK[k] & 1u) : 0u;
+                baseK[k] &= ~1u;
+#endif
                 vK[k] = wave_max_u32(mK[k]);
                 vmax = max(vmax, vK[k]);
             }
@@ -606,7 +686,16 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
 #pragma unroll
                 for (int k = 0; k < KR; ++k) {
                     TILE_STAT(2, (min(32u, vK[k] > vb ? vK[k] - vb : 0u) + 1) / 2);
+#if PM_TILE_PAIRS
+                    {
+                        /* the run's first position is odd: bit 0 of its first chunk is not its own */
+                        const uint32_t lob = vb == 0u && mK[k] ? (uint32_t)(max(sK[k], T0) - T0 - baseK[k]) : 0u;
+                        const uint32_t hib = mK[k] > vb ? mK[k] - vb : 0u;
+                        bK[k] = vK[k] > vb ? test32p(baseK[k], vb, min(32u, vK[k] - vb), lob, hib) : 0u;
+                    }
+#else
                     bK[k] = vK[k] > vb ? test32(baseK[k], vb, min(32u, vK[k] - vb), mK[k]) : 0u;
+#endif
                     nh += __builtin_popcount(bK[k]);
                     any |= bK[k];
                 }

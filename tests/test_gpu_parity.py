@@ -247,6 +247,46 @@ def test_bucket_gather_kernels_agree(radius2, W, H, paths, oracle_mod, hip_mod, 
         assert_bitexact(outs[name][0], ref_rec, f"{name} vs per-lane gather")
 
 
+def test_tile_gather_nan_photons(oracle_mod, hip_mod, monkeypatch):
+    """Uploaded slots whose positions hold NaNs of either sign (and infinities):
+    the tile kernel reads d2 < r^2 off the sign of min(d2, FLT_MAX) - r^2,
+    exact for finite d2, with a NaN d2 (of either sign) clamped first.
+    Partials and records equal the per-lane kernel's float comparisons bit
+    for bit."""
+    torch = pytest.importorskip("torch")
+    sc = scenes.cornell_box(64, 48)
+    orc = sc.load_into(oracle_mod.Oracle())
+    p, recs, slots = _gather_inputs(orc, radius2=25.0, paths=16384)
+    p.gather_structure = PM_GATHER_GRID
+    slots = slots.copy()
+    valid = np.flatnonzero(slots["bits"] & 1)
+    rng = np.random.RandomState(3)
+    pick = rng.choice(valid, size=len(valid) // 20, replace=False)
+    pos = slots["p"].view(np.uint32)
+    for k, idx in enumerate(np.array_split(pick, 4)):
+        axis = k % 3
+        pos[idx, axis] = (0x7fc00000, 0xffc00000, 0x7f800000, 0xff800001)[k]
+    outs = {}
+    for name in ("lane", "tile"):
+        monkeypatch.setenv("PM_GATHER_KERNEL", name)
+        ctx = sc.load_into(hip_mod.Context(0))
+        try:
+            ctx.upload_records(recs)
+            ctx.upload_slots(slots)
+            ctx.build_photon_map(p, len(slots))
+            part = torch.zeros((len(recs), 4), dtype=torch.int64, device="cuda")
+            torch.cuda.synchronize()
+            ctx.gather_partial(p, part.data_ptr())
+            ctx.synchronize()
+            ctx.gather(p)
+            outs[name] = (ctx.download_records(), part.cpu().numpy())
+        finally:
+            ctx.close()
+    assert (outs["lane"][1][:, 0] > 0).sum() > 100
+    assert np.array_equal(outs["tile"][1], outs["lane"][1])
+    assert_bitexact(outs["tile"][0], outs["lane"][0], "tile vs per-lane gather with NaN photons")
+
+
 def test_adaptive_grid_radius_progressive(oracle_mod, hip_mod, monkeypatch):
     """Progressive passes size the photon grid from the records' current
     radii (a histogram binned by the fused gather, PM_GRID_QUANTILE; records
