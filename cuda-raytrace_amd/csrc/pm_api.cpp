@@ -133,6 +133,8 @@ struct Ctx {
     DevBuf d_porder, d_pscratch;
     int64_t pool_waves = 0;         /* pooled kernel: waves per launch (env PM_POOL_WAVES; 0 = one occupancy round) */
     bool key_planes = true;         /* fused bucket keys / ranks plane-major (env PM_KEY_PLANES) */
+    int pool_stack = 31;            /* pooled kernel: LDS stack entries per lane (env PM_POOL_STACK; 0 = the exact bound): 31 lets five blocks share a CU's LDS */
+    DevBuf d_spill;                 /* pooled kernel: stack entries beyond pool_stack */
     int gather_kernel = PM_GK_TILE; /* bucket gather kernel (env PM_GATHER_KERNEL=tile|lane|wave) */
     bool gather_xcd = false;        /* tile gather: contiguous tile ranges per XCD (env PM_GATHER_XCD=1) */
     int cell_span = 2;              /* PPM grid: cells per axis of a query box (env PM_CELL_SPAN 2..5) */
@@ -757,6 +759,7 @@ int pm_create(void **out, const pm_config *cfg) {
     if (const char *e = getenv("PM_PATH_SORT")) c->path_sort = atoi(e) != 0;
     if (const char *e = getenv("PM_POOL_WAVES")) c->pool_waves = std::max(1LL, atoll(e));
     if (const char *e = getenv("PM_KEY_PLANES")) c->key_planes = atoi(e) != 0;
+    if (const char *e = getenv("PM_POOL_STACK")) c->pool_stack = std::max(0, atoi(e));
     if (const char *e = getenv("PM_TILE_LIST")) c->tile_list = atoi(e) != 0;
     if (const char *e = getenv("PM_KD_STACK")) c->kd_stack = std::max(1, std::min(KD_STACK, atoi(e)));
     if (const char *e = getenv("PM_STAGE_TIMERS")) if (atoi(e) == 0) c->timed_stages.clear();
@@ -798,7 +801,7 @@ void pm_destroy(void *ptr) {
                       &c->d_cell_start, &c->d_pha, &c->d_phb,
                       &c->d_kd, &c->d_out, &c->d_counters, &c->d_tiles, &c->d_tile_flags, &c->d_tile_count,
                       &c->d_r2hist, &c->d_order, &c->d_ocount, &c->d_ostart, &c->d_oscratch, &c->d_ostats,
-                      &c->d_porder, &c->d_pscratch};
+                      &c->d_porder, &c->d_pscratch, &c->d_spill};
     for (DevBuf *b : bufs) b->release();
     if (c->tile_event) (void)hipEventDestroy(c->tile_event);
     if (c->r2_event) (void)hipEventDestroy(c->r2_event);
@@ -1396,11 +1399,16 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
          * occupancy API: VGPRs and the LDS stacks) — each wave with a
          * contiguous pool of a multiple of 64 paths. C3 sweep (1M paths, 256 CUs): 4096 waves 5.25 ms, 8192
          * (two rounds) 5.81, 5462 (1.33 rounds) 6.73, 2048 7.22 */
+        /* LDS stack entries per lane (env PM_POOL_STACK; 0 = the tree's exact
+         * bound): below the bound, deeper entries spill to global memory and
+         * the smaller LDS reservation admits more resident blocks */
+        const int lstk = c->pool_stack > 0 && c->pool_stack < c->S.stack_depth ? c->pool_stack : c->S.stack_depth;
+        T.pool_stack = lstk;
         int64_t waves = c->pool_waves;
         if (waves <= 0) {
             int cus = 0;
             if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0) cus = 256;
-            const size_t lds = (size_t)c->S.stack_depth * TRACE_BLOCK * 4 + c->S.lds_bytes + (size_t)c->S.nodelets * 64;
+            const size_t lds = (size_t)lstk * TRACE_BLOCK * 4 + c->S.lds_bytes + (size_t)c->S.nodelets * 64;
             int per_cu = trace_pool_waves_per_cu(lds, 0);
             if (T.hold && c->S.wide) { /* pooled kernel: the held deposits' LDS must not cost resident waves */
                 const int per_cu_h = trace_pool_waves_per_cu(lds, 1);
@@ -1412,6 +1420,13 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
         /* any pool size works (the wave's cursor hands out paths to dead lanes) */
         const int64_t per = std::max<int64_t>(1, (path_count + waves - 1) / waves);
         T.pool_paths = per;
+        if (lstk < c->S.stack_depth) {
+            const int64_t blocks = ((path_count + per - 1) / per + TRACE_BLOCK / 64 - 1) / (TRACE_BLOCK / 64);
+            const int64_t threads = blocks * TRACE_BLOCK;
+            HIPCHK(c, c->d_spill.ensure((size_t)threads * (size_t)(c->S.stack_depth - lstk) * 4));
+            T.spill = c->d_spill.as<int>();
+            T.spill_stride = (uint32_t)threads;
+        }
     }
     T.refill_min = c->trace_refill_min;
     T.pass = pass; T.mpc = (int)mpc; T.max_spec = p->max_specular_depth; T.light_index = p->light_source_index;

@@ -718,9 +718,24 @@ PMD void trav_begin(const Ray &ray, TravState &t) {
     t.l0n = t.l1n = t.l2n = t.l3n = 0;
     t.l0s = t.l1s = t.l2s = t.l3s = 0;
 }
+/* a lane's traversal stack: entries below cap in its LDS column, deeper ones
+ * (rare: the bound is exact, typical depths are far below it) in a global
+ * spill area, entry i of thread gid at spill[(i - cap) * sstride + gid] —
+ * so the LDS a block reserves can be sized for occupancy, not the worst ray */
+struct SpillStack {
+    int *lds;
+    int stride, cap;
+    int *spill;
+    uint32_t sstride, gid;
+    PMD void put(int i, int v) const {
+        if (i < cap) lds[i * stride] = v;
+        else spill[(size_t)(i - cap) * sstride + gid] = v;
+    }
+    PMD int get(int i) const { return i < cap ? lds[i * stride] : spill[(size_t)(i - cap) * sstride + gid]; }
+};
 /* false once the ray is done (best holds its closest hit, if any) */
 template <class C>
-PMD bool trav_step(const SceneDev &S, const Ray &ray, TravState &T, int *stack, int stride, C &cen,
+PMD bool trav_step(const SceneDev &S, const Ray &ray, TravState &T, const SpillStack &stk, C &cen,
                    const uint4 *lds_nodes = nullptr, int n_lds = 0) {
     if (T.l0n != 0) {
         leaf_isect<false, PM_BVH4_QUANT != 0>(S, T.l0s, T.l0n, ray, T.best, cen);
@@ -749,11 +764,11 @@ PMD bool trav_step(const SceneDev &S, const Ray &ray, TravState &T, int *stack, 
         if (t[b] < t[a]) { const float tt = t[a]; t[a] = t[b]; t[b] = tt; const int cc = c[a]; c[a] = c[b]; c[b] = cc; }
     };
     cs(0, 1); cs(2, 3); cs(0, 2); cs(1, 3); cs(1, 2);
-    if (t[3] != INF) { stack[T.sp * stride] = c[3]; ++T.sp; }
-    if (t[2] != INF) { stack[T.sp * stride] = c[2]; ++T.sp; }
-    if (t[1] != INF) { stack[T.sp * stride] = c[1]; ++T.sp; }
+    if (t[3] != INF) { stk.put(T.sp, c[3]); ++T.sp; }
+    if (t[2] != INF) { stk.put(T.sp, c[2]); ++T.sp; }
+    if (t[1] != INF) { stk.put(T.sp, c[1]); ++T.sp; }
     if (t[0] != INF) T.cur = c[0];
-    else if (T.sp > 0) { --T.sp; T.cur = stack[T.sp * stride]; }
+    else if (T.sp > 0) { --T.sp; T.cur = stk.get(T.sp); }
     else T.cur = -1;
     return T.l0n != 0 || T.cur >= 0;
 }

@@ -106,6 +106,12 @@ struct TraceParams {
      * written once per path (pm_trace.hip Held; used when mpc == 4 and the
      * slot buffer is 16-B aligned) */
     int hold;
+    /* pooled kernel: LDS stack entries per lane (0: S.stack_depth); deeper
+     * entries go to spill (entry i of thread g at spill[(i - pool_stack) *
+     * spill_stride + g]) */
+    int pool_stack;
+    int *spill;
+    uint32_t spill_stride;
     /* fused counting: keys / ranks plane-major (deposit k of path i at k * key_np + i) when > 0, else at the slot index */
     int64_t key_np;
 };

@@ -662,7 +662,14 @@ constexpr int POOL_STEPS = PM_POOL_STEPS, POOL_SHADE_MIN = PM_POOL_SHADE_MIN;
 enum { PHASE_DEAD = 0, PHASE_TRAV = 1, PHASE_SHADE = 2 };
 
 template <int COUNT, int HOLD>
-#ifdef PM_POOL_EU /* experiment: make variant VFLAGS=-DPM_POOL_EU=5 */
+/* 5 waves/SIMD: 96 VGPRs (102 unconstrained -> 4 waves), no scratch; with
+ * the LDS stacks capped at 31 entries (PM_POOL_STACK, the rest spilled) five
+ * 256-thread blocks fit a CU. C3 trace (same box): 4.59-4.61 ms at 4 waves,
+ * 4.41-4.42 ms at 5 (stack 31 or 24); 6 (80 VGPRs, 100 B of scratch) 4.58 */
+#ifndef PM_POOL_EU
+#define PM_POOL_EU 5
+#endif
+#if PM_POOL_EU > 0
 #define POOL_OCC __attribute__((amdgpu_waves_per_eu(PM_POOL_EU, PM_POOL_EU)))
 #else
 #define POOL_OCC
@@ -675,6 +682,9 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
     const SceneDev &S = P.S;
     __syncthreads();
     int *stack = stk + tid;
+    /* LDS stack entries per lane (P.pool_stack, else the tree's bound); deeper ones spill to global memory */
+    const int lstk = P.pool_stack > 0 && P.pool_stack < P.S.stack_depth ? P.pool_stack : P.S.stack_depth;
+    const SpillStack sstk{stack, TRACE_BLOCK, lstk, P.spill, P.spill_stride, (uint32_t)(blockIdx.x * TRACE_BLOCK + tid)};
     typename std::conditional<COUNT != 0, Census, NoCensus>::type cen;
     TProf prof;
     uint32_t rays = 0, deposits = 0;
@@ -685,10 +695,10 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
     PathState st;
     TravState tr;
     Held held;
-    if (HOLD) held.col = reinterpret_cast<uint32_t *>(stk + P.S.stack_depth * TRACE_BLOCK) + tid; /* after the stacks */
+    if (HOLD) held.col = reinterpret_cast<uint32_t *>(stk + lstk * TRACE_BLOCK) + tid; /* after the stacks */
     /* nodelets after the stacks (and the held deposits): the BVH's top levels */
     const int n_lds = PM_BVH4_QUANT ? S.nodelets : 0;
-    uint4 *lnodes = reinterpret_cast<uint4 *>(stk + P.S.stack_depth * TRACE_BLOCK + (HOLD ? HOLD_WORDS * TRACE_BLOCK : 0));
+    uint4 *lnodes = reinterpret_cast<uint4 *>(stk + lstk * TRACE_BLOCK + (HOLD ? HOLD_WORDS * TRACE_BLOCK : 0));
     if (n_lds > 0) {
         const uint4 *g = reinterpret_cast<const uint4 *>(S.wnodes);
         for (int i = tid; i < 4 * n_lds; i += TRACE_BLOCK) lnodes[i] = g[i];
@@ -734,7 +744,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
         }
 #pragma unroll 1
         for (int k = 0; k < POOL_STEPS; ++k)
-            if (phase == PHASE_TRAV && !trav_step(S, st.ray, tr, stack, TRACE_BLOCK, cen, lnodes, n_lds)) phase = PHASE_SHADE;
+            if (phase == PHASE_TRAV && !trav_step(S, st.ray, tr, sstk, cen, lnodes, n_lds)) phase = PHASE_SHADE;
     }
     if (COUNT) {
         uint32_t nodes = 0, prims = 0;
@@ -871,6 +881,9 @@ hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s) {
     if (p.path_count <= 0) return hipSuccess;
     const size_t lds = (size_t)p.S.stack_depth * TRACE_BLOCK * 4 + p.S.lds_bytes;
     if (p.pool_paths > 0 && scene_mode(p.S) == MODE_GLOBAL && p.S.wide) {
+        const int lstk = p.pool_stack > 0 && p.pool_stack < p.S.stack_depth ? p.pool_stack : p.S.stack_depth;
+        if (lstk < p.S.stack_depth && !p.spill) return hipErrorInvalidValue;
+        const size_t lds = (size_t)lstk * TRACE_BLOCK * 4;
         TraceParams q = p;
         q.wave_paths = p.pool_paths;
         const int64_t waves = (p.path_count + q.wave_paths - 1) / q.wave_paths;
