@@ -611,7 +611,10 @@ __global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherPar
                 const float4 *pp = &T.pr[a + v0]; /* pair (a + v0) / 2: two float4 each */
                 uint32_t bits = 0u;
                 const uint32_t np = (cnt + 1u) >> 1;
-#pragma unroll 4
+#ifndef PM_TEST_UNROLL
+#define PM_TEST_UNROLL 2 /* 96 VGPRs, 5 waves/SIMD (4: 110 VGPRs, 4 waves): C2 gather 48.9-49.7 -> 47.5-48.4 us, C5 0.217 -> 0.206 ms, C3 0.545 -> 0.563 ms */
+#endif
+#pragma unroll PM_TEST_UNROLL
                 for (uint32_t j = 0; j < np; ++j) {
                     const float4 xy = pp[2 * j];
                     const f2 zz = *reinterpret_cast<const f2 *>(&pp[2 * j + 1]);
