@@ -135,6 +135,14 @@ struct Ctx {
     bool key_planes = true;         /* fused bucket keys / ranks plane-major (env PM_KEY_PLANES) */
     int pool_stack = 31;            /* pooled kernel: LDS stack entries per lane (env PM_POOL_STACK; 0 = the exact bound): 31 lets five blocks share a CU's LDS */
     DevBuf d_spill;                 /* pooled kernel: stack entries beyond pool_stack */
+    /* wavefront trace (env PM_TRACE_WAVEFRONT=1; 4-wide BVH scenes): one
+     * pooled launch per bounce, rays reordered between bounces by origin cell
+     * (2^wf_bits per axis, env PM_WF_BITS) and direction octant unless
+     * PM_WF_SORT=0 (queue order) */
+    bool trace_wavefront = false;
+    int wf_bits = 4;
+    bool wf_sort = true;
+    DevBuf d_wfq, d_wfw;
     int gather_kernel = PM_GK_TILE; /* bucket gather kernel (env PM_GATHER_KERNEL=tile|lane|wave) */
     bool gather_xcd = false;        /* tile gather: contiguous tile ranges per XCD (env PM_GATHER_XCD=1) */
     int cell_span = 2;              /* PPM grid: cells per axis of a query box (env PM_CELL_SPAN 2..5) */
@@ -760,6 +768,9 @@ int pm_create(void **out, const pm_config *cfg) {
     if (const char *e = getenv("PM_POOL_WAVES")) c->pool_waves = std::max(1LL, atoll(e));
     if (const char *e = getenv("PM_KEY_PLANES")) c->key_planes = atoi(e) != 0;
     if (const char *e = getenv("PM_POOL_STACK")) c->pool_stack = std::max(0, atoi(e));
+    if (const char *e = getenv("PM_TRACE_WAVEFRONT")) c->trace_wavefront = atoi(e) != 0;
+    if (const char *e = getenv("PM_WF_BITS")) c->wf_bits = std::max(0, std::min(9, atoi(e)));
+    if (const char *e = getenv("PM_WF_SORT")) c->wf_sort = atoi(e) != 0;
     if (const char *e = getenv("PM_TILE_LIST")) c->tile_list = atoi(e) != 0;
     if (const char *e = getenv("PM_KD_STACK")) c->kd_stack = std::max(1, std::min(KD_STACK, atoi(e)));
     if (const char *e = getenv("PM_STAGE_TIMERS")) if (atoi(e) == 0) c->timed_stages.clear();
@@ -801,7 +812,7 @@ void pm_destroy(void *ptr) {
                       &c->d_cell_start, &c->d_pha, &c->d_phb,
                       &c->d_kd, &c->d_out, &c->d_counters, &c->d_tiles, &c->d_tile_flags, &c->d_tile_count,
                       &c->d_r2hist, &c->d_order, &c->d_ocount, &c->d_ostart, &c->d_oscratch, &c->d_ostats,
-                      &c->d_porder, &c->d_pscratch, &c->d_spill};
+                      &c->d_porder, &c->d_pscratch, &c->d_spill, &c->d_wfq, &c->d_wfw};
     for (DevBuf *b : bufs) b->release();
     if (c->tile_event) (void)hipEventDestroy(c->tile_event);
     if (c->r2_event) (void)hipEventDestroy(c->r2_event);
@@ -1363,6 +1374,49 @@ static hipError_t count_zeroed(Ctx *c, size_t words, hipStream_t s) {
     return e;
 }
 
+/* Wavefront trace (Ctx::trace_wavefront): bounce 0 emits the paths, every
+ * later bounce takes the previous one's queue of continuing rays, reordered
+ * by (origin cell, direction octant) unless wf_sort is off. A path makes at
+ * most mpc + max_spec + 1 rays, so that many launches drain every queue; the
+ * counts stay on the device (an empty bounce exits at once). */
+static int trace_wavefront(Ctx *c, TraceParams T, int64_t path_count, hipStream_t s) {
+    const int64_t cap = path_count, cap4 = (cap + 3) & ~(int64_t)3;
+    const int maxb = T.mpc + std::max(T.max_spec, 0) + 2;
+    const int64_t nbins = (int64_t)1 << (3 * c->wf_bits + 3), cnt4 = (2 * maxb + 3) & ~3; /* counts, next positions */
+    HIPCHK(c, c->d_wfq.ensure((size_t)2 * (size_t)cap * WF_ENTRY_F4 * sizeof(float4)));
+    const size_t words = (size_t)(cnt4 + 3 * cap4 + 2 * nbins) + scan_scratch_words(nbins);
+    HIPCHK(c, c->d_wfw.ensure(words * 4));
+    uint32_t *cnt = c->d_wfw.as<uint32_t>(), *key = cnt + cnt4, *rank = key + cap4, *perm = rank + cap4;
+    uint32_t *bins = perm + cap4, *start = bins + nbins, *sums = start + nbins;
+    HIPCHK(c, hipMemsetAsync(cnt, 0, (size_t)cnt4 * 4, s));
+    HIPCHK(c, hipMemsetAsync(bins, 0, (size_t)nbins * 4, s));
+    float4 *Q[2] = {c->d_wfq.as<float4>(), c->d_wfq.as<float4>() + (size_t)cap * WF_ENTRY_F4};
+    T.hold = 0;
+    T.order = nullptr;
+    T.wf_key = key; T.wf_rank = rank; T.wf_bins = c->wf_sort ? bins : nullptr; T.wf_bits = c->wf_bits;
+    for (int a = 0; a < 3; ++a) {
+        T.wf_lo[a] = c->bbox_lo[a];
+        T.wf_scale[a] = (float)(1 << c->wf_bits) / std::max(c->bbox_hi[a] - c->bbox_lo[a], 1e-3f);
+    }
+    for (int b = 0; b < maxb; ++b) {
+        T.wf = b == 0 ? 1 : 2;
+        T.wf_perm = nullptr;
+        if (b > 0) {
+            T.wf_q_in = Q[(b - 1) & 1];
+            T.wf_n_in = cnt + b - 1;
+            T.wf_next = cnt + maxb + b;
+            if (c->wf_sort) {
+                HIPCHK(c, launch_wf_order(cnt + b - 1, (uint32_t)cap, bins, (uint32_t)nbins, start, sums, key, rank, perm, s));
+                T.wf_perm = perm;
+            }
+        }
+        T.wf_q_out = b + 1 < maxb ? Q[b & 1] : nullptr;
+        T.wf_n_out = cnt + b;
+        HIPCHK(c, launch_trace(T, c->counting, s));
+    }
+    return PM_OK;
+}
+
 int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t path_begin, int64_t path_count,
                      int64_t slot_path_base, void *stream) {
     GETCTX(ptr);
@@ -1462,8 +1516,14 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
     }
     timer_begin(c, "trace", s);
     /* the kernel writes all path_count * mpc slots: deposits, then zeros */
-    HIPCHK(c, launch_trace(T, c->counting, s));
-    timer_end(c, "trace", s);
+    if (c->trace_wavefront && T.pool_paths > 0 && c->S.wide) {
+        rc = trace_wavefront(c, T, path_count, s);
+        timer_end(c, "trace", s);
+        if (rc) return rc;
+    } else {
+        HIPCHK(c, launch_trace(T, c->counting, s));
+        timer_end(c, "trace", s);
+    }
     if (fuse) { c->fused.valid = true; c->fused.n = end_slot; c->fused.grid = T.grid; c->fused.key_np = T.key_np; c->fused.mpc = (int)mpc; c->count_zero_words = 0; }
     /* traced photons carry the scene's signs (scene_nonneg); slots outside
      * the traced range keep theirs, so the flag is reset only when this

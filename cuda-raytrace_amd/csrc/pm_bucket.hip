@@ -195,6 +195,13 @@ hipError_t launch_exclusive_scan(const uint32_t *in, int64_t n, uint32_t *out, u
     pm_launch(k_scan_down, dim3(ntile), dim3(SCAN_BLOCK), 0, s, in, n, sums, out, nullptr);
     return hipGetLastError();
 }
+hipError_t launch_exclusive_scan_clear(uint32_t *in, int64_t n, uint32_t *out, uint32_t *sums, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int ntile = (int)((n + SCAN_TILE - 1) / SCAN_TILE);
+    pm_launch(k_scan_reduce, dim3(ntile), dim3(SCAN_BLOCK), 0, s, in, n, sums);
+    pm_launch(k_scan_down, dim3(ntile), dim3(SCAN_BLOCK), 0, s, in, n, sums, out, in);
+    return hipGetLastError();
+}
 
 size_t bucket_scratch_words(int64_t n_slots, uint32_t ncells) {
     const int64_t ntile = ((int64_t)ncells + 1 + SCAN_TILE - 1) / SCAN_TILE;

@@ -426,23 +426,23 @@ hipError_t launch_r2hist_reduce(uint32_t *hist, uint32_t *out_mapped, hipStream_
 template <int KR>
 constexpr uint32_t tile_group_r() { return KR == 2 ? GROUP_R : (8u - (uint32_t)KR) / 2u; }
 template <int PARTIAL, int NN, int KR>
-__global__ __launch_bounds__(GATHER_BLOCK) TILE_OCC void k_gather_tile(GatherParams P) {
+__global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParams P) {
     static_assert(KR >= 2 && KR <= 5 && 2 * tile_group_r<KR>() + KR <= 8, "lane box / group radius");
     constexpr uint32_t GR = tile_group_r<KR>();
-    __shared__ TileLds tiles[GATHER_BLOCK / 64];
+    __shared__ TileLds tiles[TILE_BLOCK / 64];
     TileLds &T = tiles[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     int64_t r;
     if (P.order) { /* active records in cell order (incoherent tiles); past the end: not live */
-        const int64_t i = ((int64_t)blockIdx.x * (GATHER_BLOCK / 64) + (threadIdx.x >> 6)) * 64 + lane;
+        const int64_t i = ((int64_t)blockIdx.x * (TILE_BLOCK / 64) + (threadIdx.x >> 6)) * 64 + lane;
         if (i - lane >= P.n_order) return;
         r = i < P.n_order ? (int64_t)P.order[i] : P.rec_end;
     } else if (P.tiles) { /* only tiles with an active record (no block-level barrier below: a wave may leave) */
-        const int64_t w = (int64_t)blockIdx.x * (GATHER_BLOCK / 64) + (threadIdx.x >> 6);
+        const int64_t w = (int64_t)blockIdx.x * (TILE_BLOCK / 64) + (threadIdx.x >> 6);
         if (w >= (P.n_tiles_dev ? (int64_t)*P.n_tiles_dev : P.n_tiles)) return;
         r = P.rec_begin + (int64_t)P.tiles[w] * 64 + lane;
     } else {
-        r = P.rec_begin + gather_block(P) * GATHER_BLOCK + threadIdx.x;
+        r = P.rec_begin + gather_block(P) * TILE_BLOCK + threadIdx.x;
     }
     const GridDesc &g = P.grid;
     GatherRec R;
@@ -1686,10 +1686,10 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_kd(GatherParams P) {
 template <int PARTIAL, int NN>
 static void launch_tile_nn(const GatherParams &p, unsigned g, hipStream_t s) {
     switch (p.span) { /* cells per axis of a lane box at the grid's design radius */
-    case 2: pm_launch((k_gather_tile<PARTIAL, NN, 2>), dim3(g), dim3(GATHER_BLOCK), 0, s, p); break;
-    case 3: pm_launch((k_gather_tile<PARTIAL, NN, 3>), dim3(g), dim3(GATHER_BLOCK), 0, s, p); break;
-    case 4: pm_launch((k_gather_tile<PARTIAL, NN, 4>), dim3(g), dim3(GATHER_BLOCK), 0, s, p); break;
-    default: pm_launch((k_gather_tile<PARTIAL, NN, 5>), dim3(g), dim3(GATHER_BLOCK), 0, s, p); break;
+    case 2: pm_launch((k_gather_tile<PARTIAL, NN, 2>), dim3(g), dim3(TILE_BLOCK), 0, s, p); break;
+    case 3: pm_launch((k_gather_tile<PARTIAL, NN, 3>), dim3(g), dim3(TILE_BLOCK), 0, s, p); break;
+    case 4: pm_launch((k_gather_tile<PARTIAL, NN, 4>), dim3(g), dim3(TILE_BLOCK), 0, s, p); break;
+    default: pm_launch((k_gather_tile<PARTIAL, NN, 5>), dim3(g), dim3(TILE_BLOCK), 0, s, p); break;
     }
 }
 template <int PARTIAL>
@@ -1705,7 +1705,7 @@ static void launch_g(const GatherParams &p, hipStream_t s) {
         /* the tile list: only tiles with an active record; or the active
          * records in cell order, 64 per wave */
         const int64_t waves = p.order ? (p.n_order + 63) / 64 : p.n_tiles;
-        const unsigned g = (unsigned)((waves + GATHER_BLOCK / 64 - 1) / (GATHER_BLOCK / 64));
+        const unsigned g = (unsigned)((waves + TILE_BLOCK / 64 - 1) / (TILE_BLOCK / 64));
         if (g == 0) return;
         launch_tile<PARTIAL>(p, g, s);
         return;
@@ -1714,7 +1714,7 @@ static void launch_g(const GatherParams &p, hipStream_t s) {
      * photons per RECORD) is the algorithm's unit count bench.py prices; the
      * tile and wave kernels find exactly the same photons (bit-identical records) */
     if (STRUCT == PM_GATHER_GRID && !COUNT && p.kernel == PM_GK_TILE)
-        launch_tile<PARTIAL>(p, grid, s);
+        launch_tile<PARTIAL>(p, (unsigned)((p.rec_end - p.rec_begin + TILE_BLOCK - 1) / TILE_BLOCK), s);
     else if (STRUCT == PM_GATHER_GRID && !COUNT && p.kernel == PM_GK_WAVE)
         pm_launch((k_gather_wave<PARTIAL>), dim3(grid), dim3(GATHER_BLOCK), 0, s, p);
     else if (STRUCT == PM_GATHER_GRID)

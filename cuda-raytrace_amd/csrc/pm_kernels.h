@@ -35,6 +35,16 @@ constexpr int EYE_BLOCK = 128;     /* traversal kernels: LDS stack column per la
 constexpr int TRACE_BLOCK = 256;    /* k_trace: 4 waves compact paths together */
 constexpr int BVH_STACK = BVH_STACK_DEPTH; /* >= max BVH depth (builder enforces it) */
 constexpr int GATHER_BLOCK = 256;
+/* k_gather_tile: waves per block. Its waves never synchronise with each
+ * other, and a block's LDS is held until its last wave ends, so with several
+ * waves per block a tile that runs long keeps its neighbours' LDS allocated
+ * (LDS co-limits the kernel at 5 waves/SIMD). One wave per block: C2
+ * gather 47.6 -> 46.5-47.1 us, C3 0.54-0.56 -> 0.53 ms, C5 0.30 -> 0.27 ms
+ * (same box, against 256) */
+#ifndef PM_TILE_BLOCK
+#define PM_TILE_BLOCK 64
+#endif
+constexpr int TILE_BLOCK = PM_TILE_BLOCK;
 enum { PM_GK_TILE = 0, PM_GK_LANE = 1, PM_GK_WAVE = 2 };
 /* error word of a kd-tree gather: a record's traversal stack overflowed (a
  * subtree would have been dropped), or the node links are not a pbrt tree */
@@ -114,7 +124,25 @@ struct TraceParams {
     uint32_t spill_stride;
     /* fused counting: keys / ranks plane-major (deposit k of path i at k * key_np + i) when > 0, else at the slot index */
     int64_t key_np;
+    /* wavefront mode of the pooled kernel (pm_api.cpp trace_wavefront; one
+     * launch per bounce): wf 1 = emit the launch's paths, 2 = take the rays of
+     * queue wf_q_in (wf_n_in of them on the device, in wf_perm's order when
+     * non-null); both hand every continuing path to queue wf_q_out (48-B
+     * WfRay entries, wave-aggregated append to *wf_n_out) together with its
+     * reorder key (origin cell Morton code x direction octant) and rank in
+     * the key's bin counter. wf_q_out null: the last bounce (no path can
+     * continue) */
+    int wf;
+    const uint32_t *wf_n_in, *wf_perm;
+    const float4 *wf_q_in;
+    float4 *wf_q_out;
+    uint32_t *wf_n_out, *wf_key, *wf_rank, *wf_bins;
+    uint32_t *wf_next; /* wf 2: the queue's next untaken position (waves take runs of it as lanes free up) */
+    float wf_lo[3], wf_scale[3]; /* origin -> [0, 2^wf_bits) per axis */
+    int wf_bits;
 };
+/* wavefront ray queue entry: (o, tmin) (d, pid) (alpha, nI | stored << 8 | spec << 16) */
+constexpr int WF_ENTRY_F4 = 3;
 
 struct GatherParams {
     RecordsDev R;
@@ -208,6 +236,12 @@ int trace_pool_waves_per_cu(size_t lds, int hold);
 size_t scan_scratch_words(int64_t n);
 size_t path_order_scratch_words(int64_t n);
 hipError_t launch_path_order(const TraceParams &p, uint32_t *scratch, uint32_t *order, hipStream_t s);
+/* wavefront mode: the next bounce's order of queue entries [0, *n): scan of
+ * the key bins (zeroed as they are read) + scatter by key and rank */
+hipError_t launch_wf_order(const uint32_t *n, uint32_t cap, uint32_t *bins, uint32_t nbins, uint32_t *start,
+                           uint32_t *sums, const uint32_t *key, const uint32_t *rank, uint32_t *perm, hipStream_t s);
+/* exclusive scan that zeroes `in` as it reads it (pm_bucket.hip) */
+hipError_t launch_exclusive_scan_clear(uint32_t *in, int64_t n, uint32_t *out, uint32_t *sums, hipStream_t s);
 int trace_lane_waves_per_cu(const SceneDev &S, size_t lds, int hold);
 /* adaptive-grid histogram: sum the R2_COPIES copies into host-mapped
  * out[R2_BINS] with plain stores (no copy engine) and zero the copies */

@@ -661,7 +661,80 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
 constexpr int POOL_STEPS = PM_POOL_STEPS, POOL_SHADE_MIN = PM_POOL_SHADE_MIN;
 enum { PHASE_DEAD = 0, PHASE_TRAV = 1, PHASE_SHADE = 2 };
 
-template <int COUNT, int HOLD>
+/* Wavefront mode (TraceParams::wf): the pooled kernel runs one bounce per
+ * launch. A path whose ray continues leaves the kernel through a queue
+ * instead of tracing on in the same lane; between launches the queue is
+ * ordered by (origin cell, direction octant) (launch_wf_order), so the rays a
+ * wave takes next start close together and head the same way — they walk
+ * the same subtrees (shared L2 lines, similar traversal lengths). The path
+ * math is the per-lane kernel's (slots bit-identical); only the order in
+ * which rays run changes. */
+PMD void wf_load(const TraceParams &P, uint32_t i, PathState &st) {
+    const float4 *q = P.wf_q_in + (size_t)i * WF_ENTRY_F4;
+    const float4 a = q[0], b = q[1], c = q[2];
+    st.ray.o = mk(a.x, a.y, a.z);
+    st.ray.tmin = a.w;
+    st.ray.tmax = RT_DEFAULT_MAX;
+    st.ray.d = mk(b.x, b.y, b.z);
+    st.pid = __float_as_uint(b.w);
+    st.alpha = mk(c.x, c.y, c.z);
+    const uint32_t w = __float_as_uint(c.w);
+    st.nI = w & 0xffu; st.stored = (w >> 8) & 0xffu; st.spec = w >> 16;
+    st.pslot = PSLOT_NONE;
+}
+PMD uint32_t wf_spread(uint32_t v) { /* 10 bits -> every third bit */
+    v = (v | (v << 16)) & 0x030000ffu;
+    v = (v | (v << 8)) & 0x0300f00fu;
+    v = (v | (v << 4)) & 0x030c30c3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+/* reorder key: Morton code of the origin's cell (2^wf_bits per axis over the
+ * scene box) above the direction octant */
+PMD uint32_t wf_sort_key(const TraceParams &P, v3 o, v3 d) {
+    const float top = (float)((1 << P.wf_bits) - 1);
+    const float v[3] = {o.x, o.y, o.z};
+    uint32_t c[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) c[a] = (uint32_t)fminf(fmaxf((v[a] - P.wf_lo[a]) * P.wf_scale[a], 0.f), top); /* NaN -> 0 */
+    const uint32_t oct = (d.x < 0.f ? 1u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 4u : 0u);
+    return ((wf_spread(c[0]) | (wf_spread(c[1]) << 1) | (wf_spread(c[2]) << 2)) << 3) | oct;
+}
+/* append the continuing path of every calling lane (wave-aggregated: one
+ * counter atomic per wave), with its reorder key and rank in the key's bin */
+PMD void wf_push(const TraceParams &P, const PathState &st) {
+    const unsigned long long m = __ballot(1);
+    const int lane = threadIdx.x & 63, leader = __builtin_ctzll(m);
+    uint32_t base = 0u;
+    if (lane == leader) base = atomicAdd(P.wf_n_out, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, leader);
+    const uint32_t i = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    float4 *q = P.wf_q_out + (size_t)i * WF_ENTRY_F4;
+    q[0] = make_float4(st.ray.o.x, st.ray.o.y, st.ray.o.z, st.ray.tmin);
+    q[1] = make_float4(st.ray.d.x, st.ray.d.y, st.ray.d.z, __uint_as_float(st.pid));
+    q[2] = make_float4(st.alpha.x, st.alpha.y, st.alpha.z, __uint_as_float(st.nI | (st.stored << 8) | (st.spec << 16)));
+    if (P.wf_bins) {
+        /* one bin atomic per distinct key of the wave (rays of one wave share
+         * keys once sorted: per-lane atomics serialize on the same word) */
+        const uint32_t k = wf_sort_key(P, st.ray.o, st.ray.d);
+        P.wf_key[i] = k;
+        unsigned long long pend = m;
+        uint32_t rank = 0u;
+        while (pend) {
+            const int l = __builtin_ctzll(pend);
+            const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane((int)k, l);
+            const unsigned long long same = __ballot(k == kk);
+            uint32_t b = 0u;
+            if (lane == l) b = atomicAdd(&P.wf_bins[kk], (uint32_t)__popcll(same));
+            b = (uint32_t)__shfl((int)b, l);
+            if (k == kk) rank = b + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+            pend &= ~same;
+        }
+        P.wf_rank[i] = rank;
+    }
+}
+
+template <int COUNT, int HOLD, int WF>
 /* 5 waves/SIMD: 96 VGPRs (102 unconstrained -> 4 waves), no scratch; with
  * the LDS stacks capped at 31 entries (PM_POOL_STACK, the rest spilled) five
  * 256-thread blocks fit a CU. C3 trace (same box): 4.59-4.61 ms at 4 waves,
@@ -689,8 +762,19 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
     TProf prof;
     uint32_t rays = 0, deposits = 0;
     const int64_t wave_id = ((int64_t)blockIdx.x * TRACE_BLOCK + tid) >> 6;
-    const int64_t wbegin = wave_id * P.wave_paths;
-    const int64_t wend = wbegin + P.wave_paths < P.path_count ? wbegin + P.wave_paths : P.path_count;
+    int64_t wbegin, wend;
+    if (WF == 2) {
+        /* the queue's rays in its (sorted) order, handed out dynamically: a
+         * refill takes the next run of positions from P.wf_next, so a wave's
+         * lanes get neighbouring rays and no wave is left with a static share
+         * of expensive ones (contiguous static pools of a sorted queue made
+         * the launch wait for the waves that drew the costly regions) */
+        wbegin = 0;
+        wend = (int64_t)*P.wf_n_in;
+    } else {
+        wbegin = wave_id * P.wave_paths;
+        wend = wbegin + P.wave_paths < P.path_count ? wbegin + P.wave_paths : P.path_count;
+    }
     int64_t cursor = wbegin; /* wave-uniform: next unassigned path of the pool */
     PathState st;
     TravState tr;
@@ -716,7 +800,16 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
             if (phase == PHASE_SHADE) {
                 ++rays;
                 bool alive = tr.best.ref != 0xffffffffu && path_shade<HOLD>(P, S, st, tr.best, prof, held);
-                if (alive) {
+                if (WF && alive) { /* the next bounce's launch continues the path */
+                    flush_rank(P, st);
+                    if (P.wf_q_out) {
+                        wf_push(P, st);
+                        phase = PHASE_DEAD;
+                    } else { /* past the last bounce a path can reach: never taken */
+                        finish_path<HOLD>(P, st, &held);
+                        phase = PHASE_DEAD;
+                    }
+                } else if (alive) {
                     trav_begin(st.ray, tr);
                     phase = PHASE_TRAV;
                 } else {
@@ -726,9 +819,18 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
                 }
             }
             const unsigned long long dm = __ballot(phase == PHASE_DEAD);
+            if (WF == 2 && cursor < wend && dm) {
+                uint32_t b = 0u;
+                if (lane == __builtin_ctzll(dm)) b = atomicAdd(P.wf_next, (uint32_t)__popcll(dm));
+                cursor = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)b, __builtin_ctzll(dm)));
+            }
             if (cursor < wend) {
                 const int64_t mine = cursor + __popcll(dm & ((1ull << lane) - 1ull));
-                if (phase == PHASE_DEAD && mine < wend) {
+                if (WF == 2 && phase == PHASE_DEAD && mine < wend) {
+                    wf_load(P, P.wf_perm ? P.wf_perm[mine] : (uint32_t)mine, st);
+                    trav_begin(st.ray, tr);
+                    phase = PHASE_TRAV;
+                } else if (phase == PHASE_DEAD && mine < wend) {
                     if (HOLD) held_clear(held);
                     const uint32_t pid = P.order ? (uint32_t)P.path_begin + P.order[mine] : (uint32_t)(P.path_begin + mine);
                     if (emit_path(P, S, perm, pid, st)) {
@@ -773,8 +875,8 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
 int trace_pool_waves_per_cu(size_t lds, int hold) { /* lds: stacks (+ nodelets) */
     int blocks = 0;
     if (hold) lds += (size_t)HOLD_WORDS * TRACE_BLOCK * 4;
-    const hipError_t e = hold ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0, 1>, TRACE_BLOCK, lds)
-                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0, 0>, TRACE_BLOCK, lds);
+    const hipError_t e = hold ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0, 1, 0>, TRACE_BLOCK, lds)
+                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0, 0, 0>, TRACE_BLOCK, lds);
     if (e != hipSuccess) return 0;
     return blocks * (TRACE_BLOCK / 64);
 }
@@ -826,6 +928,20 @@ hipError_t launch_path_order(const TraceParams &p, uint32_t *scratch, uint32_t *
     pm_launch(k_path_key, dim3(grid), dim3(256), 0, s, p, count, key, rank);
     if ((e = launch_exclusive_scan(count, nk, start, sums, s)) != hipSuccess) return e;
     pm_launch(k_path_fill, dim3(grid), dim3(256), 0, s, n, key, rank, start, order);
+    return hipGetLastError();
+}
+
+/* wavefront order: entry i of the queue goes to position start[key] + rank */
+__global__ __launch_bounds__(256) void k_wf_perm(const uint32_t *n, const uint32_t *key, const uint32_t *rank,
+                                                 const uint32_t *start, uint32_t *perm) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < *n) perm[start[key[i]] + rank[i]] = i;
+}
+hipError_t launch_wf_order(const uint32_t *n, uint32_t cap, uint32_t *bins, uint32_t nbins, uint32_t *start,
+                           uint32_t *sums, const uint32_t *key, const uint32_t *rank, uint32_t *perm, hipStream_t s) {
+    hipError_t e = launch_exclusive_scan_clear(bins, nbins, start, sums, s);
+    if (e != hipSuccess || cap == 0) return e;
+    pm_launch(k_wf_perm, dim3((cap + 255u) / 256u), dim3(256), 0, s, n, key, rank, start, perm);
     return hipGetLastError();
 }
 
@@ -891,10 +1007,17 @@ hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s) {
         const bool hold = trace_hold(p);
         const size_t lnl = (size_t)(PM_BVH4_QUANT ? p.S.nodelets : 0) * 64; /* nodelet bytes */
         const size_t lds_h = lds + (hold ? (size_t)HOLD_WORDS * TRACE_BLOCK * 4 : 0) + lnl;
-        if (count && hold) pm_launch((k_trace_pool<1, 1>), dim3(grid), dim3(TRACE_BLOCK), lds_h, s, q);
-        else if (count) pm_launch((k_trace_pool<1, 0>), dim3(grid), dim3(TRACE_BLOCK), lds + lnl, s, q);
-        else if (hold) pm_launch((k_trace_pool<0, 1>), dim3(grid), dim3(TRACE_BLOCK), lds_h, s, q);
-        else pm_launch((k_trace_pool<0, 0>), dim3(grid), dim3(TRACE_BLOCK), lds + lnl, s, q);
+        if (p.wf) { /* wavefront bounce: no held deposits (a path's state crosses launches) */
+            if (hold) return hipErrorInvalidValue;
+            if (count && p.wf == 1) pm_launch((k_trace_pool<1, 0, 1>), dim3(grid), dim3(TRACE_BLOCK), lds + lnl, s, q);
+            else if (count) pm_launch((k_trace_pool<1, 0, 2>), dim3(grid), dim3(TRACE_BLOCK), lds + lnl, s, q);
+            else if (p.wf == 1) pm_launch((k_trace_pool<0, 0, 1>), dim3(grid), dim3(TRACE_BLOCK), lds + lnl, s, q);
+            else pm_launch((k_trace_pool<0, 0, 2>), dim3(grid), dim3(TRACE_BLOCK), lds + lnl, s, q);
+        }
+        else if (count && hold) pm_launch((k_trace_pool<1, 1, 0>), dim3(grid), dim3(TRACE_BLOCK), lds_h, s, q);
+        else if (count) pm_launch((k_trace_pool<1, 0, 0>), dim3(grid), dim3(TRACE_BLOCK), lds + lnl, s, q);
+        else if (hold) pm_launch((k_trace_pool<0, 1, 0>), dim3(grid), dim3(TRACE_BLOCK), lds_h, s, q);
+        else pm_launch((k_trace_pool<0, 0, 0>), dim3(grid), dim3(TRACE_BLOCK), lds + lnl, s, q);
         return hipGetLastError();
     }
     if (p.per_block == 0) {

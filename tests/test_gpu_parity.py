@@ -73,6 +73,39 @@ def test_photon_trace_write_modes_bitexact(hold, sort, scene, oracle_mod, hip_mo
         ctx.close()
 
 
+@pytest.mark.parametrize("sort,bits", [("1", "4"), ("0", "4"), ("1", "0"), ("1", "7")])
+def test_wavefront_trace_bitexact(sort, bits, oracle_mod, hip_mod, monkeypatch):
+    """Wavefront mode of the pooled BVH trace (PM_TRACE_WAVEFRONT=1: one launch
+    per bounce, continuing rays queued and reordered by origin cell and
+    direction octant between bounces) writes the per-lane kernel's slots:
+    a 20K-triangle soup with a glass and a mirror sphere (specular chains
+    through the queue), every slot bit-exact vs the oracle, also for a shard
+    traced at a global path offset; map photons == valid slots."""
+    monkeypatch.setenv("PM_TRACE_WAVEFRONT", "1")
+    monkeypatch.setenv("PM_WF_SORT", sort)
+    monkeypatch.setenv("PM_WF_BITS", bits)
+    sc = scenes.triangle_soup(20000, 32, 32)
+    glass = sc.material(scenes.PM_GLASS, (1.0, 1.0, 1.0))
+    mirror = sc.material(scenes.PM_MIRROR, (0.9, 0.9, 0.9))
+    for (x, y, z), r, m in (((370.0, 100.0, 250.0), 100.0, glass), ((150.0, 90.0, 380.0), 90.0, mirror)):
+        o2w, w2o = scenes.translate(x, y, z)
+        sc.spheres.append((np.float32(r), o2w, w2o, m, -1))
+    ctx, orc = make_pair(sc, oracle_mod, hip_mod)
+    try:
+        paths = 32768
+        p = RenderParams.defaults(paths_per_pass=paths)
+        ref = orc.trace_photons(p, 1, 0, paths)
+        ctx.trace_photons(p, 1, 0, paths)
+        assert_bitexact(ctx.download_slots(paths * 4), ref, f"wavefront slots (sort={sort}, bits={bits})")
+        ctx.build_photon_map(p, paths * 4)
+        assert ctx.map_info()["valid"] == int((ref["bits"] & 1).sum()) > paths // 4
+        half = paths // 2
+        ctx.trace_photons(p, 1, half, half, slot_path_base=half)
+        assert_bitexact(ctx.download_slots(half * 4), ref[half * 4:], "wavefront shard")
+    finally:
+        ctx.close()
+
+
 def test_photon_trace_sharded_equals_whole(cornell):
     """Global path ids: two shards traced separately == one launch (owner-writes)."""
     ctx, orc = cornell
