@@ -334,6 +334,32 @@ PMD long long d2ll(double d) {
 #define TILE_STAT(k, v) do { } while (0)
 #endif
 
+/* PM_GATHER_PROFILE builds (make variant VFLAGS=-DPM_GATHER_PROFILE): wave
+ * clock (s_memtime) per phase of k_gather_tile, summed over waves into
+ * counters[8..14] (record, group, stage, test, hits, direct, store) and the
+ * wave count into counters[15] (tools/gather_profile.py). A phase's time
+ * includes the memory waits of the loads it first consumes. */
+struct GProf {
+#ifdef PM_GATHER_PROFILE
+    uint64_t last = 0, acc[7] = {0, 0, 0, 0, 0, 0, 0};
+    PMD void begin() { last = __builtin_amdgcn_s_memtime(); }
+    PMD void mark(int i) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        acc[i] += t - last;
+        last = t;
+    }
+    PMD void flush(unsigned long long *out) {
+        if (!out || (threadIdx.x & 63) != 0) return;
+        for (int i = 0; i < 7; ++i) atomicAdd(&out[8 + i], (unsigned long long)acc[i]);
+        atomicAdd(&out[15], 1ull);
+    }
+#else
+    PMD void begin() {}
+    PMD void mark(int) {}
+    PMD void flush(unsigned long long *) {}
+#endif
+};
+
 #ifdef PM_TILE_WAVES
 #define TILE_OCC __attribute__((amdgpu_waves_per_eu(PM_TILE_WAVES, PM_TILE_WAVES)))
 #else
@@ -445,6 +471,8 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
         r = P.rec_begin + gather_block(P) * TILE_BLOCK + threadIdx.x;
     }
     const GridDesc &g = P.grid;
+    GProf gp;
+    gp.begin();
     GatherRec R;
     R.load<PARTIAL>(P, r);
     /* a box of <= KR cells per axis takes part in the LDS groups; larger
@@ -473,6 +501,7 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
     bool direct = R.live && R.r2 > 0.f && !small; /* lanes that scan their own cells from global memory */
     const int group_min =
         (uint64_t)P.cell_start[g.ncells] * SPARSE_CELLS < (uint64_t)g.ncells ? GROUP_MIN_SPARSE : GROUP_MIN;
+    gp.mark(0);
     while (true) {
         const unsigned long long pm = __ballot(pend);
         if (pm == 0ull) break;
@@ -532,6 +561,7 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
             sK[k] = (uint32_t)k < nz ? s0 : 0u;
             eK[k] = (uint32_t)k < nz ? e0 : 0u;
         }
+        gp.mark(1);
         for (uint32_t T0 = 0; T0 < U; T0 += TILE_CAP) {
             const uint32_t n = min((uint32_t)TILE_CAP, U - T0);
             TILE_STAT(1, 1);
@@ -599,6 +629,7 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
             }
 #endif
             wave_lds_sync();
+            gp.mark(2);
             /* 3. each run of this lane within the window: LDS positions [base,
              * base + m). Tested two photons per packed instruction, 32
              * positions at a time, into hit masks; the hits of all runs are
@@ -703,6 +734,7 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
                     any |= bK[k];
                 }
                 M += nh;
+                gp.mark(3);
                 TILE_STAT(3, wave_max_u32(nh));
                 while (any) {
                     /* the first run with a hit left: its lowest position */
@@ -720,6 +752,7 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
                     }
                     hit(t);
                 }
+                gp.mark(4);
             }
             wave_lds_sync(); /* the window is read before the next one overwrites it */
         }
@@ -735,9 +768,13 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
             direct = true;
         }
     }
+    gp.mark(4);
     if (direct) lane_scan<0>(P, R.p, R.r2, R.ns, R.fv, R.x0, R.x1, R.y0, R.y1, R.z0, R.z1, M, Lf, nv, nr);
+    gp.mark(5);
     R.store<PARTIAL>(P, r, M, Lf);
     if (!PARTIAL && P.r2hist) r2_histogram(P, R.live, R.st.w);
+    gp.mark(6);
+    gp.flush(P.counters);
 }
 
 /* Wave-cooperative bucket gather. A wave's 64 records are one 8x8 pixel
