@@ -74,13 +74,48 @@ PMD bool in_radius(v3 p, float4 a, float r2) { /* gathering.cu:32-36 (DistanceSq
     return diff.x * diff.x + diff.y * diff.y + diff.z * diff.z < r2;
 }
 
+#ifndef PM_SCAN_PIPE
+#define PM_SCAN_PIPE 1
+#endif
+#ifndef PM_SCAN_BATCH
+#define PM_SCAN_BATCH 4 /* 6: 116 VGPRs, 8: 142 — the tile kernel drops to 4 / 3 waves per SIMD */
+#endif
 /* One lane scans its own cells [x0, x1] x [y0, y1] x [z0, z1] straight from
  * global memory: the census launches (their photons-tested count is the
  * per-record unit bench.py prices), lanes whose radius exceeds the grid's
  * design radius (uploaded records), and tiles whose row union is too wide for
- * k_gather_tile's LDS staging. Rows are read four photons at a time with all
- * eight row bounds loaded first. */
-template <int COUNT>
+ * k_gather_tile's LDS staging. All eight row bounds are loaded first; rows
+ * are read in software-pipelined batches (PIPE, the tile kernel's lanes: C3
+ * gather 0.51 -> 0.45 ms, C5 0.28 -> 0.25 ms, same box) or four photons at a
+ * time (the census / per-lane kernel, whose 64-VGPR budget the pipeline
+ * would spill). */
+/* the lane's rows, each one contiguous run [b, e) of photons, passed to RANGE(b, e) */
+#define PM_LANE_SCAN_CELLS(RANGE) \
+    if (y1 <= y0 + 1 && z1 <= z0 + 1) {                                                     \
+        /* all row bounds first: 8 independent loads in flight */                           \
+        uint32_t rb[4], re[4];                                                              \
+_Pragma("unroll")                                                                           \
+        for (int k = 0; k < 4; ++k) {                                                       \
+            const uint32_t cy = y0 + (k & 1), cz = z0 + (k >> 1);                           \
+            const bool use = cy <= y1 && cz <= z1;                                          \
+            const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;               \
+            rb[k] = use ? P.cell_start[row + x0] : 0u;                                      \
+            re[k] = use ? P.cell_start[row + x1 + 1] : 0u;                                  \
+            if (COUNT) { vis += re[k] - rb[k]; rows += use; }                               \
+        }                                                                                   \
+_Pragma("unroll")                                                                           \
+        for (int k = 0; k < 4; ++k) RANGE(rb[k], re[k]);                                    \
+    } else { /* radius above the grid's design radius (uploaded records) */                 \
+        for (uint32_t cz = z0; cz <= z1; ++cz)                                              \
+            for (uint32_t cy = y0; cy <= y1; ++cy) {                                        \
+                const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;           \
+                const uint32_t b = P.cell_start[row + x0], e = P.cell_start[row + x1 + 1];  \
+                if (COUNT) { vis += e - b; rows++; }                                        \
+                RANGE(b, e);                                                                \
+            }                                                                               \
+    }                                                                                       \
+    do { } while (0)
+template <int COUNT, int PIPE = PM_SCAN_PIPE>
 PMD void lane_scan(const GatherParams &P, v3 p, float r2, v3 ns, v3 fv, uint32_t x0, uint32_t x1, uint32_t y0,
                    uint32_t y1, uint32_t z0, uint32_t z1, int &M, Fx3 &Lf, unsigned long long &vis,
                    unsigned long long &rows) {
@@ -93,35 +128,53 @@ PMD void lane_scan(const GatherParams &P, v3 p, float r2, v3 ns, v3 fv, uint32_t
             add_hit(Lf, ns, fv, a, P.ph_b[2 * (size_t)j], phb[8 * (size_t)j + 4], sc);
         }
     };
-    auto range = [&](uint32_t j, const uint32_t e) {
-        for (; j + 4 <= e; j += 4) { /* 4 photon loads in flight */
-            const float4 a0 = P.ph_a[j], a1 = P.ph_a[j + 1], a2 = P.ph_a[j + 2], a3 = P.ph_a[j + 3];
-            photon(a0, j); photon(a1, j + 1); photon(a2, j + 2); photon(a3, j + 3);
-        }
-        for (; j < e; ++j) photon(P.ph_a[j], j);
-    };
-    if (y1 <= y0 + 1 && z1 <= z0 + 1) {
-        /* all row bounds first: 8 independent loads in flight */
-        uint32_t rb[4], re[4];
+    if constexpr (PIPE != 0) {
+        (void)photon;
+        constexpr int SB = PM_SCAN_BATCH;
+        /* batches of PM_SCAN_BATCH photons, software-pipelined: the next batch's positions
+         * are requested before this batch is tested, and the flux words of all
+         * of a batch's hits are requested together before any is summed — one
+         * memory round trip per batch instead of one for the positions plus one
+         * per hit (dense cells: C5's caustic, the soup's incoherent lanes) */
+        auto range = [&](uint32_t j, const uint32_t e) {
+            if (j >= e) return;
+            float4 a[SB];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t cy = y0 + (k & 1), cz = z0 + (k >> 1);
-            const bool use = cy <= y1 && cz <= z1;
-            const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
-            rb[k] = use ? P.cell_start[row + x0] : 0u;
-            re[k] = use ? P.cell_start[row + x1 + 1] : 0u;
-            if (COUNT) { vis += re[k] - rb[k]; rows += use; }
-        }
+            for (int i = 0; i < SB; ++i) a[i] = P.ph_a[min(j + (uint32_t)i, e - 1u)]; /* past e: masked below */
+            for (; j < e; j += SB) {
+                float4 cur[SB];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) range(rb[k], re[k]);
-    } else { /* radius above the grid's design radius (uploaded records) */
-        for (uint32_t cz = z0; cz <= z1; ++cz)
-            for (uint32_t cy = y0; cy <= y1; ++cy) {
-                const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
-                const uint32_t b = P.cell_start[row + x0], e = P.cell_start[row + x1 + 1];
-                if (COUNT) { vis += e - b; rows++; }
-                range(b, e);
+                for (int i = 0; i < SB; ++i) cur[i] = a[i];
+                if (j + (uint32_t)SB < e) {
+#pragma unroll
+                    for (int i = 0; i < SB; ++i) a[i] = P.ph_a[min(j + (uint32_t)SB + (uint32_t)i, e - 1u)];
+                }
+                uint32_t m = 0u;
+#pragma unroll
+                for (int i = 0; i < SB; ++i) m |= (j + (uint32_t)i < e && in_radius(p, cur[i], r2)) ? 1u << i : 0u;
+                float4 hb[SB];
+                float hc[SB];
+#pragma unroll
+                for (int i = 0; i < SB; ++i) {
+                    hb[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    hc[i] = 0.f;
+                    if (m & (1u << i)) { hb[i] = P.ph_b[2 * (size_t)(j + i)]; hc[i] = phb[8 * (size_t)(j + i) + 4]; }
+                }
+#pragma unroll
+                for (int i = 0; i < SB; ++i)
+                    if (m & (1u << i)) { M++; add_hit(Lf, ns, fv, cur[i], hb[i], hc[i], sc); }
             }
+        };
+        PM_LANE_SCAN_CELLS(range);
+    } else {
+        auto range = [&](uint32_t j, const uint32_t e) {
+            for (; j + 4 <= e; j += 4) { /* 4 photon loads in flight */
+                const float4 a0 = P.ph_a[j], a1 = P.ph_a[j + 1], a2 = P.ph_a[j + 2], a3 = P.ph_a[j + 3];
+                photon(a0, j); photon(a1, j + 1); photon(a2, j + 2); photon(a3, j + 3);
+            }
+            for (; j < e; ++j) photon(P.ph_a[j], j);
+        };
+        PM_LANE_SCAN_CELLS(range);
     }
 }
 
@@ -204,7 +257,7 @@ __global__ __launch_bounds__(GATHER_BLOCK, 8) void k_gather_grid(GatherParams P)
     int M = 0;
     Fx3 Lf{0, 0, 0};
     if (R.live && R.r2 > 0.f)
-        lane_scan<COUNT>(P, R.p, R.r2, R.ns, R.fv, R.x0, R.x1, R.y0, R.y1, R.z0, R.z1, M, Lf, vis, rows);
+        lane_scan<COUNT, 0>(P, R.p, R.r2, R.ns, R.fv, R.x0, R.x1, R.y0, R.y1, R.z0, R.z1, M, Lf, vis, rows);
     if (COUNT && R.live) { hits += (unsigned long long)M; act++; }
     R.store<PARTIAL>(P, r, M, Lf);
     if (COUNT) count4(P.counters, vis, hits, rows, act);
