@@ -1217,6 +1217,9 @@ constexpr int KT_CAP = PM_KT_CAP;  /* photons per LDS window (one per lane) */
 #ifndef PM_KT_BINS
 #define PM_KT_BINS 32
 #endif
+#ifndef PM_KT_PIPE
+#define PM_KT_PIPE 1
+#endif
 constexpr int KT_BINS = PM_KT_BINS; /* histogram bins per pass */
 #ifndef PM_KT_LIST
 #define PM_KT_LIST 12
@@ -1262,6 +1265,8 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
     const int64_t r = P.rec_begin + (P.tiles ? (int64_t)P.tiles[blockIdx.x] * 64 + lane
                                              : (int64_t)blockIdx.x * KNN_BLOCK + threadIdx.x);
     const GridDesc &g = P.grid;
+    GProf gp; /* PM_GATHER_PROFILE: record, pass setup, stage, test, hits, pass end, direct + store */
+    gp.begin();
     const int K = P.knn_k;
     const float maxd2 = P.knn_r2;
 #pragma unroll
@@ -1441,6 +1446,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
 
     const f2 px2 = {p.x, p.x}, py2 = {p.y, p.y}, pz2 = {p.z, p.z};
     bool pend = live, direct = false;
+    gp.mark(0);
     while (true) {
         const unsigned long long pm = __ballot(pend);
         if (pm == 0ull) break;
@@ -1549,6 +1555,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
                             if (hy) bits |= 2u << j;
                         }
                     }
+                    gp.mark(3);
                     if (decltype(DO_OTHER)::value) {
                         if (hl) bits = 0u;
                         TILE_STAT(4, wave_max_u32(__builtin_popcount(bits)));
@@ -1562,6 +1569,59 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
                     }
                 }
             };
+            gp.mark(1);
+#if PM_KT_PIPE
+            /* software-pipelined staging (one photon per lane per window):
+             * the next window's positions are requested before this window
+             * is written to LDS and tested, so a window's load round trip
+             * overlaps the previous window's tests; the flux words (SUM
+             * passes only) are requested at the start of their own window */
+            static_assert(KT_CAP == 64, "pipelined staging: one photon per lane per window");
+            const float *phb = reinterpret_cast<const float *>(P.ph_b);
+            /* photon index of this lane's position in window T0: its row from
+             * a max scan over the row-start marks; past the union -> the
+             * window's first photon (never read) */
+            auto window_index = [&](uint32_t T0) PM_INLINE {
+                L.mark[lane] = -1;
+                wave_lds_sync();
+                if (len > 0u) {
+                    if (pre >= T0 && pre < T0 + KT_CAP) L.mark[pre - T0] = lane;
+                    else if (pre < T0 && pre + len > T0) L.mark[0] = lane;
+                }
+                wave_lds_sync();
+                const int u = wave_incl_max_i32(L.mark[lane]);
+                const uint32_t gi = T0 + (uint32_t)lane + (uint32_t)__shfl((int)gofs, u);
+                const uint32_t g0 = (uint32_t)__builtin_amdgcn_readlane((int)gi, 0);
+                return (uint32_t)lane < min((uint32_t)KT_CAP, U - T0) ? gi : g0;
+            };
+            uint32_t jn = U > 0u ? window_index(0u) : 0u;
+            float4 pan = U > 0u ? P.ph_a[jn] : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (uint32_t T0 = 0; T0 < U; T0 += KT_CAP) {
+                const uint32_t n = min((uint32_t)KT_CAP, U - T0);
+                TILE_STAT(2, 1);
+                TILE_STAT(3, n);
+                const uint32_t j = jn;
+                const float4 pa = pan;
+                float4 qa = make_float4(0.f, 0.f, 0.f, 0.f);
+                float ca = 0.f;
+                if (flux) { qa = P.ph_b[2 * (size_t)j]; ca = phb[8 * (size_t)j + 4]; }
+                if (T0 + KT_CAP < U) {
+                    jn = window_index(T0 + KT_CAP);
+                    pan = P.ph_a[jn];
+                }
+                L.x[lane] = pa.x; L.y[lane] = pa.y; L.z[lane] = pa.z;
+                if (flux) { L.w[lane] = pa.w; L.b[lane] = qa; L.c[lane] = ca; }
+                wave_lds_sync();
+                gp.mark(2);
+                using T_ = std::true_type;
+                using F_ = std::false_type;
+                if (hist_any && other_any) window(n, T_{}, T_{});
+                else if (hist_any) window(n, T_{}, F_{});
+                else window(n, F_{}, T_{});
+                gp.mark(4);
+                wave_lds_sync(); /* the window is read before the next one overwrites it */
+            }
+#else
             for (uint32_t T0 = 0; T0 < U; T0 += KT_CAP) {
                 const uint32_t n = min((uint32_t)KT_CAP, U - T0);
                 TILE_STAT(2, 1);
@@ -1603,15 +1663,19 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
                     if (flux) { L.w[q] = pa[h].w; L.b[q] = qa[h]; L.c[q] = ca[h]; }
                 }
                 wave_lds_sync();
+                gp.mark(2);
                 using T_ = std::true_type;
                 using F_ = std::false_type;
                 if (hist_any && other_any) window(n, T_{}, T_{});
                 else if (hist_any) window(n, T_{}, F_{});
                 else window(n, F_{}, T_{});
+                gp.mark(4);
                 wave_lds_sync(); /* the window is read before the next one overwrites it */
             }
+#endif
             if (hl) S.cntf += cntf;
             if (act) finish();
+            gp.mark(5);
         }
     }
     /* lanes of incoherent tiles: the same passes over their own rows */
@@ -1669,6 +1733,8 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
         P.R.state[r] = make_float4(flux.x, flux.y, flux.z, S.md2);
         P.R.n[r] = (float)S.cnt;
     }
+    gp.mark(6);
+    gp.flush(P.counters);
 }
 
 hipError_t launch_gather_knn(const GatherParams &p, int count, hipStream_t s) {

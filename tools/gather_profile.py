@@ -1,4 +1,4 @@
-"""k_gather_tile phase clocks (PM_GATHER_PROFILE variant build) at C2 / C3 / C5:
+"""k_gather_tile (argument knn: k_gather_knn_tile) phase clocks (PM_GATHER_PROFILE variant build) at C2 / C3 / C5:
    make -C cuda-raytrace_amd variant NAME=gprof VFLAGS=-DPM_GATHER_PROFILE
    PMHIP_LIB=cuda-raytrace_amd/lib/variants/libpmhip_gprof.so python tools/gather_profile.py [c3|c5]
 Prints the summed wave clock per phase (record load, group forming + row
@@ -12,12 +12,16 @@ sys.path.insert(0, os.path.join(R, "cuda-raytrace_amd"))
 import torch  # noqa: F401
 from pmrender import hip, scenes
 from pmrender.abi import RenderParams
-C5, C3 = "c5" in sys.argv[1:], "c3" in sys.argv[1:]
+C5, C3, KNN = "c5" in sys.argv[1:], "c3" in sys.argv[1:], "knn" in sys.argv[1:]
 sc = (scenes.caustic_scene(1920, 1080) if C5 else
       scenes.triangle_soup(1_000_000, 1920, 1080) if C3 else scenes.cornell_box(1920, 1080))
 ctx = sc.load_into(hip.Context(0))
 PATHS = 1_048_576 if (C5 or C3) else 262144
-p = RenderParams.defaults(paths_per_pass=PATHS)
+if KNN:  # k_gather_knn_tile (BASELINE C2 kNN line: K = 50, maxD^2 = 100)
+    from pmrender.abi import PM_ESTIMATOR_KNN
+    p = RenderParams.defaults(paths_per_pass=PATHS, initial_radius2=100.0, estimator=PM_ESTIMATOR_KNN, knn_lookup=50)
+else:
+    p = RenderParams.defaults(paths_per_pass=PATHS)
 ctx.eye_pass(p)
 ctx.trace_photons(p, 0, 0, PATHS)
 ctx.build_photon_map(p, PATHS * 4)
@@ -28,9 +32,10 @@ for rep in range(2):
     ctx.gather(p)
     ctx.synchronize()
 v = list(ctx.trace_profile().values())
-names = ["record", "group", "stage", "test", "hits", "direct", "store"]
+names = (["record", "pass_setup", "stage", "test", "hits", "pass_end", "direct+store"] if KNN else
+         ["record", "group", "stage", "test", "hits", "direct", "store"])
 tot = sum(v[:7])
 waves = max(v[7], 1)
-print(f"{'c5' if C5 else 'c3' if C3 else 'c2'}: {waves} waves, {tot / waves:.0f} clocks per wave")
+print(f"{'c5' if C5 else 'c3' if C3 else 'c2'}{' knn' if KNN else ''}: {waves} waves, {tot / waves:.0f} clocks per wave")
 for k, x in zip(names, v[:7]):
     print(f"  {k:8s} {100.0 * x / max(tot, 1):6.1f} %  {x / waves:9.0f} per wave")
