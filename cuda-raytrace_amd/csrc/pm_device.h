@@ -733,6 +733,9 @@ struct SpillStack {
     }
     PMD int get(int i) const { return i < cap ? lds[i * stride] : spill[(size_t)(i - cap) * sstride + gid]; }
 };
+#ifndef PM_TRAV_FUSE
+#define PM_TRAV_FUSE 1
+#endif
 /* false once the ray is done (best holds its closest hit, if any) */
 template <class C>
 PMD bool trav_step(const SceneDev &S, const Ray &ray, TravState &T, const SpillStack &stk, C &cen,
@@ -740,7 +743,17 @@ PMD bool trav_step(const SceneDev &S, const Ray &ray, TravState &T, const SpillS
     if (T.l0n != 0) {
         leaf_isect<false, PM_BVH4_QUANT != 0>(S, T.l0s, T.l0n, ray, T.best, cen);
         T.l0s = T.l1s; T.l0n = T.l1n; T.l1s = T.l2s; T.l1n = T.l2n; T.l2s = T.l3s; T.l2n = T.l3n; T.l3n = 0;
+#if PM_TRAV_FUSE
+        /* the last pending leaf done: this step also visits the next node, so
+         * a lane's leaf tests share steps with node visits (the wave runs
+         * both codes whenever its lanes differ anyway). C3 trace per 1M paths
+         * 4.42-4.43 -> 4.07-4.10 ms (same box); also testing the first leaf a
+         * visit finds in the same step: 4.44 (the second leaf code costs every
+         * step) */
+        if (T.l0n != 0) return true;
+#else
         return T.l0n != 0 || T.cur >= 0;
+#endif
     }
     if (T.cur < 0 || T.guard > S.n_nodes) return false;
     ++T.guard;
