@@ -90,6 +90,8 @@ struct Ctx {
     int64_t slots_used = 0;
     /* photon buckets */
     DevBuf d_count, d_cell_start, d_scratch, d_pha, d_phb;
+    DevBuf d_knnpk, d_knnovf; /* kNN scalar stream: photon pairs, handed-back tiles (+ count) */
+    bool knn_ss = true;       /* kNN: k_gather_knn_ss first (PM_KNN_SS=0: k_gather_knn_tile alone) */
     struct { bool valid = false; int64_t n = 0; GridDesc grid{}; float r2 = 0.f; int64_t key_np = 0; int mpc = 1; } fused; /* counts made by the last trace (keys plane-major when key_np > 0) */
     GridDesc grid{};
     float grid_r2 = 0.f; /* radius^2 the photon map's grid is designed for */
@@ -759,6 +761,7 @@ int pm_create(void **out, const pm_config *cfg) {
         c->gather_kernel = !strcmp(e, "lane") ? PM_GK_LANE : !strcmp(e, "wave") ? PM_GK_WAVE : PM_GK_TILE;
     if (const char *e = getenv("PM_GATHER_WAVE")) if (atoi(e)) c->gather_kernel = PM_GK_WAVE;
     if (const char *e = getenv("PM_GATHER_XCD")) c->gather_xcd = atoi(e) != 0;
+    if (const char *e = getenv("PM_KNN_SS")) c->knn_ss = atoi(e) != 0;
     if (const char *e = getenv("PM_CELL_SPAN")) c->cell_span = std::max(2, std::min(5, atoi(e)));
     if (const char *e = getenv("PM_GRID_QUANTILE")) c->grid_quantile = atof(e);
     if (const char *e = getenv("PM_REC_ORDER")) c->rec_order_mode = atoi(e);
@@ -809,7 +812,7 @@ void pm_destroy(void *ptr) {
         }
     DevBuf *bufs[] = {&c->d_scene, &c->d_rays, &c->d_rand2d, &c->d_pos, &c->d_nrm, &c->d_state, &c->d_n,
                       &c->d_dl, &c->d_slots, &c->d_count, &c->d_scratch, &c->d_vflags, &c->d_vrank, &c->d_vlist, &c->d_vsums,
-                      &c->d_cell_start, &c->d_pha, &c->d_phb,
+                      &c->d_cell_start, &c->d_pha, &c->d_phb, &c->d_knnpk, &c->d_knnovf,
                       &c->d_kd, &c->d_out, &c->d_counters, &c->d_tiles, &c->d_tile_flags, &c->d_tile_count,
                       &c->d_r2hist, &c->d_order, &c->d_ocount, &c->d_ostart, &c->d_oscratch, &c->d_ostats,
                       &c->d_porder, &c->d_pscratch, &c->d_spill, &c->d_wfq, &c->d_wfw};
@@ -1712,7 +1715,34 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
         const double amax = c->emit_max * std::pow(c->kd_max, (double)p->max_photon_count) * 4.0;
         G.knn_fx = (float)(std::ldexp(1.0, 47) / std::max(amax, 1e-30));
         G.slots = c->d_slots.as<pm_photon>();
+        if (c->knn_ss && !c->counting && c->gather_kernel == PM_GK_TILE) {
+            const int64_t nph = (int64_t)(c->d_pha.bytes / 16), pairs = (nph + 1) / 2 + 16;
+            const int64_t ntiles = (G.rec_end - G.rec_begin + 63) / 64;
+            HIPCHK(c, c->d_knnpk.ensure((size_t)pairs * 80));
+            HIPCHK(c, c->d_knnovf.ensure((size_t)(ntiles + KNN_OVF_HDR) * 4));
+            G.knn_pk_p = c->d_knnpk.as<float4>();
+            G.knn_pk_q = G.knn_pk_p + 2 * pairs;
+            G.knn_pk_pairs = pairs;
+            G.knn_ovf_n = c->d_knnovf.as<uint32_t>();
+            G.knn_ovf = G.knn_ovf_n + KNN_OVF_HDR;
+        }
         HIPCHK(c, launch_gather_knn(G, c->counting, s));
+        if (G.knn_ovf_n && getenv("PM_KNN_SS_DEBUG")) { /* tiles handed back to k_gather_knn_tile */
+            uint32_t nb = 0;
+            HIPCHK(c, hipMemcpyAsync(&nb, G.knn_ovf_n, 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            fprintf(stderr, "pm knn_ss: %u of %lld tiles handed back\n", nb, (long long)(G.tiles ? G.n_tiles : (G.rec_end - G.rec_begin + 63) / 64));
+            std::vector<uint32_t> hdr(KNN_OVF_HDR);
+            HIPCHK(c, hipMemcpy(hdr.data(), G.knn_ovf_n, KNN_OVF_HDR * 4, hipMemcpyDeviceToHost));
+            if (hdr[1] || hdr[2]) { /* PM_KNN_SS_DBG builds */
+                fprintf(stderr, "pm knn_ss dbg: %u bad collects, %u NaN radii\n", hdr[1], hdr[2]);
+                for (uint32_t i = 0; i < std::min<uint32_t>(hdr[1], 60); ++i) {
+                    fprintf(stderr, "  ");
+                    for (int w = 0; w < 16; ++w) fprintf(stderr, " %u", hdr[64 + 16 * i + w]);
+                    fprintf(stderr, "\n");
+                }
+            }
+        }
     } else {
         if (p->gather_structure == PM_GATHER_KDTREE) HIPCHK(c, hipMemsetAsync(G.error, 0, 4, s));
         HIPCHK(c, launch_gather(G, p->gather_structure, partial != nullptr || split, c->counting, s));

@@ -1259,6 +1259,11 @@ struct KnnLds {
 #define PM_INLINE __attribute__((always_inline))
 enum { KP_DONE = 0, KP_HIST = 1, KP_COLLECT = 2, KP_MIN = 3, KP_SUM = 4 };
 PMD float next_up(float x) { return __uint_as_float(__float_as_uint(x) + 1u); } /* x >= 0, finite */
+/* wave-uniform vector loads through the scalar cache (k_gather_knn_ss) */
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef const f32x16 __attribute__((address_space(4), aligned(4))) sv16;
+typedef const f32x8 __attribute__((address_space(4), aligned(4))) sv8;
 /* per-record fixed-point scale: the power of two below knn_fx * r_k^2 */
 PMD float knn_scale(float fx, float md2) {
     return md2 == 0.f ? 1.f : __uint_as_float(__float_as_uint(fx * md2) & 0xff800000u);
@@ -1757,15 +1762,412 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
     gp.flush(P.counters);
 }
 
+/* ---------------------------------------------------------------------- */
+/* kNN scalar-stream kernel (round 4, the default kNN path): the estimate of
+ * k_gather_knn_tile / k_gather_knn bit for bit, with the photons streamed
+ * through the scalar cache instead of staged into LDS.
+ *  - A wave (one 8x8 tile) forms the same groups as k_gather_knn_tile. Per
+ *    pass it walks the rows of the union box of its lanes' bounds; a row is a
+ *    contiguous run of the cell-sorted photons, read as photon PAIRS
+ *    (k_knn_pack: x0 x1 | y0 y1 | z0 z1 | wx0 wx1 ...) with s_load, so one
+ *    SGPR pair is the wave-uniform operand of a packed v_pk_* instruction and
+ *    every lane tests both photons of the pair against its own record. No
+ *    staging, no index mapping, no LDS traffic for the photons at all.
+ *  - r_k^2 by radix-style histograms on the d^2 BIT PATTERNS (a non-negative
+ *    float orders like its bits): bin = min(sat(bits - A) >> sh, 32), 32 bins
+ *    + a sink per lane in LDS (one ds_add per photon, no conversions, exact
+ *    bin edges). Level 0 covers the two octaves below maxD^2 at 1/16 octave
+ *    (bin 0 also takes everything nearer); the bin holding the K-th value is
+ *    COLLECTed into a per-lane list (<= 12) and ranked, or, when it holds
+ *    more, histogrammed again at 32x the resolution (or, for a dense lane
+ *    whose K-th is in bin 0, over all of [0, hi) in 4-octave bins).
+ *  - SUM: every lane adds, for each pair, the pbrt kernel terms of the
+ *    photons below its r_k^2 that face it, in the record's fixed point
+ *    (rint, exact double sums: order-free), masked per lane; a pair no lane
+ *    hits costs only its distance test.
+ *  - Passes are phase-serialised per wave (HIST before COLLECT before SUM),
+ *    so each pass runs one specialised loop.
+ * A tile this kernel does not handle — a lane group whose union box exceeds
+ * the 64-row map, r_k^2 = 0 (pbrt's 0/0 and its lowest-slot ties) — is
+ * appended to P.knn_ovf and re-run by k_gather_knn_tile. */
+constexpr int KS_NB = 32;   /* bins per histogram level (+1 sink) */
+constexpr int KS_LIST = 12; /* values a COLLECT keeps per lane (rows 0..KS_LIST of the histogram, +1 scratch) */
+enum { KS_HIST = 0, KS_COLLECT = 1, KS_SUM = 2, KS_DONE = 3 };
+static_assert(KS_LIST + 1 <= KS_NB, "the COLLECT list aliases histogram rows");
+
+/* photon pairs of the bucket order for the scalar stream: pair k = photons
+ * 2k, 2k + 1, P block (x x y y z z wx wx), Q block (r r g g b b wy wy wz wz
+ * . .); photons past the map are zero (the stream masks them). Block 0
+ * thread 0 also clears the overflow-tile counter of this gather. */
+__global__ __launch_bounds__(256) void k_knn_pack(const uint32_t *cell_start, uint32_t ncells, const float4 *ph_a,
+                                                  const float4 *ph_b, float4 *pk_p, float4 *pk_q, int64_t npairs,
+                                                  uint32_t *ovf_n) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k < 64 && ovf_n) ovf_n[k] = 0u;
+    if (k >= npairs) return;
+    const int64_t n = cell_start[ncells], j = 2 * k;
+    if (j >= n + 16) return; /* a few zero pairs past the map: never read unmasked */
+    float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, b0 = a0, b1 = a0;
+    float c0 = 0.f, c1 = 0.f;
+    if (j < n) { a0 = ph_a[j]; b0 = ph_b[2 * j]; c0 = ph_b[2 * j + 1].x; }
+    if (j + 1 < n) { a1 = ph_a[j + 1]; b1 = ph_b[2 * j + 2]; c1 = ph_b[2 * j + 3].x; }
+    pk_p[2 * k] = make_float4(a0.x, a1.x, a0.y, a1.y);
+    pk_p[2 * k + 1] = make_float4(a0.z, a1.z, a0.w, a1.w);
+    pk_q[3 * k] = make_float4(b0.x, b1.x, b0.y, b1.y);
+    pk_q[3 * k + 1] = make_float4(b0.z, b1.z, b0.w, b1.w);
+    pk_q[3 * k + 2] = make_float4(c0, c1, 0.f, 0.f);
+}
+
+
+__global__ __launch_bounds__(64) void k_gather_knn_ss(GatherParams P) {
+    __shared__ uint32_t H[(KS_NB + 1) * 64]; /* [bin][lane]; bin KS_NB = sink */
+    const int lane = threadIdx.x & 63;
+    if (P.tiles && P.n_tiles_dev && (int64_t)blockIdx.x >= (int64_t)*P.n_tiles_dev) return;
+    const uint32_t tile = P.tiles ? P.tiles[blockIdx.x] : blockIdx.x;
+    const int64_t r = P.rec_begin + (int64_t)tile * 64 + lane;
+    const int K = P.knn_k;
+    const float maxd2 = P.knn_r2;
+#pragma unroll
+    for (int b = 0; b <= KS_NB; ++b) H[b * 64 + lane] = 0u;
+    bool active = false, live = false, back = false;
+    float4 pos = make_float4(0.f, 0.f, 0.f, 0.f), nrm = pos;
+    if (r < P.rec_end) {
+        pos = P.R.pos[r];
+        const uint32_t flags = (uint32_t)__float_as_int(pos.w);
+        active = !(flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID));
+        back = (flags & PM_REC_BACKFACE) != 0;
+        if (active) {
+            nrm = P.R.nrm[r];
+            live = __float_as_int(P.materials[__float_as_int(nrm.w)].w) == PM_MATTE; /* non-specular BSDF only */
+        }
+    }
+    const v3 p = xyz(pos);
+    /* Faceforward folded into the normal: Dot(-n, w) = -Dot(n, w) exactly */
+    const float nsx = back ? -nrm.x : nrm.x, nsy = back ? -nrm.y : nrm.y, nsz = back ? -nrm.z : nrm.z;
+    const GridDesc g = P.grid;
+    uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0, z0 = 0, z1 = 0;
+    if (live) { /* KnnGrid::init's cells */
+        const float rq = sqrtf(maxd2) * 1.0001f + 1e-4f;
+        x0 = cell_axis(p.x - rq, g.gx, g.inv_cs, g.dx); x1 = cell_axis(p.x + rq, g.gx, g.inv_cs, g.dx);
+        y0 = cell_axis(p.y - rq, g.gy, g.inv_cs, g.dy); y1 = cell_axis(p.y + rq, g.gy, g.inv_cs, g.dy);
+        z0 = cell_axis(p.z - rq, g.gz, g.inv_cs, g.dz); z1 = cell_axis(p.z + rq, g.gz, g.inv_cs, g.dz);
+    }
+    /* selection state: HIST level (A, sh) counts the values below
+     * A + (32 << sh) (bin 0 includes everything below A + (1 << sh)) */
+    const uint32_t Bm = __float_as_uint(maxd2);
+    uint32_t sh = 19u;
+    while (sh > 0u && (32u << sh) > Bm) --sh;
+    uint32_t A = Bm - (32u << sh);
+    /* lowopen: bin 0 also holds everything below A (level 0, before any
+     * refinement); otherwise the K-th is known to be >= A and `base` values
+     * lie below A (bin 0 counts them too: every histogram counts global ranks) */
+    uint32_t base = 0u;
+    int phase = live ? KS_HIST : KS_DONE;
+    bool lvl0 = true, full = true, defer = false, lowopen = true;
+    uint32_t klo = 0u, kw = 0u, cc = 0u;
+    int need = 0, less = 0, cnt = 0;
+    float md2 = maxd2, inv = 0.f, sc = 1.f;
+    Dx3 acc{0, 0, 0};
+
+    const const_f32_ptr pkp = (const_f32_ptr)P.knn_pk_p;
+    const const_f32_ptr pkq = (const_f32_ptr)P.knn_pk_q;
+    const f2 px2 = {p.x, p.x}, py2 = {p.y, p.y}, pz2 = {p.z, p.z};
+    bool pend = live;
+    while (!defer) {
+        const unsigned long long pm = __ballot(pend);
+        if (pm == 0ull) break;
+        /* the group: every pending lane if their union box fits the 64-lane
+         * row map, else the first pending lane's neighbourhood */
+        uint32_t X0, X1, Y0, Y1, Z0, Z1;
+        bool mine = pend;
+        union_box6(g, mine, x0, x1, y0, y1, z0, z1, X0, X1, Y0, Y1, Z0, Z1);
+        uint32_t LY = Y1 > Y0 ? 32u - (uint32_t)__builtin_clz(Y1 - Y0) : 0u;
+        if (LY > 6u || ((uint64_t)(Z1 - Z0 + 1u) << LY) > 64u) {
+            const int leader = __builtin_ctzll(pm);
+            const uint32_t lx = __builtin_amdgcn_readlane(x0, leader), ly = __builtin_amdgcn_readlane(y0, leader),
+                           lz = __builtin_amdgcn_readlane(z0, leader);
+            mine = pend && x0 + KT_GROUP_R - lx <= 2u * KT_GROUP_R && y0 + KT_GROUP_R - ly <= 2u * KT_GROUP_R &&
+                   z0 + KT_GROUP_R - lz <= 2u * KT_GROUP_R;
+            union_box6(g, mine, x0, x1, y0, y1, z0, z1, X0, X1, Y0, Y1, Z0, Z1);
+            LY = Y1 > Y0 ? 32u - (uint32_t)__builtin_clz(Y1 - Y0) : 0u;
+            if (LY > 6u || ((uint64_t)(Z1 - Z0 + 1u) << LY) > 64u) { defer = true; break; } /* grid too coarse */
+        }
+        pend = pend && !mine;
+        /* passes until every lane of the group has its estimate (a level
+         * descends 5 bits or slides to [0, hi): far fewer than 64 passes;
+         * the bound only guarantees that every wave ends) */
+        for (int npass = 0;; ++npass) {
+            if (npass == 64) { defer = true; break; }
+            const bool in = mine && phase != KS_DONE;
+            const unsigned long long mh = __ballot(in && phase == KS_HIST), mc = __ballot(in && phase == KS_COLLECT),
+                                     ms = __ballot(in && phase == KS_SUM);
+            if ((mh | mc | ms) == 0ull) break;
+            const int pt = mh ? KS_HIST : (mc ? KS_COLLECT : KS_SUM);
+            const bool act = in && phase == pt;
+            /* this lane's bound (every value the pass needs is below it) */
+            float bnd = 0.f;
+            if (act) {
+                if (pt == KS_HIST) { /* the level's upper edge A + (32 << sh), at most maxD^2 */
+                    const uint64_t ub = (uint64_t)A + ((uint64_t)32u << sh);
+                    bnd = ub >= (uint64_t)Bm ? maxd2 : __uint_as_float((uint32_t)ub);
+                }
+                else if (pt == KS_COLLECT) bnd = __uint_as_float(klo + kw);
+                else bnd = full ? next_up(md2) : md2;
+            }
+            /* the pass's union: cells of [p - r', p + r'], r'^2 = bnd: a
+             * sub-box of the group's (bnd <= maxD^2), so it fits the row map */
+            uint32_t a0 = 0, a1 = 0, b0 = 0, b1 = 0, c0 = 0, c1 = 0;
+            if (act) {
+                const float rq = sqrtf(bnd) * 1.0001f + 1e-4f;
+                a0 = cell_axis(p.x - rq, g.gx, g.inv_cs, g.dx); a1 = cell_axis(p.x + rq, g.gx, g.inv_cs, g.dx);
+                b0 = cell_axis(p.y - rq, g.gy, g.inv_cs, g.dy); b1 = cell_axis(p.y + rq, g.gy, g.inv_cs, g.dy);
+                c0 = cell_axis(p.z - rq, g.gz, g.inv_cs, g.dz); c1 = cell_axis(p.z + rq, g.gz, g.inv_cs, g.dz);
+            }
+            uint32_t PX0, PX1, PY0, PY1, PZ0, PZ1;
+            union_box6(g, act, a0, a1, b0, b1, c0, c1, PX0, PX1, PY0, PY1, PZ0, PZ1);
+            const uint32_t PLY = PY1 > PY0 ? 32u - (uint32_t)__builtin_clz(PY1 - PY0) : 0u;
+            /* union row u = lane: photons [Bu, Bu + Lu) of cells PX0..PX1 */
+            uint32_t Bu = 0u, Lu = 0u;
+            {
+                const uint32_t cy = PY0 + ((uint32_t)lane & ((1u << PLY) - 1u)), cz = PZ0 + ((uint32_t)lane >> PLY);
+                if (cy <= PY1 && cz <= PZ1) {
+                    const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+                    Bu = P.cell_start[row + PX0];
+                    Lu = P.cell_start[row + PX1 + 1u] - Bu;
+                }
+            }
+            unsigned long long rows = __ballot(Lu > 0u);
+#ifdef PM_KNN_SS_DBG
+            const unsigned long long rows0 = rows;
+#endif
+            /* per-lane constants of the pass (lanes outside it never hit) */
+            const uint32_t hA = act ? A : 0u, hsh = act ? sh : 0u, hlo = act ? 0u : (uint32_t)KS_NB;
+            const uint32_t clo = act ? klo : 0u, cw = act ? kw : 0u;
+            const float smd = act ? md2 : -1.f, sinv = inv, ssc = sc;
+            const f2 inv2 = {sinv, sinv}, sc2 = {ssc, ssc}, one2 = {1.f, 1.f}, c3 = {3.f * INV_PI, 3.f * INV_PI};
+            const f2 nx2 = {nsx, nsx}, ny2 = {nsy, nsy}, nz2 = {nsz, nsz};
+            uint32_t *hcol = H + lane;
+            /* COLLECT: the lane's list rows (lanes outside the pass write the sink row) */
+            uint32_t *lcol = hcol + (act ? 0 : KS_NB * 64);
+            uint32_t ccl = 0u;
+            /* one specialised loop per pass type over the rows' photon pairs */
+            /* one specialised loop per pass type over the rows' photon pairs,
+             * NP pairs per batch: the batch's s_loads are issued together and
+             * waited on once (the scalar cache returns out of order, so a wave
+             * cannot wait for an older load while a younger one is in flight) */
+            auto stream = [&](auto PT_) PM_INLINE {
+                constexpr int PT = decltype(PT_)::value;
+                constexpr int NP = PT == KS_SUM ? 2 : 4;
+                unsigned long long rm = rows;
+                while (rm) {
+                    const int u = __builtin_ctzll(rm);
+                    rm &= rm - 1ull;
+                    const uint32_t b = uniform_u32(__builtin_amdgcn_readlane(Bu, u));
+                    const uint32_t e = b + uniform_u32(__builtin_amdgcn_readlane(Lu, u));
+                    const uint32_t k1 = (e + 1u) >> 1;
+                    for (uint32_t k0 = b >> 1; k0 < k1; k0 += NP) {
+                        /* the batch (reads past the run stay inside the packed
+                         * buffer's zero pairs; their photons are never counted) */
+                        /* whole-vector loads: one s_load_dwordx16 per 64 B, none of
+                         * them sunk into the per-pair branches below */
+                        float pv[NP][8], qv[PT == KS_SUM ? NP : 1][12];
+                        const sv16 *q = (const sv16 *)(pkp + 8 * (size_t)k0);
+                        if constexpr (PT == KS_SUM) {
+                            static_assert(NP == 2, "one P vector + 24 Q floats per batch");
+                            f32x16 v = q[0], a = ((const sv16 *)(pkq + 12 * (size_t)k0))[0];
+                            f32x8 c8 = ((const sv8 *)(pkq + 12 * (size_t)k0 + 16))[0];
+                            asm volatile("" : "+s"(v), "+s"(a), "+s"(c8)); /* the whole batch, one wait */
+#pragma unroll
+                            for (int c = 0; c < 16; ++c) pv[c / 8][c % 8] = v[c];
+#pragma unroll
+                            for (int c = 0; c < 12; ++c) qv[0][c] = a[c];
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) qv[1][c] = a[12 + c];
+#pragma unroll
+                            for (int c = 0; c < 8; ++c) qv[1][4 + c] = c8[c];
+                        } else {
+                            static_assert(NP == 4, "two P vectors per batch");
+                            f32x16 v0 = q[0], v1 = q[1];
+                            asm volatile("" : "+s"(v0), "+s"(v1)); /* the whole batch, one wait */
+#pragma unroll
+                            for (int c = 0; c < 16; ++c) { pv[c / 8][c % 8] = v0[c]; pv[2 + c / 8][c % 8] = v1[c]; }
+                        }
+#pragma unroll
+                        for (int i = 0; i < NP; ++i) {
+                            const uint32_t k = k0 + (uint32_t)i;
+                            if (i > 0 && k >= k1) break;
+                            f2 X = {pv[i][0], pv[i][1]};
+                            const f2 Y = {pv[i][2], pv[i][3]}, Z = {pv[i][4], pv[i][5]};
+                            /* the run's ends: a half pair outside [b, e) is pushed to infinity */
+                            if (2u * k < b) X.x = INFINITY;
+                            if (2u * k + 1u >= e) X.y = INFINITY;
+                            const f2 dx = px2 - X, dy = py2 - Y, dz = pz2 - Z;
+                            const f2 d2 = (dx * dx + dy * dy) + dz * dz; /* in_radius / KnnGrid::scan's order */
+                            const uint32_t u0 = __float_as_uint(d2.x), u1 = __float_as_uint(d2.y);
+                            if constexpr (PT == KS_HIST) {
+                                const uint32_t h0 = min(max(__builtin_elementwise_sub_sat(u0, hA) >> hsh, hlo), (uint32_t)KS_NB);
+                                const uint32_t h1 = min(max(__builtin_elementwise_sub_sat(u1, hA) >> hsh, hlo), (uint32_t)KS_NB);
+                                atomicAdd(hcol + h0 * 64u, 1u);
+                                atomicAdd(hcol + h1 * 64u, 1u);
+                            } else if constexpr (PT == KS_COLLECT) {
+                                lcol[ccl * 64u] = u0;
+                                ccl += (u0 - clo) < cw ? 1u : 0u;
+                                lcol[ccl * 64u] = u1;
+                                ccl += (u1 - clo) < cw ? 1u : 0u;
+                            } else {
+                                const f2 WX = {pv[i][6], pv[i][7]}, R = {qv[i][0], qv[i][1]}, G = {qv[i][2], qv[i][3]};
+                                const f2 Bl = {qv[i][4], qv[i][5]}, WY = {qv[i][6], qv[i][7]}, WZ = {qv[i][8], qv[i][9]};
+                                const bool h0 = d2.x < smd, h1 = d2.y < smd;
+                                less += (int)h0 + (int)h1;
+                                if (__ballot(h0 || h1)) {
+                                    const f2 dn = (nx2 * WX + ny2 * WY) + nz2 * WZ; /* knn_facing */
+                                    /* knn_add: s = 1 - d^2 / r_k^2, kernel 3/pi s^2, times 1/r_k^2 and alpha;
+                                     * a photon that does not count gets ki = 0, so every term of it is rint(0) = 0 */
+                                    const f2 sv = one2 - d2 * inv2;
+                                    f2 ki = ((c3 * sv) * sv) * inv2;
+                                    if (!(h0 && dn.x > 0.f)) ki.x = 0.f;
+                                    if (!(h1 && dn.y > 0.f)) ki.y = 0.f;
+                                    const f2 cr = (ki * R) * sc2, cg = (ki * G) * sc2, cb = (ki * Bl) * sc2;
+                                    acc.x += (double)rintf(cr.x) + (double)rintf(cr.y);
+                                    acc.y += (double)rintf(cg.x) + (double)rintf(cg.y);
+                                    acc.z += (double)rintf(cb.x) + (double)rintf(cb.y);
+                                }
+                            }
+                        }
+                    }
+                }
+            };
+            if (pt == KS_HIST) stream(std::integral_constant<int, KS_HIST>{});
+            else if (pt == KS_COLLECT) stream(std::integral_constant<int, KS_COLLECT>{});
+            else stream(std::integral_constant<int, KS_SUM>{});
+            if (!act) continue;
+            if (pt == KS_HIST) {
+                /* the bin holding the K-th value; the column is left zeroed */
+                uint32_t cum = 0u, below = 0u, cntb = 0u;
+                int bs = -1;
+#pragma unroll
+                for (int bb = 0; bb < KS_NB; ++bb) {
+                    const uint32_t c = hcol[bb * 64];
+                    hcol[bb * 64] = 0u;
+                    if (bs < 0 && cum + c >= (uint32_t)K) { bs = bb; below = cum; cntb = c; }
+                    cum += c;
+                }
+                hcol[KS_NB * 64] = 0u;
+                if (lvl0 && cum < (uint32_t)K) { /* fewer than K inside maxD: r_k^2 = maxD^2 */
+                    full = false;
+                    md2 = maxd2;
+                    phase = KS_SUM;
+                } else {
+                    lvl0 = false;
+                    /* the K-th value's bin [lo, hi): bin 0 of an open level
+                     * starts at 0; bin 0 of a refined level holds the base
+                     * values below A as well, which are not in [A, hi) */
+                    const bool open0 = bs == 0 && lowopen && A != 0u;
+                    const uint32_t lo = open0 ? 0u : A + ((uint32_t)bs << sh), hi = A + ((uint32_t)(bs + 1) << sh);
+                    if (bs == 0 && !open0) { cntb -= base; below = base; }
+                    if (sh == 0u && !open0) { /* a bin of one bit pattern */
+                        md2 = __uint_as_float(lo);
+                        phase = KS_SUM;
+                    } else if (cntb <= (uint32_t)KS_LIST) {
+                        phase = KS_COLLECT;
+                        klo = lo; kw = hi - lo; need = K - (int)below; cc = 0u;
+                    } else if (!open0) { /* 32x finer over the bin */
+                        A = lo;
+                        base = below;
+                        sh = sh >= 5u ? sh - 5u : 0u;
+                    } else { /* the K-th is below A + 2^sh (a dense lane): the 32 bins
+                               * slide down to end at hi, 4x wider (8 octaves at 1/4 octave) */
+                        const uint32_t sh2 = min(sh + 2u, 26u);
+                        A = hi > (32u << sh2) ? hi - (32u << sh2) : 0u;
+                        base = 0u;
+                        sh = sh2;
+                    }
+                    lowopen = open0 && A != 0u && cntb > (uint32_t)KS_LIST;
+                }
+            } else if (pt == KS_COLLECT) {
+                cc = ccl;
+                /* rank the kept values (cc of them): the need-th smallest */
+                uint32_t v[KS_LIST];
+#pragma unroll
+                for (int a = 0; a < KS_LIST; ++a) v[a] = (uint32_t)a < cc ? hcol[a * 64] : 0xffffffffu;
+#pragma unroll
+                for (int a = 0; a <= KS_LIST; ++a) hcol[a * 64] = 0u;
+                uint32_t ans = v[0];
+#pragma unroll
+                for (int a = 0; a < KS_LIST; ++a) {
+                    int lt = 0, le = 0;
+#pragma unroll
+                    for (int bb = 0; bb < KS_LIST; ++bb) { lt += v[bb] < v[a]; le += v[bb] <= v[a]; }
+                    if ((uint32_t)a < cc && lt < need && need <= le) ans = v[a];
+                }
+                md2 = __uint_as_float(ans);
+                phase = KS_SUM;
+                if (md2 == 0.f) defer = true; /* pbrt's 0/0: k_gather_knn_tile's tie rules */
+#ifdef PM_KNN_SS_DBG
+                if (ans == 0xffffffffu) {
+                    const uint32_t i = atomicAdd(P.knn_ovf_n + 1, 1u);
+                    if (i < 60u) {
+                        uint32_t *d = P.knn_ovf_n + 64 + 16 * i;
+                        d[0] = tile; d[1] = lane; d[2] = cc; d[3] = (uint32_t)need; d[4] = klo; d[5] = kw; d[6] = A;
+                        d[7] = sh; d[8] = __float_as_uint(p.x); d[9] = __float_as_uint(p.y); d[10] = __float_as_uint(p.z);
+                        d[11] = PX0; d[12] = PX1; d[13] = PY0 | (PY1 << 16); d[14] = PZ0 | (PZ1 << 16); d[15] = (uint32_t)__popcll(rows0);
+                    }
+                }
+#endif
+            }
+            if (phase == KS_SUM && pt != KS_SUM) { /* begin_sum */
+                sc = knn_scale(P.knn_fx, md2);
+                inv = 1.f / md2;
+                acc = Dx3{0, 0, 0};
+                less = 0;
+            } else if (pt == KS_SUM) {
+                cnt = full ? K : less;
+                phase = KS_DONE;
+            }
+        }
+        if (__ballot(defer)) defer = true;
+    }
+    if (__ballot(defer)) { /* re-run by k_gather_knn_tile */
+        if (lane == 0) P.knn_ovf[atomicAdd(P.knn_ovf_n, 1u)] = tile;
+        return;
+    }
+#ifdef PM_KNN_SS_DBG
+    if (active && md2 != md2) atomicAdd(P.knn_ovf_n + 2, 1u);
+#endif
+    if (active) {
+        if (!live) md2 = maxd2; /* specular: nothing found, cnt 0 */
+        const float4 st = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : P.R.state[r];
+        const double isc = 1.0 / (double)sc;
+        const v3 Lr = mk((float)(acc.x * isc), (float)(acc.y * isc), (float)(acc.z * isc));
+        const v3 flux = xyz(st) + Lr;
+        P.R.state[r] = make_float4(flux.x, flux.y, flux.z, md2);
+        P.R.n[r] = (float)cnt;
+    }
+}
+
 hipError_t launch_gather_knn(const GatherParams &p, int count, hipStream_t s) {
     if (p.rec_end <= p.rec_begin) return hipSuccess;
     if (p.knn_k < 1 || p.knn_k > PM_KNN_MAX) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)((p.rec_end - p.rec_begin + KNN_BLOCK - 1) / KNN_BLOCK);
     /* census launches run the per-lane kernel (its photons-tested count is the
-     * per-record unit bench.py prices); the tile kernel finds the same set */
+     * per-record unit bench.py prices); the tile kernels find the same set */
     if (!count && p.kernel == PM_GK_TILE) {
         const unsigned g = p.tiles ? (unsigned)p.n_tiles : grid;
-        if (g) pm_launch(k_gather_knn_tile, dim3(g), dim3(KNN_BLOCK), 0, s, p);
+        if (!g) return hipSuccess;
+        if (p.knn_pk_p && p.knn_r2 > 1e-30f) { /* the level-0 bins need bits(maxD^2) >= 32 << sh */
+            /* scalar stream, then k_gather_knn_tile over the tiles it handed back */
+            const int64_t np = p.knn_pk_pairs;
+            pm_launch(k_knn_pack, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, p.cell_start, p.grid.ncells,
+                      p.ph_a, p.ph_b, p.knn_pk_p, p.knn_pk_q, np, p.knn_ovf_n);
+            pm_launch(k_gather_knn_ss, dim3(g), dim3(64), 0, s, p);
+            GatherParams q = p;
+            q.tiles = p.knn_ovf;
+            q.n_tiles_dev = p.knn_ovf_n;
+            q.rec_begin = p.rec_begin;
+            pm_launch(k_gather_knn_tile, dim3(g), dim3(KNN_BLOCK), 0, s, q);
+            return hipGetLastError();
+        }
+        pm_launch(k_gather_knn_tile, dim3(g), dim3(KNN_BLOCK), 0, s, p);
         return hipGetLastError();
     }
     const uint32_t lds = (uint32_t)(p.knn_k * KNN_BLOCK * sizeof(uint32_t));

@@ -209,7 +209,16 @@ struct GatherParams {
     /* non-null: the list's length is this device word (the host has not read
      * it back yet); n_tiles then bounds the grid (every tile) */
     const uint32_t *n_tiles_dev;
+    /* kNN scalar-stream kernel (k_gather_knn_ss): photon pairs (k_knn_pack,
+     * knn_pk_pairs of them: 2 float4 + 3 float4 per pair) and the list of
+     * tiles it hands back to k_gather_knn_tile (knn_ovf, length *knn_ovf_n) */
+    float4 *knn_pk_p, *knn_pk_q;
+    int64_t knn_pk_pairs;
+    uint32_t *knn_ovf, *knn_ovf_n;
 };
+/* knn_ovf_n[0] = handed-back tiles; [1..63] and the 16-word records at
+ * [64, 1024 + 64) are PM_KNN_SS_DBG diagnostics; the list follows */
+constexpr int KNN_OVF_HDR = 64 + 1024;
 
 struct FinalParams {
     RecordsDev R;

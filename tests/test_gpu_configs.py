@@ -226,8 +226,9 @@ def test_c2_full_knn(oracle_mod, hip_mod, monkeypatch):
     recs = orc.eye_pass(p)
     slots = orc.trace_photons(p, 0, 0, 262_144)
     outs = {}
-    for name in ("lane", "tile"):
-        monkeypatch.setenv("PM_GATHER_KERNEL", name)
+    for name in ("lane", "tile", "ss"):
+        monkeypatch.setenv("PM_GATHER_KERNEL", "lane" if name == "lane" else "tile")
+        monkeypatch.setenv("PM_KNN_SS", "1" if name == "ss" else "0")
         ctx = sc.load_into(hip_mod.Context(0))
         try:
             ctx.upload_records(recs)
@@ -238,6 +239,7 @@ def test_c2_full_knn(oracle_mod, hip_mod, monkeypatch):
         finally:
             ctx.close()
     assert_bitexact(outs["tile"], outs["lane"], "C2 kNN tile vs per-lane")
+    assert_bitexact(outs["ss"], outs["lane"], "C2 kNN scalar-stream vs per-lane")
     ref = recs.copy()
     orc.gather(orc.build_kdtree(slots), ref, p)
     act = (ref["flags"] & 7) == 0

@@ -707,9 +707,10 @@ def test_knn_render_parity(cornell):
     ("cornell", 32, 24, 40000, 8, 1.0e7),         # >= 2^16 photons inside maxD: minimum extraction
 ])
 def test_knn_kernels_agree(scene, W, H, paths, K, radius2, oracle_mod, hip_mod, monkeypatch):
-    """The kNN tile kernel (LDS-staged tile unions, histogram selection of
-    r_k^2) and the per-lane heap kernel give bit-identical records: same
-    found count, r_k^2 and fixed-point flux, over two accumulating passes."""
+    """The kNN tile kernels (k_gather_knn_tile: LDS-staged tile unions;
+    k_gather_knn_ss: scalar-streamed photon pairs, bit-pattern histograms)
+    and the per-lane heap kernel give bit-identical records: same found
+    count, r_k^2 and fixed-point flux, over two accumulating passes."""
     from pmrender.abi import PM_ESTIMATOR_KNN
     sc = {"cornell": lambda: scenes.cornell_box(W, H), "caustic": lambda: scenes.caustic_scene(W, H),
           "soup": lambda: scenes.triangle_soup(20000, W, H)}[scene]()
@@ -719,8 +720,9 @@ def test_knn_kernels_agree(scene, W, H, paths, K, radius2, oracle_mod, hip_mod, 
     recs = orc.eye_pass(p)
     slots = [orc.trace_photons(p, i, 0, paths) for i in range(2)]
     outs = {}
-    for name in ("lane", "tile"):
-        monkeypatch.setenv("PM_GATHER_KERNEL", name)
+    for name in ("lane", "tile", "ss"):
+        monkeypatch.setenv("PM_GATHER_KERNEL", "lane" if name == "lane" else "tile")
+        monkeypatch.setenv("PM_KNN_SS", "1" if name == "ss" else "0")
         ctx = sc.load_into(hip_mod.Context(0))
         try:
             ctx.upload_records(recs)
@@ -739,6 +741,7 @@ def test_knn_kernels_agree(scene, W, H, paths, K, radius2, oracle_mod, hip_mod, 
     else:
         assert (n == K).all() and (slots[1]["bits"] & 1).sum() >= 65536
     assert_bitexact(outs["tile"], outs["lane"], f"kNN tile vs per-lane ({scene}, K={K})")
+    assert_bitexact(outs["ss"], outs["lane"], f"kNN scalar-stream vs per-lane ({scene}, K={K})")
 
 
 def test_knn_rejects_partial_gathers(cornell, hip_mod):
