@@ -1790,10 +1790,17 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
  * A tile this kernel does not handle — a lane group whose union box exceeds
  * the 64-row map, r_k^2 = 0 (pbrt's 0/0 and its lowest-slot ties) — is
  * appended to P.knn_ovf and re-run by k_gather_knn_tile. */
-constexpr int KS_NB = 32;   /* bins per histogram level (+1 sink) */
+/* waves per SIMD (VGPR budget; the 4.25 KB histogram allows 9): C2 kNN gather
+ * 5 (81 VGPRs) 0.746-0.757 ms, 6 (73) 0.735, 7 (72) 0.747 (same box) */
+#ifndef PM_KS_WAVES
+#define PM_KS_WAVES 6
+#endif
+#define KS_OCC __attribute__((amdgpu_waves_per_eu(PM_KS_WAVES, PM_KS_WAVES)))
+constexpr int KS_NB = 32;   /* bins per histogram level (+1 sink), two 16-bit counters per word */
+constexpr int KS_HW = KS_NB / 2 + 1; /* histogram words per lane (the sink is bin KS_NB: word KS_HW - 1) */
 constexpr int KS_LIST = 12; /* values a COLLECT keeps per lane (rows 0..KS_LIST of the histogram, +1 scratch) */
 enum { KS_HIST = 0, KS_COLLECT = 1, KS_SUM = 2, KS_DONE = 3 };
-static_assert(KS_LIST + 1 <= KS_NB, "the COLLECT list aliases histogram rows");
+static_assert(KS_LIST + 1 < KS_HW, "the COLLECT list aliases histogram rows (not the sink's)");
 
 /* photon pairs of the bucket order for the scalar stream: pair k = photons
  * 2k, 2k + 1, P block (x x y y z z wx wx), Q block (r r g g b b wy wy wz wz
@@ -1819,8 +1826,31 @@ __global__ __launch_bounds__(256) void k_knn_pack(const uint32_t *cell_start, ui
 }
 
 
-__global__ __launch_bounds__(64) void k_gather_knn_ss(GatherParams P) {
-    __shared__ uint32_t H[(KS_NB + 1) * 64]; /* [bin][lane]; bin KS_NB = sink */
+/* wave-uniform float minimum / maximum (every lane active) */
+PMD float wave_min_f(float v) {
+    const int m = wave_scan_dpp(__float_as_int(v), __float_as_int(INFINITY),
+                                [](int a, int b) { return __float_as_int(fminf(__int_as_float(a), __int_as_float(b))); });
+    return __int_as_float(__builtin_amdgcn_readlane(m, 63));
+}
+PMD float wave_max_f(float v) {
+    const int m = wave_scan_dpp(__float_as_int(v), __float_as_int(-INFINITY),
+                                [](int a, int b) { return __float_as_int(fmaxf(__int_as_float(a), __int_as_float(b))); });
+    return __int_as_float(__builtin_amdgcn_readlane(m, 63));
+}
+/* gap (cell units) between [lo, hi] and cell c of an axis of dim cells —
+ * the border cells extend to infinity (cell_axis clamps) — less a 1e-3
+ * margin for the rounding of the cell-unit coordinates */
+PMD float box_gap(float lo, float hi, uint32_t c, int dim) {
+    const float a = c == 0 ? -INFINITY : (float)c, b = (int)c + 1 == dim ? INFINITY : (float)(c + 1);
+    return fmaxf(fmaxf(a - hi, lo - b) - 1e-3f, 0.f);
+}
+/* cell of a cell-unit coordinate, clamped like cell_axis */
+PMD uint32_t cell_u(float u, int dim) {
+    const int c = (int)floorf(u);
+    return (uint32_t)(c < 0 ? 0 : (c >= dim ? dim - 1 : c));
+}
+__global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
+    __shared__ uint32_t H[KS_HW * 64]; /* [word][lane]: bins 2w (low half), 2w + 1 (high half); 4.25 KB */
     const int lane = threadIdx.x & 63;
     if (P.tiles && P.n_tiles_dev && (int64_t)blockIdx.x >= (int64_t)*P.n_tiles_dev) return;
     const uint32_t tile = P.tiles ? P.tiles[blockIdx.x] : blockIdx.x;
@@ -1828,7 +1858,7 @@ __global__ __launch_bounds__(64) void k_gather_knn_ss(GatherParams P) {
     const int K = P.knn_k;
     const float maxd2 = P.knn_r2;
 #pragma unroll
-    for (int b = 0; b <= KS_NB; ++b) H[b * 64 + lane] = 0u;
+    for (int b = 0; b < KS_HW; ++b) H[b * 64 + lane] = 0u;
     bool active = false, live = false, back = false;
     float4 pos = make_float4(0.f, 0.f, 0.f, 0.f), nrm = pos;
     if (r < P.rec_end) {
@@ -1845,6 +1875,9 @@ __global__ __launch_bounds__(64) void k_gather_knn_ss(GatherParams P) {
     /* Faceforward folded into the normal: Dot(-n, w) = -Dot(n, w) exactly */
     const float nsx = back ? -nrm.x : nrm.x, nsy = back ? -nrm.y : nrm.y, nsz = back ? -nrm.z : nrm.z;
     const GridDesc g = P.grid;
+    TILE_STAT(0, 1);
+    GProf gp; /* PM_GATHER_PROFILE: record + groups, pass setup, HIST, COLLECT, SUM, pass end, store */
+    gp.begin();
     uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0, z0 = 0, z1 = 0;
     if (live) { /* KnnGrid::init's cells */
         const float rq = sqrtf(maxd2) * 1.0001f + 1e-4f;
@@ -1904,6 +1937,9 @@ __global__ __launch_bounds__(64) void k_gather_knn_ss(GatherParams P) {
             if ((mh | mc | ms) == 0ull) break;
             const int pt = mh ? KS_HIST : (mc ? KS_COLLECT : KS_SUM);
             const bool act = in && phase == pt;
+            TILE_STAT(1, 1);
+            TILE_STAT(2, pt == KS_HIST);
+            gp.mark(0);
             /* this lane's bound (every value the pass needs is below it) */
             float bnd = 0.f;
             if (act) {
@@ -1926,17 +1962,38 @@ __global__ __launch_bounds__(64) void k_gather_knn_ss(GatherParams P) {
             uint32_t PX0, PX1, PY0, PY1, PZ0, PZ1;
             union_box6(g, act, a0, a1, b0, b1, c0, c1, PX0, PX1, PY0, PY1, PZ0, PZ1);
             const uint32_t PLY = PY1 > PY0 ? 32u - (uint32_t)__builtin_clz(PY1 - PY0) : 0u;
-            /* union row u = lane: photons [Bu, Bu + Lu) of cells PX0..PX1 */
+            /* rows pruned to the union of the pass's spheres: with the act
+             * lanes' positions in the box [Pmin, Pmax] and R the largest
+             * bound (cell units), a photon within R_l of lane l lies in a row
+             * whose (y, z) gap to the box is <= R and, in that row, within
+             * sqrt(R^2 - gap^2) of [Pmin.x, Pmax.x] (KnnGrid::scan's pruning
+             * for the whole pass at once; cell_gap's 1e-3 margins) */
+            const float ux = (p.x - g.gx) * g.inv_cs, uy = (p.y - g.gy) * g.inv_cs, uz = (p.z - g.gz) * g.inv_cs;
+            const float Rq = wave_max_f(act ? (sqrtf(bnd) * 1.0001f + 1e-4f) * g.inv_cs : 0.f);
+            const float mnx = wave_min_f(act ? ux : INFINITY), mxx = wave_max_f(act ? ux : -INFINITY);
+            const float mny = wave_min_f(act ? uy : INFINITY), mxy = wave_max_f(act ? uy : -INFINITY);
+            const float mnz = wave_min_f(act ? uz : INFINITY), mxz = wave_max_f(act ? uz : -INFINITY);
+            /* union row u = lane: photons [Bu, Bu + Lu) of cells xa..xb of its (y, z) */
             uint32_t Bu = 0u, Lu = 0u;
             {
                 const uint32_t cy = PY0 + ((uint32_t)lane & ((1u << PLY) - 1u)), cz = PZ0 + ((uint32_t)lane >> PLY);
                 if (cy <= PY1 && cz <= PZ1) {
-                    const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
-                    Bu = P.cell_start[row + PX0];
-                    Lu = P.cell_start[row + PX1 + 1u] - Bu;
+                    const float gy = box_gap(mny, mxy, cy, g.dy), gz = box_gap(mnz, mxz, cz, g.dz);
+                    const float rem = Rq * Rq - (gy * gy + gz * gz);
+                    if (rem >= 0.f) {
+                        const float sx = sqrtf(rem) * 1.0001f + 1e-3f;
+                        const uint32_t xa = max(PX0, cell_u(mnx - sx, g.dx)), xb = min(PX1, cell_u(mxx + sx, g.dx));
+                        if (xa <= xb) {
+                            const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+                            Bu = P.cell_start[row + xa];
+                            Lu = P.cell_start[row + xb + 1u] - Bu;
+                        }
+                    }
                 }
             }
             unsigned long long rows = __ballot(Lu > 0u);
+            /* 16-bit bin counters: a union of >= 2^16 photons goes to k_gather_knn_tile */
+            if (uniform_u32(__builtin_amdgcn_readlane(wave_incl_sum_u32(Lu), 63)) >= 65536u) { defer = true; break; }
 #ifdef PM_KNN_SS_DBG
             const unsigned long long rows0 = rows;
 #endif
@@ -1948,7 +2005,7 @@ __global__ __launch_bounds__(64) void k_gather_knn_ss(GatherParams P) {
             const f2 nx2 = {nsx, nsx}, ny2 = {nsy, nsy}, nz2 = {nsz, nsz};
             uint32_t *hcol = H + lane;
             /* COLLECT: the lane's list rows (lanes outside the pass write the sink row) */
-            uint32_t *lcol = hcol + (act ? 0 : KS_NB * 64);
+            uint32_t *lcol = hcol + (act ? 0 : (KS_HW - 1) * 64);
             uint32_t ccl = 0u;
             /* one specialised loop per pass type over the rows' photon pairs */
             /* one specialised loop per pass type over the rows' photon pairs,
@@ -1965,6 +2022,8 @@ __global__ __launch_bounds__(64) void k_gather_knn_ss(GatherParams P) {
                     const uint32_t b = uniform_u32(__builtin_amdgcn_readlane(Bu, u));
                     const uint32_t e = b + uniform_u32(__builtin_amdgcn_readlane(Lu, u));
                     const uint32_t k1 = (e + 1u) >> 1;
+                    TILE_STAT(3, 1);
+                    TILE_STAT(PT == KS_HIST ? 4 : PT == KS_COLLECT ? 5 : 6, k1 - (b >> 1));
                     for (uint32_t k0 = b >> 1; k0 < k1; k0 += NP) {
                         /* the batch (reads past the run stay inside the packed
                          * buffer's zero pairs; their photons are never counted) */
@@ -2007,8 +2066,8 @@ __global__ __launch_bounds__(64) void k_gather_knn_ss(GatherParams P) {
                             if constexpr (PT == KS_HIST) {
                                 const uint32_t h0 = min(max(__builtin_elementwise_sub_sat(u0, hA) >> hsh, hlo), (uint32_t)KS_NB);
                                 const uint32_t h1 = min(max(__builtin_elementwise_sub_sat(u1, hA) >> hsh, hlo), (uint32_t)KS_NB);
-                                atomicAdd(hcol + h0 * 64u, 1u);
-                                atomicAdd(hcol + h1 * 64u, 1u);
+                                atomicAdd(hcol + (h0 >> 1) * 64u, 1u << (h0 << 4)); /* shift mod 32: (h & 1) * 16 */
+                                atomicAdd(hcol + (h1 >> 1) * 64u, 1u << (h1 << 4));
                             } else if constexpr (PT == KS_COLLECT) {
                                 lcol[ccl * 64u] = u0;
                                 ccl += (u0 - clo) < cw ? 1u : 0u;
@@ -2020,6 +2079,7 @@ __global__ __launch_bounds__(64) void k_gather_knn_ss(GatherParams P) {
                                 const bool h0 = d2.x < smd, h1 = d2.y < smd;
                                 less += (int)h0 + (int)h1;
                                 if (__ballot(h0 || h1)) {
+                                    TILE_STAT(7, 1);
                                     const f2 dn = (nx2 * WX + ny2 * WY) + nz2 * WZ; /* knn_facing */
                                     /* knn_add: s = 1 - d^2 / r_k^2, kernel 3/pi s^2, times 1/r_k^2 and alpha;
                                      * a photon that does not count gets ki = 0, so every term of it is rint(0) = 0 */
@@ -2037,22 +2097,28 @@ __global__ __launch_bounds__(64) void k_gather_knn_ss(GatherParams P) {
                     }
                 }
             };
+            gp.mark(1);
             if (pt == KS_HIST) stream(std::integral_constant<int, KS_HIST>{});
             else if (pt == KS_COLLECT) stream(std::integral_constant<int, KS_COLLECT>{});
             else stream(std::integral_constant<int, KS_SUM>{});
+            gp.mark(pt == KS_HIST ? 2 : pt == KS_COLLECT ? 3 : 4);
             if (!act) continue;
             if (pt == KS_HIST) {
                 /* the bin holding the K-th value; the column is left zeroed */
                 uint32_t cum = 0u, below = 0u, cntb = 0u;
                 int bs = -1;
+#pragma unroll 4
+                for (int w = 0; w < KS_NB / 2; ++w) {
+                    const uint32_t hw = hcol[w * 64];
+                    hcol[w * 64] = 0u;
 #pragma unroll
-                for (int bb = 0; bb < KS_NB; ++bb) {
-                    const uint32_t c = hcol[bb * 64];
-                    hcol[bb * 64] = 0u;
-                    if (bs < 0 && cum + c >= (uint32_t)K) { bs = bb; below = cum; cntb = c; }
-                    cum += c;
+                    for (int hh = 0; hh < 2; ++hh) {
+                        const uint32_t c = (hw >> (16 * hh)) & 0xffffu;
+                        if (bs < 0 && cum + c >= (uint32_t)K) { bs = 2 * w + hh; below = cum; cntb = c; }
+                        cum += c;
+                    }
                 }
-                hcol[KS_NB * 64] = 0u;
+                hcol[(KS_HW - 1) * 64] = 0u;
                 if (lvl0 && cum < (uint32_t)K) { /* fewer than K inside maxD: r_k^2 = maxD^2 */
                     full = false;
                     md2 = maxd2;
@@ -2090,16 +2156,17 @@ __global__ __launch_bounds__(64) void k_gather_knn_ss(GatherParams P) {
                 uint32_t v[KS_LIST];
 #pragma unroll
                 for (int a = 0; a < KS_LIST; ++a) v[a] = (uint32_t)a < cc ? hcol[a * 64] : 0xffffffffu;
-#pragma unroll
-                for (int a = 0; a <= KS_LIST; ++a) hcol[a * 64] = 0u;
+                const uint32_t *lcand = hcol;
                 uint32_t ans = v[0];
-#pragma unroll
-                for (int a = 0; a < KS_LIST; ++a) {
+                for (uint32_t a = 0; a < cc; ++a) { /* candidate a (re-read from LDS: a rolled loop) */
+                    const uint32_t va = lcand[a * 64];
                     int lt = 0, le = 0;
 #pragma unroll
-                    for (int bb = 0; bb < KS_LIST; ++bb) { lt += v[bb] < v[a]; le += v[bb] <= v[a]; }
-                    if ((uint32_t)a < cc && lt < need && need <= le) ans = v[a];
+                    for (int bb = 0; bb < KS_LIST; ++bb) { lt += v[bb] < va; le += v[bb] <= va; }
+                    if (lt < need && need <= le) ans = va;
                 }
+#pragma unroll
+                for (int a = 0; a <= KS_LIST; ++a) hcol[a * 64] = 0u;
                 md2 = __uint_as_float(ans);
                 phase = KS_SUM;
                 if (md2 == 0.f) defer = true; /* pbrt's 0/0: k_gather_knn_tile's tie rules */
@@ -2126,6 +2193,7 @@ __global__ __launch_bounds__(64) void k_gather_knn_ss(GatherParams P) {
             }
         }
         if (__ballot(defer)) defer = true;
+        gp.mark(5);
     }
     if (__ballot(defer)) { /* re-run by k_gather_knn_tile */
         if (lane == 0) P.knn_ovf[atomicAdd(P.knn_ovf_n, 1u)] = tile;
@@ -2143,6 +2211,8 @@ __global__ __launch_bounds__(64) void k_gather_knn_ss(GatherParams P) {
         P.R.state[r] = make_float4(flux.x, flux.y, flux.z, md2);
         P.R.n[r] = (float)cnt;
     }
+    gp.mark(6);
+    gp.flush(P.counters);
 }
 
 hipError_t launch_gather_knn(const GatherParams &p, int count, hipStream_t s) {

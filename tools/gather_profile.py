@@ -1,4 +1,4 @@
-"""k_gather_tile (argument knn: k_gather_knn_tile) phase clocks (PM_GATHER_PROFILE variant build) at C2 / C3 / C5:
+"""k_gather_tile (argument knn: k_gather_knn_ss, PM_KNN_SS=0: k_gather_knn_tile) phase clocks (PM_GATHER_PROFILE variant build) at C2 / C3 / C5:
    make -C cuda-raytrace_amd variant NAME=gprof VFLAGS=-DPM_GATHER_PROFILE
    PMHIP_LIB=cuda-raytrace_amd/lib/variants/libpmhip_gprof.so python tools/gather_profile.py [c3|c5]
 Prints the summed wave clock per phase (record load, group forming + row
@@ -32,7 +32,9 @@ for rep in range(2):
     ctx.gather(p)
     ctx.synchronize()
 v = list(ctx.trace_profile().values())
-names = (["record", "pass_setup", "stage", "test", "hits", "pass_end", "direct+store"] if KNN else
+names = (["record+groups", "pass_setup", "hist", "collect", "sum", "pass_end", "store"]
+         if KNN and os.environ.get("PM_KNN_SS", "1") != "0" else
+         ["record", "pass_setup", "stage", "test", "hits", "pass_end", "direct+store"] if KNN else
          ["record", "group", "stage", "test", "hits", "direct", "store"])
 tot = sum(v[:7])
 waves = max(v[7], 1)

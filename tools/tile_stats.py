@@ -1,4 +1,4 @@
-"""k_gather_tile (or with argument knn: k_gather_knn_tile) event counts at C2 (PM_TILE_STATS variant build):
+"""k_gather_tile (or with argument knn: k_gather_knn_ss, PM_KNN_SS=0: k_gather_knn_tile) event counts at C2 (PM_TILE_STATS variant build):
    make -C cuda-raytrace_amd variant NAME=tstats VFLAGS=-DPM_TILE_STATS
    PMHIP_LIB=cuda-raytrace_amd/lib/variants/libpmhip_tstats.so python tools/tile_stats.py"""
 import os, sys
@@ -28,7 +28,9 @@ ctx.gather(p)
 ctx.synchronize()
 v = list(ctx.trace_profile().values())
 names = ["tile_waves", "windows", "test_pairs", "hit_iters", "direct_lanes", "chunks", "wide_waves", "staged"]
-if KNN:  # k_gather_knn_tile: per-wave sums
+if KNN and os.environ.get("PM_KNN_SS", "1") != "0":  # k_gather_knn_ss (the default kNN kernel)
+    names = ["tile_waves", "passes", "hist_passes", "rows", "hist_pairs", "collect_pairs", "sum_pairs", "sum_pairs_hit"]
+elif KNN:  # k_gather_knn_tile: per-wave sums
     names = ["groups", "passes", "windows", "staged", "hit_iters", "direct_lanes", "min_lane_passes", "rebin_lane_passes"]
 for k, x in zip(names, v):
     print(f"{k:14s} {x:12d}  per tile wave {x / max(v[0], 1):8.2f}")
