@@ -14,7 +14,13 @@ records) already resident in HBM:
 Mphotons/s); `mgather_samples_per_s` = gather points / step time.
 
 Single GPU: `python bench.py`. N GPUs (one process per GPU):
-`python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N`.
+`python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N`
+(weak scaling: the config's paths per GPU). Strong scaling: `--total-paths T`
+splits T paths per pass over the N ranks (`--config c4 --total-paths 4194304`
+is BASELINE C4's 16,777,216 photon slots at any N) and reports "scaling":
+"strong". At N > 1 `stages_ms.exchange` is the per-pass exchange (RCCL
+all-reduce + reduce-scatter, or the slot all-gather) timed to completion in
+the stage-timed passes after the timed region.
 """
 import argparse
 import json
@@ -59,6 +65,10 @@ def parse():
     ap.add_argument("--structure", default="grid", choices=["grid", "kd"])
     ap.add_argument("--exchange", default="reduce", choices=["reduce", "allgather"])
     ap.add_argument("--paths", type=int, default=None, help="photon paths per GPU per pass (default: the config's)")
+    ap.add_argument("--total-paths", type=int, default=None,
+                    help="strong scaling: photon paths per pass over ALL ranks, split evenly (e.g. --config c4 "
+                         "--total-paths 4194304: BASELINE C4's 16,777,216 slots at any N); reported as scaling "
+                         "'strong'. Default: weak scaling, --paths per GPU")
     ap.add_argument("--estimator", default="ppm", choices=["ppm", "knn"],
                     help="ppm: the reference's fixed-radius PPM gather (headline); knn: pbrt-v2 LPhoton kNN")
     ap.add_argument("--knn-k", type=int, default=50, help="kNN photons per lookup (pbrt 'nused')")
@@ -95,14 +105,14 @@ def kernel_src_sha():
     return h.hexdigest()[:16]
 
 
-def load_pmc_traffic(kernel_prefix, config):
+def load_pmc_traffic(kernel_prefix, config, field="hbm_bytes_per_launch"):
     """Per-launch HBM bytes (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, gfx950
     FETCH x2 correction; tools/pmc_traffic.py) of this kernel from the
     committed profile — only if it was measured on these exact HIP sources
     and this config; else (None, reason)."""
     sha = kernel_src_sha()
     path, d = None, None
-    for rnd in ("r03", "r02"):      # the newest committed profile of these sources
+    for rnd in ("r04", "r03", "r02"):      # the newest committed profile of these sources
         cand = os.path.join(ROOT, "profiles", rnd, "pmc_traffic_%s.json" % config)
         if os.path.exists(cand):
             with open(cand) as f:
@@ -119,7 +129,7 @@ def load_pmc_traffic(kernel_prefix, config):
     k = d.get("kernels", {}).get(kernel_prefix)
     if not k:
         return None, "kernel not in the committed PMC profile"
-    return k.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    return k.get(field), os.path.relpath(path, ROOT)
 
 
 def cpu_model():
@@ -220,9 +230,15 @@ def main():
     from pmrender.dist import HipEngine, PassRunner
 
     cfg = CONFIGS[args.config]
+    if args.total_paths is not None:
+        args.paths = -(-args.total_paths // world)      # this rank's chunk (PassRunner's split)
     if args.paths is None:
         args.paths = cfg["paths"]
     scene, workload = build_scene(args.config), cfg["desc"]
+    if args.total_paths is not None:
+        workload = (f"{args.config.upper()} strong scaling: {args.total_paths:,} photon paths "
+                    f"({args.total_paths * 4:,} slots) per pass over all {world} GPU(s), "
+                    f"{scene.width}x{scene.height} gather points; scene of: " + cfg["desc"])
     progressive = cfg["progressive"]
     t_setup = time.perf_counter()
     ctx = scene.load_into(hip.Context(local))
@@ -237,7 +253,7 @@ def main():
     with torch.cuda.stream(stream):
         eng = HipEngine(ctx)
         ctx.eye_pass(p, eng._s())
-        runner = PassRunner(eng, p, rank, world, args.exchange)
+        runner = PassRunner(eng, p, rank, world, args.exchange, total_paths=args.total_paths)
         # a step is one pass over the config's workload: from the initial PPM
         # state (the reference's single pass), or for progressive configs the
         # next pass of one render (Halton permutation of pass k, radii shrink)
@@ -278,15 +294,21 @@ def main():
         # per-stage split: a few more passes after the timed region, every stage timed
         ctx.set_stage_timing("all")
         ctx.timing_reset()
+        # N > 1: each pass's exchange also timed here, run to completion at
+        # once (in the timed steps it overlaps the next pass's trace + build)
+        runner.time_exchange = world > 1
         for _ in range(min(args.steps, 10)):
             step()
         runner.flush()
         torch.cuda.synchronize()
+        runner.time_exchange = False
         stages = {}
         for name in ("reset", "trace", "build", "gather", "update"):
             n, ms = ctx.timing_total(name)
             if n:
                 stages[name] = round(ms / n, 5)
+        if runner.exchange_ms:
+            stages["exchange"] = round(sum(runner.exchange_ms) / len(runner.exchange_ms), 5)
 
         census = canonical = tcensus = None
         n_valid = None
@@ -316,12 +338,12 @@ def main():
     recs = ctx.download_records()
     active = int(((recs["flags"] & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) == 0).sum())
     g_points = scene.width * scene.height
-    paths_total = args.paths * world
+    paths_total = runner.total             # all ranks' paths per pass (strong: --total-paths)
     ms_per_step = elapsed / args.steps * 1e3
     value = paths_total * args.steps / elapsed / 1e6
 
     roofline = None
-    kernel_name = ("k_gather_knn" if knn else "k_gather_tile" if structure == PM_GATHER_GRID else "k_gather_kd")
+    kernel_name = ("k_gather_knn_ss" if knn else "k_gather_tile" if structure == PM_GATHER_GRID else "k_gather_kd")
     if census is not None:
         vis, hits, rows, act = census
         inactive = n_rec - act
@@ -341,9 +363,13 @@ def main():
             l1_bytes = 72 * act + 16 * inactive + 16 * vis + 24 * hits
             l1_formula = "72*G_act + 16*G_inactive + 16*kd_nodes_visited + 24*photons_in_radius"
         roofline = {
-            "bound": "hbm",
-            "kernel": "k_gather_knn_tile (pbrt LPhoton kNN: LDS tile unions, exact histogram selection of r_k^2, "
-                      "fused record update)" if knn
+            # what bounds the kernel (see "limiter"); the roofline it is priced
+            # against is HBM ("peak", "unit"): the path moves bytes, no MFMA work
+            "bound": "valu" if knn else "latency",
+            "priced_against": "hbm",
+            "kernel": "k_knn_pack + k_gather_knn_ss (pbrt LPhoton kNN: photon pairs through the scalar cache, "
+                      "bit-pattern histograms for r_k^2, fused record update; + k_gather_knn_tile for handed-back "
+                      "tiles)" if knn
             else "k_gather_tile<0,1> (LDS-staged range query + fused PPM update)" if structure == PM_GATHER_GRID
             else "k_gather_kd<0,0>",
             "achieved": round(achieved, 1),
@@ -365,12 +391,18 @@ def main():
             # what actually limits it is stated in "limiter"
             "achieved_basis": "SURVEY.md §8d compulsory bytes since round 2 (round 1 priced the per-lane "
                               "algorithmic bytes, so r01 fractions are not comparable)",
-            "limiter": ("VALU issue (profiles/r02 counters): ~3 selection passes over each tile's staged union, "
-                        "every lane testing every staged photon — arithmetic, not memory" if knn else
+            "limiter": ("VALU issue + scalar-cache misses (profiles/r04): ~3.7 passes over each tile's union "
+                        "(histogram, collect, sum), every lane testing every streamed photon pair" if knn else
                         "VALU issue + per-wave latency (profiles/r02 counters): the kernel reads each record "
                         "once and each tile's photons once, so HBM is not what bounds it"),
         }
         if traffic is not None:
+            raw = load_pmc_traffic(kernel_name, args.config + ("_knn" if knn else ""), "hbm_bytes_uncorrected")[0]
+            roofline["traffic_uncorrected"] = raw
+            roofline["traffic_correction"] = ("traffic = 2 x FETCH_SIZE + WRITE_SIZE (the guide's gfx950 halving of "
+                                              "FETCH_SIZE, stated for wide coalesced streaming reads; this kernel's "
+                                              "reads are 16-B records and photon rows, so the true bytes lie between "
+                                              "traffic_uncorrected and traffic)")
             roofline["traffic_GBs"] = round(traffic / (gather_ms * 1e-3) / 1e9, 1)
             roofline["traffic_frac"] = round(traffic / (gather_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
             roofline["traffic_source"] = traffic_src
@@ -430,14 +462,15 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 5),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.total_paths else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic: scene built in code (pmrender/scenes.py), BASELINE.json config " + args.config.upper(),
         "config": {
             "workload": workload,
-            "photon_slots_per_gpu": args.paths * int(p.max_photon_count),
-            "paths_per_gpu": args.paths,
+            "photon_slots_per_gpu": runner.per * int(p.max_photon_count),
+            "paths_per_gpu": runner.per,
+            "paths_per_pass_all_gpus": runner.total,
             "gather_points": g_points,
             "active_gather_points": active,
             "structure": args.structure,
@@ -448,7 +481,7 @@ def main():
         },
         "mgather_samples_per_s": round(g_points * args.steps / elapsed / 1e6, 3),
         "kernel_rates": {
-            "trace_mphotons_per_s": round(args.paths / (stages["trace"] * 1e-3) / 1e6, 2) if "trace" in stages else None,
+            "trace_mphotons_per_s": round(runner.paths / (stages["trace"] * 1e-3) / 1e6, 2) if "trace" in stages else None,
             "gather_msamples_per_s": round(g_points / (gather_ms * 1e-3) / 1e6, 2) if gather_ms > 0 else None,
         },
         "stages_ms": stages,

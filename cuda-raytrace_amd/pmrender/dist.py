@@ -181,10 +181,15 @@ class HipEngine:
 
 
 class PassRunner:
-    def __init__(self, engine, params, rank=0, world=1, exchange="reduce", force_exchange=False):
+    def __init__(self, engine, params, rank=0, world=1, exchange="reduce", force_exchange=False, total_paths=None):
         """force_exchange: run the N > 1 code path (record view, collectives,
         owned chunks / bands) even at world size 1 — how a 1-GPU box executes
-        the RCCL branch of the exchange (tests/test_dist_gpu.py)."""
+        the RCCL branch of the exchange (tests/test_dist_gpu.py).
+        total_paths: strong scaling — the pass emits total_paths paths over
+        all ranks (rank r traces global paths [r*per, min(total, (r+1)*per)),
+        per = ceil(total / world); the last rank's short chunk leaves its
+        tail slots invalid); None: weak scaling, params.paths_per_pass per
+        rank."""
         if exchange not in ("reduce", "allgather"):
             raise ValueError(exchange)
         self.multi = world > 1 or force_exchange
@@ -192,9 +197,20 @@ class PassRunner:
             # the kNN estimate is not a sum over photon shards
             raise ValueError("the kNN estimator needs the all-gather exchange")
         self.e, self.p, self.rank, self.world, self.exchange = engine, params, rank, world, exchange
-        self.paths = int(params.paths_per_pass)           # per rank
-        self.path_begin = rank * self.paths
-        self.slots_per_rank = self.paths * int(params.max_photon_count)
+        if total_paths is None:
+            self.per = int(params.paths_per_pass)         # chunk per rank
+            self.total = self.per * world
+        else:
+            self.total = int(total_paths)
+            self.per = -(-self.total // world)
+        self.path_begin = min(self.total, rank * self.per)
+        self.paths = min(self.total, self.path_begin + self.per) - self.path_begin   # this rank's paths
+        self.slots_per_rank = self.per * int(params.max_photon_count)             # slot chunk per rank
+        self.slots_mine = self.paths * int(params.max_photon_count)
+        # exchange timing (bench.py, after its timed region): run each exchange
+        # to completion at once and record its GPU time (ms) per pass
+        self.time_exchange = False
+        self.exchange_ms = []
         n = engine.num_records()
         self.n_records = n
         self.rec_begin, self.rec_count, self.rec_per = _chunk(n, world, rank)   # final image split
@@ -220,7 +236,21 @@ class PassRunner:
 
     @property
     def emitted_per_pass(self):
-        return self.paths * self.world
+        return self.total
+
+    def _timed(self, fn):
+        """fn() with its GPU time appended to exchange_ms when time_exchange
+        is set (CUDA events on the current stream; the collectives are joined
+        inside fn, so the stream waits for them before the end event)"""
+        if not self.time_exchange or not torch.cuda.is_available():
+            return fn()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        r = fn()
+        b.record()
+        b.synchronize()
+        self.exchange_ms.append(a.elapsed_time(b))
+        return r
 
     # gloo (CPU tests, or several ranks sharing one GPU) works on host tensors:
     # device tensors are staged through host memory
@@ -258,25 +288,29 @@ class PassRunner:
             if reset:
                 e.reset_records(p)
             e.trace_photons(p, pass_index, 0, self.paths, 0)
-            e.build_photon_map(p, self.slots_per_rank)
+            e.build_photon_map(p, self.slots_mine)
             e.gather(p)
             return
         if self.exchange == "reduce":
             # trace + build do not read records: they overlap the previous exchange
-            e.trace_photons(p, pass_index, self.path_begin, self.paths, self.path_begin)
-            e.build_photon_map(p, self.slots_per_rank)
+            if self.paths:
+                e.trace_photons(p, pass_index, self.path_begin, self.paths, self.path_begin)
+            e.build_photon_map(p, self.slots_mine)
             self._finish_exchange()
             if reset:
                 e.reset_records(p)
             e.gather_split(p, self.count, self.flux)
             self._start_exchange()
+            if self.time_exchange:
+                self._timed(self._finish_exchange)
         else:
             if reset:
                 e.reset_records(p)
-            e.trace_photons(p, pass_index, self.path_begin, self.paths, 0)
+            if self.paths:
+                e.trace_photons(p, pass_index, self.path_begin, self.paths, 0)
             mine = self.slot_buf[self.rank * self.slots_per_rank * PHOTON_DTYPE.itemsize:
                                  (self.rank + 1) * self.slots_per_rank * PHOTON_DTYPE.itemsize]
-            self._all_gather(self.slot_buf, mine)
+            self._timed(lambda: self._all_gather(self.slot_buf, mine))
             e.build_photon_map(p, self.world * self.slots_per_rank)
             for b, c in self.bands[self.rank]:                  # replicated map, owned bands
                 e.gather_range(p, b, c)

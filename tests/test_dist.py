@@ -1,4 +1,4 @@
-"""World-size-2 gloo tests of the multi-GPU pass runner (pmrender/dist.py) on
+"""World-size-2..8 gloo tests of the multi-GPU pass runner (pmrender/dist.py) on
 CPU: the same PassRunner that bench.py drives over RCCL, here over gloo with
 an oracle-backed engine. Checks both photon exchanges against a
 single-process run over the same global paths."""
@@ -159,7 +159,7 @@ def _scene():
     return sc
 
 
-def _worker(rank, world, port, exchange, outdir):
+def _worker(rank, world, port, exchange, outdir, total=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -168,12 +168,13 @@ def _worker(rank, world, port, exchange, outdir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     p = RenderParams.defaults(paths_per_pass=PATHS, initial_radius2=25.0)
     eng = OracleEngine(_scene(), p)
-    runner = PassRunner(eng, p, rank, world, exchange, force_exchange=world == 1)
+    runner = PassRunner(eng, p, rank, world, exchange, force_exchange=world == 1, total_paths=total)
     for pass_index in range(2):
         runner.step(pass_index)
     runner.flush()
     out = torch.zeros((runner.n_records, 3), dtype=torch.float32)
     runner.final_gather(float(runner.emitted_per_pass * 2), out)
+    assert runner.emitted_per_pass == (total if total is not None else PATHS * world)
     if exchange == "reduce":   # PPM state is owned per chunk of the active-record view
         owned = eng.view[runner.v_begin:runner.v_begin + runner.v_count]
     else:                      # the rank's interleaved 8-row bands
@@ -191,28 +192,34 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _single_process_reference(world):
-    """1 process, the union of both ranks' global paths, kd gather."""
+def _single_process_reference(world, total=None):
+    """1 process, the union of all ranks' global paths, kd gather."""
     import oracle
-    p = RenderParams.defaults(paths_per_pass=PATHS * world, initial_radius2=25.0)
+    n = total if total is not None else PATHS * world
+    p = RenderParams.defaults(paths_per_pass=n, initial_radius2=25.0)
     orc = _scene().load_into(oracle.Oracle(nthreads=2))
     recs = orc.eye_pass(p)
     for pass_index in range(2):
-        slots = orc.trace_photons(p, pass_index, 0, PATHS * world)
+        slots = orc.trace_photons(p, pass_index, 0, n)
         orc.gather(oracle.Oracle.build_kdtree(slots), recs, p)
-    return recs, orc.final(recs, float(PATHS * world * 2))
+    return recs, orc.final(recs, float(n * 2))
 
 
-@pytest.mark.parametrize("exchange,world", [("allgather", 2), ("reduce", 2), ("reduce", 4), ("allgather", 3),
-                                            ("reduce", 1), ("allgather", 1)])
-def test_two_rank_pass_matches_single_process(exchange, world, tmp_path):
-    """world-size 2 (and 3 / 4: view chunks and bands that do not divide
-    evenly, as at N = 8) over gloo vs one process over the same global paths;
-    world 1 with the exchange path forced (force_exchange: what the GPU test
-    runs on RCCL)"""
-    mp.start_processes(_worker, args=(world, _free_port(), exchange, str(tmp_path)), nprocs=world, join=True,
+@pytest.mark.parametrize("exchange,world,total", [("allgather", 2, None), ("reduce", 2, None), ("reduce", 4, None),
+                                                  ("allgather", 3, None), ("reduce", 1, None), ("allgather", 1, None),
+                                                  ("reduce", 8, None), ("allgather", 8, None),
+                                                  ("reduce", 3, 3 * PATHS + 1001), ("allgather", 3, 3 * PATHS + 1001),
+                                                  ("allgather", 8, 8 * PATHS - 4093)])
+def test_two_rank_pass_matches_single_process(exchange, world, total, tmp_path):
+    """world-size 2 (and 3 / 4 / 8: view chunks and bands that do not divide
+    evenly; 8 = the production rank count of one node) over gloo vs one
+    process over the same global paths; world 1 with the exchange path forced
+    (force_exchange: what the GPU test runs on RCCL); `total`: strong scaling
+    (bench.py --total-paths), a fixed path count split over the ranks with a
+    short last chunk"""
+    mp.start_processes(_worker, args=(world, _free_port(), exchange, str(tmp_path), total), nprocs=world, join=True,
                        start_method="spawn")
-    ref_recs, ref_img = _single_process_reference(world)
+    ref_recs, ref_img = _single_process_reference(world, total)
     idx = np.concatenate([np.load(tmp_path / f"idx{r}.npy") for r in range(world)])
     recs = np.concatenate([np.load(tmp_path / f"recs{r}.npy") for r in range(world)]).view(RECORD_DTYPE)
     expect = np.nonzero((ref_recs["flags"] & 7) == 0)[0] if exchange == "reduce" else np.arange(len(ref_recs))

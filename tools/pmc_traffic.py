@@ -32,7 +32,7 @@ def load(d, counter):
 
 
 def short(name):
-    for k in ("k_gather_tile", "k_gather_grid", "k_gather_knn", "k_gather_kd", "k_trace", "k_eye", "k_bucket_fill",
+    for k in ("k_gather_tile", "k_gather_grid", "k_gather_knn_ss", "k_knn_pack", "k_gather_knn", "k_gather_kd", "k_trace", "k_eye", "k_bucket_fill",
               "k_scan_down", "k_scan_reduce", "k_reset_records", "k_ppm_update", "k_final"):
         if k in name:
             return k
