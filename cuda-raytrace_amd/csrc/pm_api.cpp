@@ -117,36 +117,17 @@ struct Ctx {
     bool tile_count_known = false; /* its length read back (pinned copy + event, never waited on) */
     uint32_t *h_tile_count = nullptr;
     hipEvent_t tile_event = nullptr;
-    bool tile_list = true; /* env PM_TILE_LIST=0: launch over every tile */
     /* pm_reset_records is deferred: records read as (flux 0, N 0, r2 = rec_fresh_r2) */
     bool rec_fresh = false;
     float rec_fresh_r2 = 0.f;
     /* estimator of the last gather: what the records' flux / radius2 /
      * photon_count mean for the final pass (PPM state or kNN sums) */
     int rec_estimator = PM_ESTIMATOR_PPM;
-    int64_t trace_per_block = 0; /* 0: per-lane paths (default); >0: block-compacting pool (env PM_TRACE_PATHS_PER_BLOCK) */
-    int64_t trace_wave_paths = 64; /* per-lane kernel: paths per wave (env PM_TRACE_WAVE_PATHS) */
-    int trace_refill_min = 32;     /* per-lane kernel: idle lanes that trigger a refill (env PM_TRACE_REFILL_MIN) */
-    bool fuse_count = true;        /* bucket counting inside the trace kernel (env PM_FUSE_COUNT=0 disables) */
     int kd_stack = KD_STACK;        /* kd gather stack entries (env PM_KD_STACK, tests only) */
-    bool trace_pool = true;         /* pooled trace kernel for 4-wide BVH scenes (env PM_TRACE_POOL=0 disables) */
-    bool trace_hold = true;         /* deposits written once per path (env PM_TRACE_HOLD=0: per deposit) */
-    bool path_sort = false;         /* pooled kernel: paths by first-ray direction (env PM_PATH_SORT=1) */
-    DevBuf d_porder, d_pscratch;
-    int64_t pool_waves = 0;         /* pooled kernel: waves per launch (env PM_POOL_WAVES; 0 = one occupancy round) */
-    bool key_planes = true;         /* fused bucket keys / ranks plane-major (env PM_KEY_PLANES) */
+    bool trace_hold = true;         /* deposits written once per path where it costs no waves (env PM_TRACE_HOLD=0: per deposit) */
     int pool_stack = 31;            /* pooled kernel: LDS stack entries per lane (env PM_POOL_STACK; 0 = the exact bound): 31 lets five blocks share a CU's LDS */
     DevBuf d_spill;                 /* pooled kernel: stack entries beyond pool_stack */
-    /* wavefront trace (env PM_TRACE_WAVEFRONT=1; 4-wide BVH scenes): one
-     * pooled launch per bounce, rays reordered between bounces by origin cell
-     * (2^wf_bits per axis, env PM_WF_BITS) and direction octant unless
-     * PM_WF_SORT=0 (queue order) */
-    bool trace_wavefront = false;
-    int wf_bits = 4;
-    bool wf_sort = true;
-    DevBuf d_wfq, d_wfw;
-    int gather_kernel = PM_GK_TILE; /* bucket gather kernel (env PM_GATHER_KERNEL=tile|lane|wave) */
-    bool gather_xcd = false;        /* tile gather: contiguous tile ranges per XCD (env PM_GATHER_XCD=1) */
+    int gather_kernel = PM_GK_TILE; /* bucket gather kernel (env PM_GATHER_KERNEL=tile|lane) */
     int cell_span = 2;              /* PPM grid: cells per axis of a query box (env PM_CELL_SPAN 2..5) */
     /* adaptive grid radius (progressive PPM: radii shrink pass by pass). The
      * fused tile gather bins every updated r^2 (R2_BINS log bins per copy,
@@ -156,15 +137,6 @@ struct Ctx {
      * Staleness is safe (radii only shrink); anything that can raise a
      * radius (eye pass, reset, upload, set_radius2, split / partial updates)
      * invalidates it. env PM_GRID_QUANTILE (default 0.9; <= 0 disables). */
-    /* gather order (incoherent scenes, launch_record_order): active records
-     * in cell order, built once per eye pass; env PM_REC_ORDER = 1 always,
-     * -1 auto (when > 20 % of the active tiles do not fit one LDS group),
-     * default 0 off: measured slower on C3 (gather 0.56 -> 0.67 ms: the
-     * records' own reads become scattered) */
-    DevBuf d_order, d_ocount, d_ostart, d_oscratch, d_ostats;
-    bool order_valid = false, use_order = false;
-    int64_t n_order = 0;
-    int rec_order_mode = 0;
     DevBuf d_r2hist;
     uint32_t *h_r2hist = nullptr, *h_r2hist_dev = nullptr; /* host-mapped R2_BINS words, its device address */
     hipEvent_t r2_event = nullptr;
@@ -392,7 +364,6 @@ int ensure_records(Ctx *c) {
     HIPCHK(c, c->d_dl.ensure(n * sizeof(float4)));
     c->nrec = n;
     c->tiles_valid = false;
-    c->order_valid = false;
     c->r2_valid = false;
     c->design_r2 = 0.f;
     return PM_OK;
@@ -428,7 +399,6 @@ GatherParams gather_params(Ctx *c, const pm_render_params *p) {
     G.kd_stack = c->kd_stack;
     G.error = reinterpret_cast<unsigned int *>(c->d_counters.as<unsigned long long>() + 16);
     G.fx_nonneg = c->scene_nonneg && c->slots_nonneg ? 1 : 0;
-    G.xcd = c->gather_xcd ? 1 : 0;
     G.span = grid_span(c->grid, c->grid_r2 > 0.f ? c->grid_r2 : p->initial_radius2);
     if (c->view_active) { G.view_rank = c->d_vrank.as<uint32_t>(); G.view_list = c->d_vlist.as<uint32_t>(); }
     /* fixed-point scale 2^S: a single contribution is bounded by
@@ -498,7 +468,7 @@ struct SceneLayout {
            o_spheres = 0, o_mats = 0, o_lights = 0, o_wnodes = 0, bytes = 0;
     int64_t n_nodes = 0, n_refs = 0, n_tris = 0;
     bool id_order = false;
-    int wide = 0, wide_stack = 0, nodelets = 0;
+    int wide = 0, wide_stack = 0;
 };
 
 /* per triangle t: (p0, e0, e1, n) for the intersector, the normalized
@@ -547,10 +517,8 @@ bool gpu_bvh_wanted(int64_t nprims) {
     if (const char *e = getenv("PM_BVH_GPU_MIN")) gmin = std::max<int64_t>(2, atoll(e));
     const bool want = m == "gpu" ? nprims >= 2 : (m == "auto" && nprims >= gmin);
     if (!want || PM_BVH4_QUANT == 0) return false;
-    /* the host path's experiment knobs for the 4-wide tree are host-only */
-    for (const char *k : {"PM_BVH_WIDE", "PM_BVH4_LEAF", "PM_NODELETS", "PM_BVH4_BFS", "PM_LEAF_TRIS", "PM_BVH_LEAF_MAX"})
-        if (getenv(k)) return false;
-    return true;
+    /* the breadth-first renumbering of the host tree is a host-path switch */
+    return getenv("PM_BVH4_BFS") == nullptr;
 }
 
 struct TmpBuf : DevBuf {
@@ -669,7 +637,6 @@ int commit_gpu_bvh(Ctx *c, const std::vector<BuildPrim> &prims, int64_t nt, Scen
     L.id_order = false;
     L.wide = 2;
     L.wide_stack = out.max_stack;
-    L.nodelets = 0;
     built = true;
     return PM_OK;
 }
@@ -753,28 +720,13 @@ int pm_create(void **out, const pm_config *cfg) {
     if (dev < 0 || dev >= ndev) FAIL((Ctx *)nullptr, PM_ERR_INVALID, "device %d out of range (%d devices)", dev, ndev);
     Ctx *c = new Ctx();
     c->device = dev;
-    if (const char *e = getenv("PM_TRACE_PATHS_PER_BLOCK")) c->trace_per_block = std::max(0LL, atoll(e));
-    if (const char *e = getenv("PM_TRACE_WAVE_PATHS")) c->trace_wave_paths = std::max(64LL, atoll(e));
-    if (const char *e = getenv("PM_TRACE_REFILL_MIN")) c->trace_refill_min = std::max(1, std::min(64, atoi(e)));
-    if (const char *e = getenv("PM_FUSE_COUNT")) c->fuse_count = atoi(e) != 0;
     if (const char *e = getenv("PM_GATHER_KERNEL"))
-        c->gather_kernel = !strcmp(e, "lane") ? PM_GK_LANE : !strcmp(e, "wave") ? PM_GK_WAVE : PM_GK_TILE;
-    if (const char *e = getenv("PM_GATHER_WAVE")) if (atoi(e)) c->gather_kernel = PM_GK_WAVE;
-    if (const char *e = getenv("PM_GATHER_XCD")) c->gather_xcd = atoi(e) != 0;
+        c->gather_kernel = !strcmp(e, "lane") ? PM_GK_LANE : PM_GK_TILE;
     if (const char *e = getenv("PM_KNN_SS")) c->knn_ss = atoi(e) != 0;
     if (const char *e = getenv("PM_CELL_SPAN")) c->cell_span = std::max(2, std::min(5, atoi(e)));
     if (const char *e = getenv("PM_GRID_QUANTILE")) c->grid_quantile = atof(e);
-    if (const char *e = getenv("PM_REC_ORDER")) c->rec_order_mode = atoi(e);
-    if (const char *e = getenv("PM_TRACE_POOL")) c->trace_pool = atoi(e) != 0;
     if (const char *e = getenv("PM_TRACE_HOLD")) c->trace_hold = atoi(e) != 0;
-    if (const char *e = getenv("PM_PATH_SORT")) c->path_sort = atoi(e) != 0;
-    if (const char *e = getenv("PM_POOL_WAVES")) c->pool_waves = std::max(1LL, atoll(e));
-    if (const char *e = getenv("PM_KEY_PLANES")) c->key_planes = atoi(e) != 0;
     if (const char *e = getenv("PM_POOL_STACK")) c->pool_stack = std::max(0, atoi(e));
-    if (const char *e = getenv("PM_TRACE_WAVEFRONT")) c->trace_wavefront = atoi(e) != 0;
-    if (const char *e = getenv("PM_WF_BITS")) c->wf_bits = std::max(0, std::min(9, atoi(e)));
-    if (const char *e = getenv("PM_WF_SORT")) c->wf_sort = atoi(e) != 0;
-    if (const char *e = getenv("PM_TILE_LIST")) c->tile_list = atoi(e) != 0;
     if (const char *e = getenv("PM_KD_STACK")) c->kd_stack = std::max(1, std::min(KD_STACK, atoi(e)));
     if (const char *e = getenv("PM_STAGE_TIMERS")) if (atoi(e) == 0) c->timed_stages.clear();
     (void)hipSetDevice(dev);
@@ -814,8 +766,7 @@ void pm_destroy(void *ptr) {
                       &c->d_dl, &c->d_slots, &c->d_count, &c->d_scratch, &c->d_vflags, &c->d_vrank, &c->d_vlist, &c->d_vsums,
                       &c->d_cell_start, &c->d_pha, &c->d_phb, &c->d_knnpk, &c->d_knnovf,
                       &c->d_kd, &c->d_out, &c->d_counters, &c->d_tiles, &c->d_tile_flags, &c->d_tile_count,
-                      &c->d_r2hist, &c->d_order, &c->d_ocount, &c->d_ostart, &c->d_oscratch, &c->d_ostats,
-                      &c->d_porder, &c->d_pscratch, &c->d_spill, &c->d_wfq, &c->d_wfw};
+                      &c->d_r2hist, &c->d_spill};
     for (DevBuf *b : bufs) b->release();
     if (c->tile_event) (void)hipEventDestroy(c->tile_event);
     if (c->r2_event) (void)hipEventDestroy(c->r2_event);
@@ -1061,8 +1012,6 @@ int pm_commit(void *ptr) {
         L = SceneLayout();
         BvhOut bvh;
         BvhCost cost;
-        if (const char *e = getenv("PM_BVH_LEAF_MAX")) cost.leaf_max = std::max(1, atoi(e));
-        if (const char *e = getenv("PM_BVH_CTRAV")) cost.c_trav = (float)atof(e);
         const auto t_build0 = tnow();
         /* env PM_BVH_BUILD=ploc-host: the device builder's PLOC tree built on
          * the host (A/B of the tree quality; PM_PLOC_RADIUS) */
@@ -1079,12 +1028,10 @@ int pm_commit(void *ptr) {
         c->bvh_depth = bvh.depth;
         if (bvh.depth >= BVH_STACK) FAIL(c, PM_ERR_INVALID, "BVH too deep (%d)", bvh.depth);
 
-        /* tiny LDS scenes skip the BVH (MODE_BRUTE); env PM_TRACE_BRUTE_MAX
-         * overrides the limit (0 = never). Their triangles are stored in global-id
-         * order (brute_isect's tie-break relies on it), others in leaf order. */
-        const char *brute_env = getenv("PM_TRACE_BRUTE_MAX");
-        const int brute_max = brute_env ? atoi(brute_env) : BRUTE_MAX_PRIMS;
-        const bool id_order = (int64_t)bvh.refs.size() <= brute_max;
+        /* tiny LDS scenes skip the BVH (MODE_BRUTE). Their triangles are stored
+         * in global-id order (brute_isect's tie-break relies on it), others in
+         * leaf order. */
+        const bool id_order = (int64_t)bvh.refs.size() <= BRUTE_MAX_PRIMS;
         std::vector<uint32_t> tri_order; /* triangle ids in storage order */
         tri_order.reserve(nt);
         if (id_order) {
@@ -1145,38 +1092,31 @@ int pm_commit(void *ptr) {
         L.o_mats = put(c->materials.data(), c->materials.size() * sizeof(float4));
         L.o_lights = put(c->lights.data(), c->lights.size() * sizeof(LightDev));
         /* scenes traversed from HBM also get the 4-wide BVH (half the dependent
-         * node fetches per ray); env PM_BVH_WIDE=0 keeps the binary traversal,
-         * PM_BVH4_LEAF sets the largest subtree folded into one leaf */
+         * node fetches per ray; binary leaves of one primitive) */
         if (blob.size() > LDS_SCENE_MAX) {
-            const char *we = getenv("PM_BVH_WIDE");
-            if (!we || atoi(we) != 0) {
-                const char *le = getenv("PM_BVH4_LEAF");
+            {
                 Bvh4Out w;
                 const auto t_c0 = tnow();
-                collapse_bvh4(bvh, le ? atoi(le) : 1, w);
+                collapse_bvh4(bvh, 1, w);
                 if (ptimes) fprintf(stderr, "pm_commit: collapse %.1f ms\n", tms(t_c0, tnow()));
                 /* node format fixed at build time (pm_device.h PM_BVH4_QUANT) */
                 std::vector<uint32_t> qn;
                 const bool quant = PM_BVH4_QUANT != 0;
-                const char *lt = getenv("PM_LEAF_TRIS"); /* 0: every leaf through its refs (A/B knob) */
                 /* a leaf the quantized count cannot code (>= LEAF_TRIS primitives,
                  * possible at build_bvh's depth limit) keeps the binary traversal,
-                 * like a tree whose stack bound exceeds BVH_STACK */
-                /* env PM_NODELETS=N: the pooled trace kernel keeps the first N nodes
-                 * in LDS, the tree renumbered breadth-first so that they are its
-                 * top levels (PM_BVH4_BFS=1 renumbers without nodelets) */
-                const char *nl = getenv("PM_NODELETS"), *bf = getenv("PM_BVH4_BFS");
-                const int nodelets = nl ? std::max(0, atoi(nl)) : 0;
-                if (nodelets > 0 || (bf && atoi(bf) != 0)) bvh4_bfs_order(w.nodes);
+                 * like a tree whose stack bound exceeds BVH_STACK. env
+                 * PM_BVH4_BFS=1 renumbers the tree breadth-first, the order the
+                 * device build produces (tests/test_bvh_gpu.py compares them) */
+                const char *bf = getenv("PM_BVH4_BFS");
+                if (bf && atoi(bf) != 0) bvh4_bfs_order(w.nodes);
                 const auto t_q0 = tnow();
-                const bool coded = !quant || quantize_bvh4(w.nodes, lt && atoi(lt) == 0 ? std::vector<uint32_t>() : bvh.refs, qn);
+                const bool coded = !quant || quantize_bvh4(w.nodes, bvh.refs, qn);
                 if (ptimes) fprintf(stderr, "pm_commit: quantize %.1f ms\n", tms(t_q0, tnow()));
                 if (coded && w.max_stack <= BVH_STACK) {
                     L.o_wnodes = quant ? put(qn.data(), qn.size() * sizeof(uint32_t))
                                        : put(w.nodes.data(), w.nodes.size() * sizeof(float));
                     L.wide = quant ? 2 : 1;
                     L.wide_stack = w.max_stack;
-                    L.nodelets = nodelets;
                     c->bvh4_nodes = (int64_t)(w.nodes.size() / 32);
                     c->bvh4_depth = w.depth;
                 }
@@ -1215,7 +1155,6 @@ int pm_commit(void *ptr) {
     S.stack_depth = std::min(BVH_STACK, std::max(2, c->bvh_depth + 2));
     S.wide = L.wide;
     S.wnodes = L.wide ? (const float4 *)(base + L.o_wnodes) : nullptr;
-    S.nodelets = L.wide == 2 ? (int)std::min<int64_t>(L.nodelets, c->bvh4_nodes) : 0;
     /* wide scenes traverse only the 4-wide tree (traverse() dispatches every
      * MODE_GLOBAL query to traverse4): its exact stack bound sizes the LDS
      * stacks, not the binary tree's depth — k_trace_pool's 256-thread blocks
@@ -1263,7 +1202,6 @@ int pm_eye_pass(void *ptr, const pm_render_params *p, void *stream) {
     timer_end(c, "eye", s);
     c->rec_fresh = false; /* the eye pass writes every record */
     c->tiles_valid = false;
-    c->order_valid = false;
     c->r2_valid = false;
     c->design_r2 = 0.f;
     if (c->view_active && (rc = build_view(c, s))) return rc;
@@ -1377,49 +1315,6 @@ static hipError_t count_zeroed(Ctx *c, size_t words, hipStream_t s) {
     return e;
 }
 
-/* Wavefront trace (Ctx::trace_wavefront): bounce 0 emits the paths, every
- * later bounce takes the previous one's queue of continuing rays, reordered
- * by (origin cell, direction octant) unless wf_sort is off. A path makes at
- * most mpc + max_spec + 1 rays, so that many launches drain every queue; the
- * counts stay on the device (an empty bounce exits at once). */
-static int trace_wavefront(Ctx *c, TraceParams T, int64_t path_count, hipStream_t s) {
-    const int64_t cap = path_count, cap4 = (cap + 3) & ~(int64_t)3;
-    const int maxb = T.mpc + std::max(T.max_spec, 0) + 2;
-    const int64_t nbins = (int64_t)1 << (3 * c->wf_bits + 3), cnt4 = (2 * maxb + 3) & ~3; /* counts, next positions */
-    HIPCHK(c, c->d_wfq.ensure((size_t)2 * (size_t)cap * WF_ENTRY_F4 * sizeof(float4)));
-    const size_t words = (size_t)(cnt4 + 3 * cap4 + 2 * nbins) + scan_scratch_words(nbins);
-    HIPCHK(c, c->d_wfw.ensure(words * 4));
-    uint32_t *cnt = c->d_wfw.as<uint32_t>(), *key = cnt + cnt4, *rank = key + cap4, *perm = rank + cap4;
-    uint32_t *bins = perm + cap4, *start = bins + nbins, *sums = start + nbins;
-    HIPCHK(c, hipMemsetAsync(cnt, 0, (size_t)cnt4 * 4, s));
-    HIPCHK(c, hipMemsetAsync(bins, 0, (size_t)nbins * 4, s));
-    float4 *Q[2] = {c->d_wfq.as<float4>(), c->d_wfq.as<float4>() + (size_t)cap * WF_ENTRY_F4};
-    T.hold = 0;
-    T.order = nullptr;
-    T.wf_key = key; T.wf_rank = rank; T.wf_bins = c->wf_sort ? bins : nullptr; T.wf_bits = c->wf_bits;
-    for (int a = 0; a < 3; ++a) {
-        T.wf_lo[a] = c->bbox_lo[a];
-        T.wf_scale[a] = (float)(1 << c->wf_bits) / std::max(c->bbox_hi[a] - c->bbox_lo[a], 1e-3f);
-    }
-    for (int b = 0; b < maxb; ++b) {
-        T.wf = b == 0 ? 1 : 2;
-        T.wf_perm = nullptr;
-        if (b > 0) {
-            T.wf_q_in = Q[(b - 1) & 1];
-            T.wf_n_in = cnt + b - 1;
-            T.wf_next = cnt + maxb + b;
-            if (c->wf_sort) {
-                HIPCHK(c, launch_wf_order(cnt + b - 1, (uint32_t)cap, bins, (uint32_t)nbins, start, sums, key, rank, perm, s));
-                T.wf_perm = perm;
-            }
-        }
-        T.wf_q_out = b + 1 < maxb ? Q[b & 1] : nullptr;
-        T.wf_n_out = cnt + b;
-        HIPCHK(c, launch_trace(T, c->counting, s));
-    }
-    return PM_OK;
-}
-
 int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t path_begin, int64_t path_count,
                      int64_t slot_path_base, void *stream) {
     GETCTX(ptr);
@@ -1444,14 +1339,12 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
         }
     }
     T.path_begin = path_begin; T.path_count = path_count; T.slot_path_base = slot_path_base;
-    T.per_block = c->trace_per_block;
-    T.wave_paths = c->trace_wave_paths;
     T.hold = c->trace_hold ? 1 : 0;
     if (T.hold && !c->S.wide) { /* per-lane kernel: only when the held deposits' LDS costs no resident waves */
         const size_t lds = (size_t)c->S.stack_depth * TRACE_BLOCK * 4 + c->S.lds_bytes;
         if (trace_lane_waves_per_cu(c->S, lds, 1) < trace_lane_waves_per_cu(c->S, lds, 0)) T.hold = 0;
     }
-    if (c->trace_pool && T.per_block == 0) {
+    if (c->S.wide) {
         /* pooled kernel: one occupancy round (resident waves per CU from the
          * occupancy API: VGPRs and the LDS stacks) — each wave with a
          * contiguous pool of a multiple of 64 paths. C3 sweep (1M paths, 256 CUs): 4096 waves 5.25 ms, 8192
@@ -1461,19 +1354,16 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
          * the smaller LDS reservation admits more resident blocks */
         const int lstk = c->pool_stack > 0 && c->pool_stack < c->S.stack_depth ? c->pool_stack : c->S.stack_depth;
         T.pool_stack = lstk;
-        int64_t waves = c->pool_waves;
-        if (waves <= 0) {
-            int cus = 0;
-            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0) cus = 256;
-            const size_t lds = (size_t)lstk * TRACE_BLOCK * 4 + c->S.lds_bytes + (size_t)c->S.nodelets * 64;
-            int per_cu = trace_pool_waves_per_cu(lds, 0);
-            if (T.hold && c->S.wide) { /* pooled kernel: the held deposits' LDS must not cost resident waves */
-                const int per_cu_h = trace_pool_waves_per_cu(lds, 1);
-                if (per_cu_h < per_cu) T.hold = 0;
-                else per_cu = per_cu_h;
-            }
-            waves = (int64_t)cus * (per_cu > 0 ? per_cu : 16);
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0) cus = 256;
+        const size_t lds = (size_t)lstk * TRACE_BLOCK * 4 + c->S.lds_bytes;
+        int per_cu = trace_pool_waves_per_cu(lds, 0);
+        if (T.hold) { /* pooled kernel: the held deposits' LDS must not cost resident waves */
+            const int per_cu_h = trace_pool_waves_per_cu(lds, 1);
+            if (per_cu_h < per_cu) T.hold = 0;
+            else per_cu = per_cu_h;
         }
+        const int64_t waves = (int64_t)cus * (per_cu > 0 ? per_cu : 16);
         /* any pool size works (the wave's cursor hands out paths to dead lanes) */
         const int64_t per = std::max<int64_t>(1, (path_count + waves - 1) / waves);
         T.pool_paths = per;
@@ -1485,7 +1375,6 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
             T.spill_stride = (uint32_t)threads;
         }
     }
-    T.refill_min = c->trace_refill_min;
     T.pass = pass; T.mpc = (int)mpc; T.max_spec = p->max_specular_depth; T.light_index = p->light_source_index;
     T.eps = p->scene_epsilon; T.seed = p->rng_seed;
     T.counters = c->d_counters.as<unsigned long long>() + 4;
@@ -1495,7 +1384,7 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
      * of the bucket build (keys, ranks, per-cell counts) at deposit time; the
      * build then skips it (c->fused). Any other slot producer invalidates it. */
     c->fused.valid = false;
-    const bool fuse = c->fuse_count && p->gather_structure == PM_GATHER_GRID && path_begin == slot_path_base;
+    const bool fuse = p->gather_structure == PM_GATHER_GRID && path_begin == slot_path_base;
     if (fuse) {
         c->fused.r2 = grid_radius2(c, p, true);
         const GridDesc g = make_grid(c, p, c->fused.r2);
@@ -1507,26 +1396,14 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
         T.count = c->d_count.as<uint32_t>();
         T.key = c->d_scratch.as<uint32_t>();
         T.rank = c->d_scratch.as<uint32_t>() + end_slot;
-        /* plane-major keys / ranks (env PM_KEY_PLANES=0: slot order); the held
-         * deposits write a path's four keys as one 16-B store in slot order */
-        T.key_np = c->key_planes && !T.hold ? path_count : 0;
-    }
-    if (c->path_sort && T.pool_paths > 0 && c->S.wide) {
-        HIPCHK(c, c->d_porder.ensure((size_t)path_count * 4));
-        HIPCHK(c, c->d_pscratch.ensure(path_order_scratch_words(path_count) * 4));
-        HIPCHK(c, launch_path_order(T, c->d_pscratch.as<uint32_t>(), c->d_porder.as<uint32_t>(), s));
-        T.order = c->d_porder.as<uint32_t>();
+        /* plane-major keys / ranks; the held deposits write a path's four
+         * keys as one 16-B store in slot order */
+        T.key_np = !T.hold ? path_count : 0;
     }
     timer_begin(c, "trace", s);
     /* the kernel writes all path_count * mpc slots: deposits, then zeros */
-    if (c->trace_wavefront && T.pool_paths > 0 && c->S.wide) {
-        rc = trace_wavefront(c, T, path_count, s);
-        timer_end(c, "trace", s);
-        if (rc) return rc;
-    } else {
-        HIPCHK(c, launch_trace(T, c->counting, s));
-        timer_end(c, "trace", s);
-    }
+    HIPCHK(c, launch_trace(T, c->counting, s));
+    timer_end(c, "trace", s);
     if (fuse) { c->fused.valid = true; c->fused.n = end_slot; c->fused.grid = T.grid; c->fused.key_np = T.key_np; c->fused.mpc = (int)mpc; c->count_zero_words = 0; }
     /* traced photons carry the scene's signs (scene_nonneg); slots outside
      * the traced range keep theirs, so the flag is reset only when this
@@ -1620,31 +1497,6 @@ static int ensure_tiles(Ctx *c, hipStream_t s) {
     return PM_OK;
 }
 
-/* the gather order of the active records (records fixed after the eye pass;
- * synchronizes once to read its length and the tile census) */
-static int ensure_order(Ctx *c, const pm_render_params *p, hipStream_t s) {
-    if (c->order_valid) return PM_OK;
-    const GridDesc g = make_grid(c, p, p->initial_radius2);
-    const int64_t n = c->nrec;
-    HIPCHK(c, c->d_order.ensure(std::max<int64_t>(n, 16) * 4));
-    HIPCHK(c, c->d_ocount.ensure(((size_t)g.ncells + 1) * 4));
-    HIPCHK(c, c->d_ostart.ensure(((size_t)g.ncells + 1) * 4));
-    HIPCHK(c, c->d_oscratch.ensure(record_order_scratch_words(n, g.ncells) * 4));
-    HIPCHK(c, c->d_ostats.ensure(16));
-    HIPCHK(c, launch_record_order(recs(c), g, p->initial_radius2, c->d_ocount.as<uint32_t>(), c->d_ostart.as<uint32_t>(),
-                                  c->d_oscratch.as<uint32_t>(), c->d_order.as<uint32_t>(),
-                                  c->d_ostats.as<unsigned long long>(), s));
-    unsigned long long st[2] = {0, 0};
-    uint32_t na = 0;
-    HIPCHK(c, hipMemcpyAsync(st, c->d_ostats.p, 16, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipMemcpyAsync(&na, c->d_ostart.as<uint32_t>() + g.ncells, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    c->n_order = na;
-    c->use_order = c->rec_order_mode == 1 || (c->rec_order_mode < 0 && (double)st[0] > 0.2 * (double)st[1]);
-    c->order_valid = true;
-    return PM_OK;
-}
-
 static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, int64_t rec_begin, int64_t rec_count,
                          void *stream, int *count = nullptr, long long *flux = nullptr) {
     int rc;
@@ -1672,17 +1524,12 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
     else if ((rc = materialize_reset(c, s))) return rc;
     /* full-range tile gathers skip the tiles without an active record (their
      * records are neither read nor written, except as partials outside a view) */
-    if (c->tile_list && c->gather_kernel == PM_GK_TILE && !c->counting && rec_begin == 0 && rec_count == c->nrec &&
+    if (c->gather_kernel == PM_GK_TILE && !c->counting && rec_begin == 0 && rec_count == c->nrec &&
         p->gather_structure == PM_GATHER_GRID && ((!partial && !split) || c->view_active)) {
         if ((rc = ensure_tiles(c, s))) return rc;
         G.tiles = c->d_tiles.as<uint32_t>();
         if (c->tile_count_known) { G.n_tiles = c->n_tiles; G.n_tiles_dev = nullptr; }
         else { G.n_tiles = (c->nrec + 63) / 64; G.n_tiles_dev = c->d_tile_count.as<uint32_t>(); }
-        /* incoherent tiles (fused gathers): waves over the records in cell order */
-        if (!partial && !split && c->rec_order_mode != 0 && p->estimator == PM_ESTIMATOR_PPM) {
-            if ((rc = ensure_order(c, p, s))) return rc;
-            if (c->use_order) { G.order = c->d_order.as<uint32_t>(); G.n_order = c->n_order; G.tiles = nullptr; }
-        }
     }
     if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters.p, 0, 32, s));
     /* a fused full PPM tile gather bins the updated radii (grid_radius2) */
@@ -2233,7 +2080,6 @@ int pm_upload_records(void *ptr, const pm_record *in, int64_t n) {
     HIPCHK(c, hipMemcpy(c->d_n.p, N.data(), n * 4, hipMemcpyHostToDevice));
     c->rec_fresh = false; /* every record overwritten */
     c->tiles_valid = false;
-    c->order_valid = false;
     c->r2_valid = false;
     c->design_r2 = 0.f;
     if (c->view_active && (rc = build_view(c, c->stream))) return rc;

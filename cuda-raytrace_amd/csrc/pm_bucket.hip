@@ -195,14 +195,6 @@ hipError_t launch_exclusive_scan(const uint32_t *in, int64_t n, uint32_t *out, u
     pm_launch(k_scan_down, dim3(ntile), dim3(SCAN_BLOCK), 0, s, in, n, sums, out, nullptr);
     return hipGetLastError();
 }
-hipError_t launch_exclusive_scan_clear(uint32_t *in, int64_t n, uint32_t *out, uint32_t *sums, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    const int ntile = (int)((n + SCAN_TILE - 1) / SCAN_TILE);
-    pm_launch(k_scan_reduce, dim3(ntile), dim3(SCAN_BLOCK), 0, s, in, n, sums);
-    pm_launch(k_scan_down, dim3(ntile), dim3(SCAN_BLOCK), 0, s, in, n, sums, out, in);
-    return hipGetLastError();
-}
-
 size_t bucket_scratch_words(int64_t n_slots, uint32_t ncells) {
     const int64_t ntile = ((int64_t)ncells + 1 + SCAN_TILE - 1) / SCAN_TILE;
     return (size_t)(2 * n_slots + ntile + 16);
@@ -224,78 +216,6 @@ hipError_t launch_bucket_build(const pm_photon *slots, int64_t n, GridDesc g, ui
     if (n > 0)
         pm_launch(k_bucket_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slots, n, key, rank,
                            cell_start, ph_a, ph_b, key_np, mpc > 0 ? mpc : 1);
-    return hipGetLastError();
-}
-
-/* ---------------------------------------------------------------------- */
-/* Gather order of the active records: their cell keys on
- * grid g (row-major z, y, x), counting-sorted like the photons, so that the
- * 64 records of a gather wave share bucket rows even when the 8x8 pixel
- * tiles do not (a triangle soup: neighbouring pixels on unrelated
- * triangles). The census counts tiles whose cell boxes ([p - r', p + r']
- * for r'^2 = r2) do not fit one 64-row group, and active tiles. */
-PMD uint32_t wave_min_u(uint32_t v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off));
-    return v;
-}
-PMD uint32_t wave_max_u(uint32_t v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
-    return v;
-}
-__global__ __launch_bounds__(256) void k_rec_key(RecordsDev R, GridDesc g, float rq, uint32_t *count, uint32_t *key_out,
-                                                 uint32_t *rank_out, unsigned long long *stats) {
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    bool act = false;
-    float4 pos = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (r < R.count) {
-        pos = R.pos[r];
-        act = !((uint32_t)__float_as_int(pos.w) & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID));
-    }
-    uint32_t key = 0xffffffffu, rank = 0u;
-    uint32_t y0 = 0xffffffffu, y1 = 0u, z0 = 0xffffffffu, z1 = 0u;
-    if (act) {
-        const uint32_t cx = cell_axis(pos.x, g.gx, g.inv_cs, g.dx);
-        const uint32_t cy = cell_axis(pos.y, g.gy, g.inv_cs, g.dy);
-        const uint32_t cz = cell_axis(pos.z, g.gz, g.inv_cs, g.dz);
-        key = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx + cx;
-        rank = atomicAdd(&count[key], 1u);
-        y0 = cell_axis(pos.y - rq, g.gy, g.inv_cs, g.dy); y1 = cell_axis(pos.y + rq, g.gy, g.inv_cs, g.dy);
-        z0 = cell_axis(pos.z - rq, g.gz, g.inv_cs, g.dz); z1 = cell_axis(pos.z + rq, g.gz, g.inv_cs, g.dz);
-    }
-    if (r < R.count) { key_out[r] = key; rank_out[r] = rank; }
-    /* the tile (= this wave's 64 records): does its union fit 8 rows x 8 layers? */
-    const bool any = __ballot(act) != 0ull;
-    const uint32_t Y0 = wave_min_u(y0), Y1 = wave_max_u(y1), Z0 = wave_min_u(z0), Z1 = wave_max_u(z1);
-    if (any && (threadIdx.x & 63) == 0) {
-        atomicAdd(&stats[1], 1ull);
-        if (Y1 - Y0 >= 8u || Z1 - Z0 >= 8u) atomicAdd(&stats[0], 1ull);
-    }
-}
-__global__ __launch_bounds__(256) void k_rec_fill(int64_t n, const uint32_t *key, const uint32_t *rank,
-                                                  const uint32_t *start, uint32_t *order) {
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= n) return;
-    const uint32_t k = key[r];
-    if (k != 0xffffffffu) order[start[k] + rank[r]] = (uint32_t)r;
-}
-size_t record_order_scratch_words(int64_t nrec, uint32_t ncells) {
-    return (size_t)(2 * nrec) + scan_scratch_words((int64_t)ncells + 1);
-}
-hipError_t launch_record_order(const RecordsDev &R, GridDesc g, float r2, uint32_t *count, uint32_t *start,
-                               uint32_t *scratch, uint32_t *order, unsigned long long *stats, hipStream_t s) {
-    const int64_t n = R.count, nc = (int64_t)g.ncells + 1;
-    if (n <= 0) return hipSuccess;
-    uint32_t *key = scratch, *rank = scratch + n, *sums = scratch + 2 * n;
-    hipError_t e = hipMemsetAsync(count, 0, (size_t)nc * 4, s);
-    if (e == hipSuccess) e = hipMemsetAsync(stats, 0, 16, s);
-    if (e != hipSuccess) return e;
-    const float rq = sqrtf(r2) * 1.0001f + 1e-4f;
-    const unsigned grid = (unsigned)((n + 255) / 256);
-    pm_launch(k_rec_key, dim3(grid), dim3(256), 0, s, R, g, rq, count, key, rank, stats);
-    if ((e = launch_exclusive_scan(count, nc, start, sums, s)) != hipSuccess) return e;
-    pm_launch(k_rec_fill, dim3(grid), dim3(256), 0, s, n, key, rank, start, order);
     return hipGetLastError();
 }
 

@@ -99,7 +99,6 @@ struct SceneDev {
      * for the LDS modes */
     const float4 *wnodes;
     int wide;        /* 4-wide BVH in wnodes: 1 = 128-B float nodes, 2 = 64-B quantized (pm_build.h) */
-    int nodelets;    /* k_trace_pool: the first `nodelets` quantized nodes (top levels, BFS order) go to LDS */
     /* all arrays above are 16-B aligned sections of one blob in HBM */
     const char *blob;
     uint32_t blob_bytes;
@@ -598,11 +597,9 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
 #define PM_BVH4_QUANT 1 /* build-time node format: 1 = quantized 64-B nodes, 0 = 128-B float nodes */
 #endif
 PMD void node4_test(const SceneDev &S, int cur, const v3 &oinv, const v3 &inv, float tmin, float tmax, float t[4],
-                    int c[4], int n[4], const uint4 *lds_nodes = nullptr, int n_lds = 0) {
+                    int c[4], int n[4]) {
     if (PM_BVH4_QUANT) {
-        /* nodelets: the first n_lds nodes (the top levels, breadth-first
-         * order) read from this block's LDS copy */
-        const uint4 *nd = (cur < n_lds ? lds_nodes : reinterpret_cast<const uint4 *>(S.wnodes)) + 4 * cur;
+        const uint4 *nd = reinterpret_cast<const uint4 *>(S.wnodes) + 4 * cur;
         const uint4 w0 = nd[0], w1 = nd[1], w2 = nd[2], w3 = nd[3];
         const float ox = __uint_as_float(w0.x), oy = __uint_as_float(w0.y), oz = __uint_as_float(w0.z);
         /* step 2^e: exponent field e + 127 = stored byte - 1 */
@@ -738,8 +735,7 @@ struct SpillStack {
 #endif
 /* false once the ray is done (best holds its closest hit, if any) */
 template <class C>
-PMD bool trav_step(const SceneDev &S, const Ray &ray, TravState &T, const SpillStack &stk, C &cen,
-                   const uint4 *lds_nodes = nullptr, int n_lds = 0) {
+PMD bool trav_step(const SceneDev &S, const Ray &ray, TravState &T, const SpillStack &stk, C &cen) {
     if (T.l0n != 0) {
         leaf_isect<false, PM_BVH4_QUANT != 0>(S, T.l0s, T.l0n, ray, T.best, cen);
         T.l0s = T.l1s; T.l0n = T.l1n; T.l1s = T.l2s; T.l1n = T.l2n; T.l2s = T.l3s; T.l2n = T.l3n; T.l3n = 0;
@@ -761,7 +757,7 @@ PMD bool trav_step(const SceneDev &S, const Ray &ray, TravState &T, const SpillS
     const float INF = __int_as_float(0x7f800000);
     float t[4];
     int c[4], n[4];
-    node4_test(S, T.cur, T.oinv, T.inv, ray.tmin, T.best.t, t, c, n, lds_nodes, n_lds);
+    node4_test(S, T.cur, T.oinv, T.inv, ray.tmin, T.best.t, t, c, n);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         if (t[k] != INF && n[k] > 0) {

@@ -377,15 +377,6 @@ PMD int64_t xcd_tile(int64_t w, int64_t nt) {
 #endif
     return w;
 }
-/* blockIdx -> block of tiles. Blocks are dispatched round-robin over the 8
- * XCDs; with xcd set, XCD x processes one contiguous range of tiles, so the
- * photon rows neighbouring tiles share stay in that XCD's own L2 */
-PMD int64_t gather_block(const GatherParams &P) {
-    const uint32_t b = blockIdx.x;
-    if (!P.xcd) return b;
-    const uint32_t nb = gridDim.x, q = nb / 8u, rm = nb % 8u, x = b % 8u, i = b / 8u;
-    return (int64_t)((x < rm ? x * (q + 1u) : rm * (q + 1u) + (x - rm) * q) + i);
-}
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 /* integer-valued double in [0, 2^53) -> int64, exactly (two 32-bit halves) */
@@ -530,18 +521,14 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
     TileLds &T = tiles[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     int64_t r;
-    if (P.order) { /* active records in cell order (incoherent tiles); past the end: not live */
-        const int64_t i = ((int64_t)blockIdx.x * (TILE_BLOCK / 64) + (threadIdx.x >> 6)) * 64 + lane;
-        if (i - lane >= P.n_order) return;
-        r = i < P.n_order ? (int64_t)P.order[i] : P.rec_end;
-    } else if (P.tiles) { /* only tiles with an active record (no block-level barrier below: a wave may leave) */
+    if (P.tiles) { /* only tiles with an active record (no block-level barrier below: a wave may leave) */
         int64_t w = (int64_t)blockIdx.x * (TILE_BLOCK / 64) + (threadIdx.x >> 6);
         const int64_t nt = P.n_tiles_dev ? (int64_t)*P.n_tiles_dev : P.n_tiles;
         if (w >= nt) return;
         if (TILE_BLOCK == 64) w = xcd_tile(w, nt);
         r = P.rec_begin + (int64_t)P.tiles[w] * 64 + lane;
     } else {
-        r = P.rec_begin + gather_block(P) * TILE_BLOCK + threadIdx.x;
+        r = P.rec_begin + (int64_t)blockIdx.x * TILE_BLOCK + threadIdx.x;
     }
     const GridDesc &g = P.grid;
     GProf gp;
@@ -848,129 +835,6 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
     if (!PARTIAL && P.r2hist) r2_histogram(P, R.live, R.st.w);
     gp.mark(6);
     gp.flush(P.counters);
-}
-
-/* Wave-cooperative bucket gather. A wave's 64 records are one 8x8 pixel
- * tile, so their bucket rows mostly coincide. The wave walks the union of
- * its lanes' rows once, row by row: the row is chosen wave-uniformly (the
- * first pending row of the first lane that has one), every lane holding that
- * row takes part, and the row's photons are read through the SCALAR cache
- * (uniform addresses, constant address space: s_load, no vector-memory /
- * texture-addresser instruction per photon) and tested by all participants
- * at once. A participant scans the union of the participants' x-ranges, a
- * superset of its own cells; photons outside its cells are farther than its
- * radius (the cells cover [p - r', p + r']), and each of its rows is taken
- * exactly once, so it counts exactly the photons the per-lane kernel counts,
- * and the fixed-point sums make the result bit-identical to it. Lanes whose
- * radius exceeds the grid's design radius (uploaded records) fall back to
- * the per-lane scan. (Census launches use k_gather_grid, see launch_g.)
- * Experiment, off by default (PM_GATHER_WAVE=1): bit-identical, but C2
- * 139 us vs 69 us for k_gather_grid — every photon costs two dependent
- * scalar-load round trips for the whole wave, and every participant tests
- * the union of the tile's x-ranges. */
-template <int PARTIAL>
-__global__ __launch_bounds__(GATHER_BLOCK, 8) void k_gather_wave(GatherParams P) {
-    const int64_t r = P.rec_begin + (int64_t)blockIdx.x * GATHER_BLOCK + threadIdx.x;
-    const GridDesc &g = P.grid;
-    bool live = false, big = false;
-    float4 st = make_float4(0.f, 0.f, 0.f, 0.f);
-    v3 p = mk(0.f, 0.f, 0.f), ns = p, fv = p;
-    float r2 = 0.f;
-    uint32_t x0 = 0, x1 = 0, y0 = 0, y1 = 0, z0 = 0, z1 = 0;
-    uint32_t key0 = 0, key1 = 0, key2 = 0, key3 = 0, pend = 0;
-    if (r < P.rec_end) {
-        const float4 pos = P.R.pos[r];
-        const uint32_t flags = (uint32_t)__float_as_int(pos.w);
-        if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) {
-            if (PARTIAL) write_partial(P, partial_index(P, r), 0, Fx3{0, 0, 0});
-        } else {
-            live = true;
-            st = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : P.R.state[r];
-            const float4 nrm = P.R.nrm[r];
-            r2 = st.w;
-            const float4 m = P.materials[__float_as_int(nrm.w)];
-            fv = __float_as_int(m.w) == PM_MATTE ? xyz(m) * INV_PI : mk(0.f, 0.f, 0.f);
-            p = xyz(pos); ns = xyz(nrm);
-            if (r2 > 0.f) {
-                const float rq = sqrtf(r2) * 1.0001f + 1e-4f;
-                x0 = cell_axis(p.x - rq, g.gx, g.inv_cs, g.dx); x1 = cell_axis(p.x + rq, g.gx, g.inv_cs, g.dx);
-                y0 = cell_axis(p.y - rq, g.gy, g.inv_cs, g.dy); y1 = cell_axis(p.y + rq, g.gy, g.inv_cs, g.dy);
-                z0 = cell_axis(p.z - rq, g.gz, g.inv_cs, g.dz); z1 = cell_axis(p.z + rq, g.gz, g.inv_cs, g.dz);
-                if (y1 <= y0 + 1 && z1 <= z0 + 1 && x1 <= x0 + 1) {
-                    const uint32_t dy = (uint32_t)g.dy;
-                    key0 = z0 * dy + y0; key1 = z0 * dy + y1; key2 = z1 * dy + y0; key3 = z1 * dy + y1;
-                    pend = 1u | (y1 > y0 ? 2u : 0u) | (z1 > z0 ? 4u : 0u) | (y1 > y0 && z1 > z0 ? 8u : 0u);
-                } else {
-                    big = true;
-                }
-            }
-        }
-    }
-    int M = 0;
-    Fx3 Lf{0, 0, 0};
-    const float sc = P.fx_scale;
-    const const_u32_ptr cs = (const_u32_ptr)P.cell_start;
-    const const_f32_ptr pa = (const_f32_ptr)P.ph_a; /* 4 floats per photon */
-    const const_f32_ptr pb = (const_f32_ptr)P.ph_b; /* 8 floats per photon */
-    /* one photon against this lane's record (participants only) */
-    auto test = [&](const float4 a, const float4 b0, const float4 b1, bool part) {
-        const v3 diff = p - xyz(a);
-        const float dist2 = diff.x * diff.x + diff.y * diff.y + diff.z * diff.z;
-        if (part && dist2 < r2) {
-            M++;
-            const v3 wi = mk(a.w, b0.w, b1.x);
-            const v3 c = fabsf(dot(ns, wi)) * fv * xyz(b0); /* processPhoton, gathering.cu:17-23 */
-            Lf.x += to_fx(c.x, sc); Lf.y += to_fx(c.y, sc); Lf.z += to_fx(c.z, sc);
-        }
-    };
-    while (true) {
-        const unsigned long long any = __ballot(pend != 0);
-        if (any == 0ull) break;
-        const int leader = __builtin_ctzll(any);
-        /* the leader's first pending row, broadcast */
-        const uint32_t first = (pend & 1u) ? key0 : (pend & 2u) ? key1 : (pend & 4u) ? key2 : key3;
-        const uint32_t key = __builtin_amdgcn_readlane(first, leader);
-        uint32_t mine = 0u;
-        if ((pend & 1u) && key0 == key) mine = 1u;
-        else if ((pend & 2u) && key1 == key) mine = 2u;
-        else if ((pend & 4u) && key2 == key) mine = 4u;
-        else if ((pend & 8u) && key3 == key) mine = 8u;
-        const bool part = mine != 0u;
-        pend &= ~mine;
-        const uint32_t xs = __builtin_amdgcn_readfirstlane(wave_min_u32(part ? x0 : 0xffffffffu));
-        const uint32_t xe = __builtin_amdgcn_readfirstlane(wave_max_u32(part ? x1 : 0u));
-        const uint32_t row = key * (uint32_t)g.dx;
-        const uint32_t b = __builtin_amdgcn_readfirstlane(cs[row + xs]);
-        const uint32_t e = __builtin_amdgcn_readfirstlane(cs[row + xe + 1]);
-        uint32_t j = b;
-        for (; j + 2 <= e; j += 2) { /* two photons' 48 B each in flight through the scalar cache */
-            const float4 a0 = ldc4(pa + 4 * j), a1 = ldc4(pa + 4 * j + 4);
-            const float4 b00 = ldc4(pb + 8 * j), b01 = ldc4(pb + 8 * j + 4);
-            const float4 b10 = ldc4(pb + 8 * j + 8), b11 = ldc4(pb + 8 * j + 12);
-            test(a0, b00, b01, part);
-            test(a1, b10, b11, part);
-        }
-        if (j < e) test(ldc4(pa + 4 * j), ldc4(pb + 8 * j), ldc4(pb + 8 * j + 4), part);
-    }
-    if (big) { /* radius above the grid's design radius: this lane alone, vector loads */
-        for (uint32_t cz = z0; cz <= z1; ++cz)
-            for (uint32_t cy = y0; cy <= y1; ++cy) {
-                const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
-                const uint32_t b = P.cell_start[row + x0], e = P.cell_start[row + x1 + 1];
-                for (uint32_t j = b; j < e; ++j) test(P.ph_a[j], P.ph_b[2 * (size_t)j], P.ph_b[2 * (size_t)j + 1], true);
-            }
-    }
-    if (live) {
-        if (PARTIAL) {
-            write_partial(P, partial_index(P, r), M, Lf);
-        } else {
-            const double inv = P.fx_inv;
-            const v3 L = mk((float)((double)Lf.x * inv), (float)((double)Lf.y * inv), (float)((double)Lf.z * inv));
-            float N = P.fresh ? 0.f : P.R.n[r];
-            ppm_apply(st, N, M, L, P.ppm_alpha);
-            if (M > 0 || P.fresh) { P.R.state[r] = st; P.R.n[r] = N; }
-        }
-    }
 }
 
 /* ---------------------------------------------------------------------- */
@@ -2349,10 +2213,9 @@ static void launch_tile(const GatherParams &p, unsigned g, hipStream_t s) {
 template <int STRUCT, int PARTIAL, int COUNT>
 static void launch_g(const GatherParams &p, hipStream_t s) {
     unsigned grid = (unsigned)((p.rec_end - p.rec_begin + GATHER_BLOCK - 1) / GATHER_BLOCK);
-    if (STRUCT == PM_GATHER_GRID && !COUNT && p.kernel == PM_GK_TILE && (p.tiles || p.order)) {
-        /* the tile list: only tiles with an active record; or the active
-         * records in cell order, 64 per wave */
-        const int64_t waves = p.order ? (p.n_order + 63) / 64 : p.n_tiles;
+    if (STRUCT == PM_GATHER_GRID && !COUNT && p.kernel == PM_GK_TILE && p.tiles) {
+        /* the tile list: only tiles with an active record */
+        const int64_t waves = p.n_tiles;
         const unsigned g = (unsigned)((waves + TILE_BLOCK / 64 - 1) / (TILE_BLOCK / 64));
         if (g == 0) return;
         launch_tile<PARTIAL>(p, g, s);
@@ -2363,8 +2226,6 @@ static void launch_g(const GatherParams &p, hipStream_t s) {
      * tile and wave kernels find exactly the same photons (bit-identical records) */
     if (STRUCT == PM_GATHER_GRID && !COUNT && p.kernel == PM_GK_TILE)
         launch_tile<PARTIAL>(p, (unsigned)((p.rec_end - p.rec_begin + TILE_BLOCK - 1) / TILE_BLOCK), s);
-    else if (STRUCT == PM_GATHER_GRID && !COUNT && p.kernel == PM_GK_WAVE)
-        pm_launch((k_gather_wave<PARTIAL>), dim3(grid), dim3(GATHER_BLOCK), 0, s, p);
     else if (STRUCT == PM_GATHER_GRID)
         pm_launch((k_gather_grid<PARTIAL, COUNT>), dim3(grid), dim3(GATHER_BLOCK), 0, s, p);
     else

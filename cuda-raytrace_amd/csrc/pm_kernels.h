@@ -45,7 +45,7 @@ constexpr int GATHER_BLOCK = 256;
 #define PM_TILE_BLOCK 64
 #endif
 constexpr int TILE_BLOCK = PM_TILE_BLOCK;
-enum { PM_GK_TILE = 0, PM_GK_LANE = 1, PM_GK_WAVE = 2 };
+enum { PM_GK_TILE = 0, PM_GK_LANE = 1 };
 /* error word of a kd-tree gather: a record's traversal stack overflowed (a
  * subtree would have been dropped), or the node links are not a pbrt tree */
 enum { PM_GATHER_ERR_STACK = 1u, PM_GATHER_ERR_TREE = 2u };
@@ -95,10 +95,7 @@ struct TraceParams {
     uint32_t perm[28];
     uint32_t perm_bits[3]; /* the base 3, 5, 7 tables of perm, 3 bits per digit (permuted_halton4) */
     int64_t path_begin, path_count, slot_path_base;
-    int64_t per_block;  /* > 0: block-compacting kernel, paths per block pool; 0: per-lane kernel */
-    int64_t wave_paths; /* per-lane kernel: paths per wave pool (>= 64; 64 = no refills) */
-    int refill_min;     /* per-lane kernel: refill when at least this many lanes are idle */
-    int64_t pool_paths; /* > 0: pooled kernel (k_trace_pool, 4-wide BVH scenes), paths per wave */
+    int64_t pool_paths; /* > 0: pooled kernel (k_trace_pool, 4-wide BVH scenes), paths per wave; else one path per lane */
     int pass, mpc, max_spec, light_index;
     float eps;
     uint32_t seed;
@@ -109,9 +106,6 @@ struct TraceParams {
     int bucket;
     GridDesc grid;
     uint32_t *count, *key, *rank;
-    /* pooled kernel: non-null -> pool position i traces path path_begin +
-     * order[i] (launch_path_order: paths sorted by first-ray direction) */
-    const uint32_t *order;
     /* per-lane / pooled kernels: a path's deposits held in registers and
      * written once per path (pm_trace.hip Held; used when mpc == 4 and the
      * slot buffer is 16-B aligned) */
@@ -124,25 +118,7 @@ struct TraceParams {
     uint32_t spill_stride;
     /* fused counting: keys / ranks plane-major (deposit k of path i at k * key_np + i) when > 0, else at the slot index */
     int64_t key_np;
-    /* wavefront mode of the pooled kernel (pm_api.cpp trace_wavefront; one
-     * launch per bounce): wf 1 = emit the launch's paths, 2 = take the rays of
-     * queue wf_q_in (wf_n_in of them on the device, in wf_perm's order when
-     * non-null); both hand every continuing path to queue wf_q_out (48-B
-     * WfRay entries, wave-aggregated append to *wf_n_out) together with its
-     * reorder key (origin cell Morton code x direction octant) and rank in
-     * the key's bin counter. wf_q_out null: the last bounce (no path can
-     * continue) */
-    int wf;
-    const uint32_t *wf_n_in, *wf_perm;
-    const float4 *wf_q_in;
-    float4 *wf_q_out;
-    uint32_t *wf_n_out, *wf_key, *wf_rank, *wf_bins;
-    uint32_t *wf_next; /* wf 2: the queue's next untaken position (waves take runs of it as lanes free up) */
-    float wf_lo[3], wf_scale[3]; /* origin -> [0, 2^wf_bits) per axis */
-    int wf_bits;
 };
-/* wavefront ray queue entry: (o, tmin) (d, pid) (alpha, nI | stored << 8 | spec << 16) */
-constexpr int WF_ENTRY_F4 = 3;
 
 struct GatherParams {
     RecordsDev R;
@@ -179,20 +155,14 @@ struct GatherParams {
     const uint32_t *view_rank;
     const uint32_t *view_list;
     /* grid gather kernel (PM_GK_*): tile (k_gather_tile, LDS-staged, default),
-     * lane (k_gather_grid, per lane from global memory), wave (k_gather_wave,
-     * scalar-cache experiment); census launches always run k_gather_grid */
+     * lane (k_gather_grid, per lane from global memory); census launches
+     * always run k_gather_grid */
     int kernel;
-    int xcd; /* tile kernel: contiguous tile ranges per XCD (gather_block) */
     int span; /* tile kernel: cells per axis of a lane box at the grid's design radius (2..5) */
     /* non-null: k_gather_tile bins every updated radius, R2_COPIES x R2_BINS
      * counters, bin = floor(-log2(r^2 * r2hist_inv) * R2_PER_OCTAVE) clamped */
     uint32_t *r2hist;
     float r2hist_inv;
-    /* non-null (k_gather_tile, full fused gathers of incoherent scenes): wave
-     * w gathers records order[64 w + lane] (< n_order), the active records in
-     * cell order, instead of tile w */
-    const uint32_t *order;
-    int64_t n_order;
     /* kNN estimator (k_gather_knn): knn_k nearest photons with d^2 < knn_r2;
      * per-record fixed-point scale = power of two below knn_fx * r_k^2;
      * slots = the slot buffer the buckets were built from (ph_b carries the
@@ -243,14 +213,6 @@ hipError_t launch_simple(const EyeParams &p, float *out, hipStream_t s);
 /* resident waves of k_trace_pool per CU with `lds` bytes of dynamic LDS per block */
 int trace_pool_waves_per_cu(size_t lds, int hold);
 size_t scan_scratch_words(int64_t n);
-size_t path_order_scratch_words(int64_t n);
-hipError_t launch_path_order(const TraceParams &p, uint32_t *scratch, uint32_t *order, hipStream_t s);
-/* wavefront mode: the next bounce's order of queue entries [0, *n): scan of
- * the key bins (zeroed as they are read) + scatter by key and rank */
-hipError_t launch_wf_order(const uint32_t *n, uint32_t cap, uint32_t *bins, uint32_t nbins, uint32_t *start,
-                           uint32_t *sums, const uint32_t *key, const uint32_t *rank, uint32_t *perm, hipStream_t s);
-/* exclusive scan that zeroes `in` as it reads it (pm_bucket.hip) */
-hipError_t launch_exclusive_scan_clear(uint32_t *in, int64_t n, uint32_t *out, uint32_t *sums, hipStream_t s);
 int trace_lane_waves_per_cu(const SceneDev &S, size_t lds, int hold);
 /* adaptive-grid histogram: sum the R2_COPIES copies into host-mapped
  * out[R2_BINS] with plain stores (no copy engine) and zero the copies */
@@ -282,12 +244,6 @@ hipError_t launch_radius2_io(const RecordsDev &R, float *buf, int64_t rec_begin,
 /* exclusive scan of n uint32 (pm_bucket.hip); in/out 16-B aligned; sums: scan_scratch_words(n) */
 size_t scan_scratch_words(int64_t n);
 hipError_t launch_exclusive_scan(const uint32_t *in, int64_t n, uint32_t *out, uint32_t *sums, hipStream_t s);
-/* gather order of the active records (cell order on g) + tile census
- * stats[0] = tiles whose union exceeds one group, stats[1] = active tiles;
- * start[ncells] = number of active records */
-size_t record_order_scratch_words(int64_t nrec, uint32_t ncells);
-hipError_t launch_record_order(const RecordsDev &R, GridDesc g, float r2, uint32_t *count, uint32_t *start,
-                               uint32_t *scratch, uint32_t *order, unsigned long long *stats, hipStream_t s);
 /* active-record view: flags/rank n+1 words, list n words; rank[n] = active count */
 hipError_t launch_record_view(const RecordsDev &R, uint32_t *flags, uint32_t *rank, uint32_t *list, uint32_t *sums,
                               hipStream_t s);

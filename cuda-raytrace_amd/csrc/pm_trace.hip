@@ -472,123 +472,18 @@ PMD void finish_path(const TraceParams &P, PathState &st, const Held *held = nul
     }
 }
 
-constexpr int STATE_WORDS = 13;
-
-PMD void state_put(uint32_t (*lds)[TRACE_BLOCK], int slot, const PathState &st) {
-    lds[0][slot] = __float_as_uint(st.ray.o.x); lds[1][slot] = __float_as_uint(st.ray.o.y);
-    lds[2][slot] = __float_as_uint(st.ray.o.z); lds[3][slot] = __float_as_uint(st.ray.d.x);
-    lds[4][slot] = __float_as_uint(st.ray.d.y); lds[5][slot] = __float_as_uint(st.ray.d.z);
-    lds[6][slot] = __float_as_uint(st.ray.tmin); lds[7][slot] = __float_as_uint(st.alpha.x);
-    lds[8][slot] = __float_as_uint(st.alpha.y); lds[9][slot] = __float_as_uint(st.alpha.z);
-    lds[10][slot] = st.pid; lds[11][slot] = st.nI | (st.stored << 8); lds[12][slot] = st.spec;
-}
-
-PMD void state_get(uint32_t (*lds)[TRACE_BLOCK], int slot, PathState &st) {
-    st.ray.o = mk(__uint_as_float(lds[0][slot]), __uint_as_float(lds[1][slot]), __uint_as_float(lds[2][slot]));
-    st.ray.d = mk(__uint_as_float(lds[3][slot]), __uint_as_float(lds[4][slot]), __uint_as_float(lds[5][slot]));
-    st.ray.tmin = __uint_as_float(lds[6][slot]);
-    st.ray.tmax = RT_DEFAULT_MAX;
-    st.alpha = mk(__uint_as_float(lds[7][slot]), __uint_as_float(lds[8][slot]), __uint_as_float(lds[9][slot]));
-    st.pid = lds[10][slot];
-    st.nI = lds[11][slot] & 0xffu; st.stored = lds[11][slot] >> 8;
-    st.spec = lds[12][slot];
-}
-
-/* Block-compacting photon tracer. Block b owns paths
- * [b*per_block, (b+1)*per_block) of the launch. Each iteration every live
- * thread advances its path by one ray; then live paths are compacted to the
- * front of the block (wave ballot + popcount ranks, LDS state exchange) and
- * the tail is refilled with fresh paths from the block's pool. Dead lanes
- * thus retire whole waves instead of idling inside them: the kernel is
- * VALU-issue bound, and a wave otherwise runs until its longest path ends.
- * Results are identical to one-thread-per-path (path math unchanged).
+/* Per-lane photon tracer: one path per lane, no block barriers; a wave lives
+ * as long as its longest path (C2: one occupancy round of 4,096 waves, 3.46
+ * rays per path on average). Pools of several paths per lane, refilled as
+ * lanes finish, and a block-compacting variant were measured slower (DESIGN.md
+ * §5) and removed. HOLD: deposits held in LDS and written per path.
  * COUNT: census [rays traced, BVH nodes entered, primitive tests, photons
  * deposited], one atomic per wave (counting launches only, never timed). */
-template <int COUNT, int MODE>
-__global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceParams P) {
-    extern __shared__ __attribute__((aligned(16))) int stk[]; /* [stack_depth x TRACE_BLOCK][scene blob (LDS)] */
-    __shared__ uint32_t perm[28];
-    __shared__ uint32_t sstate[STATE_WORDS][TRACE_BLOCK];
-    __shared__ uint32_t wcount[TRACE_BLOCK / 64];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid < 28) perm[tid] = P.perm[tid];
-    const SceneDev S = scene_view<MODE != MODE_GLOBAL>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * TRACE_BLOCK),
-                                                       tid, TRACE_BLOCK);
-    __syncthreads();
-    int *stack = stk + tid;
-    typename std::conditional<COUNT != 0, Census, NoCensus>::type cen;
-    uint32_t rays = 0, deposits = 0;
-
-    const int64_t pool_begin = (int64_t)blockIdx.x * P.per_block;
-    const int64_t pool_end = pool_begin + P.per_block < P.path_count ? pool_begin + P.per_block : P.path_count;
-    int64_t next = pool_begin;
-    int live = 0;
-    PathState st;
-    TProf prof;
-    prof.begin();
-    while (true) {
-        const int64_t left = pool_end - next;
-        const int n_new = (int)((int64_t)(TRACE_BLOCK - live) < left ? (int64_t)(TRACE_BLOCK - live) : left);
-        if (live + n_new == 0) break; /* block-uniform: every wave leaves together */
-        bool alive = false;
-        if (tid < live) {
-            alive = true;
-        } else if (tid < live + n_new) {
-            alive = emit_path(P, S, perm, (uint32_t)(P.path_begin + next + (tid - live)), st);
-            if (!alive) finish_path(P, st);
-        }
-        prof.mark(0);
-        if (alive) {
-            ++rays;
-            Held none;
-            alive = path_step<MODE, 0>(P, S, stack, st, cen, prof, none);
-            if (!alive) {
-                if (COUNT) deposits += st.stored;
-                finish_path(P, st);
-            } else {
-                flush_rank(P, st); /* the path state moves through LDS below */
-            }
-        }
-        next += n_new;
-        prof.mark(2);
-        /* compaction: rank = live paths before this thread in the block */
-        const unsigned long long bal = __ballot(alive);
-        if (lane == 0) wcount[wave] = (uint32_t)__popcll(bal);
-        __syncthreads();
-        prof.mark(3);
-        int base = 0, total = 0;
-#pragma unroll
-        for (int w = 0; w < TRACE_BLOCK / 64; ++w) {
-            const int c = (int)wcount[w];
-            base += w < wave ? c : 0;
-            total += c;
-        }
-        if (alive) state_put(sstate, base + __popcll(bal & ((1ull << lane) - 1ull)), st);
-        __syncthreads();
-        live = total;
-        if (tid < live) state_get(sstate, tid, st);
-        prof.mark(4);
-        /* the next writes of wcount / sstate follow the next barrier, which
-         * every thread reaches only after these reads */
-    }
-    prof.flush(P.prof);
-    if (COUNT) {
-        uint32_t nodes = 0, prims = 0;
-        if constexpr (COUNT != 0) { nodes = cen.nodes; prims = cen.prims; }
-        count4(P.counters, rays, nodes, prims, deposits);
-    }
-}
-
-/* Per-lane variant (per_block == 0): no block barriers. Each wave owns
- * wave_paths consecutive paths; every lane runs one path at a time, and when
- * at least refill_min lanes (or all) have finished, the wave hands them the
- * next paths of its pool (ballot + popcount ranks). With wave_paths == 64
- * every lane runs exactly one path and a wave lives as long as its longest. */
 template <int COUNT, int MODE, int HOLD>
 __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
     extern __shared__ __attribute__((aligned(16))) int stk[];
     __shared__ uint32_t perm[28];
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x;
     if (tid < 28) perm[tid] = P.perm[tid];
     const SceneDev S = scene_view<MODE != MODE_GLOBAL>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * TRACE_BLOCK),
                                                        tid, TRACE_BLOCK);
@@ -597,42 +492,23 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
     typename std::conditional<COUNT != 0, Census, NoCensus>::type cen;
     TProf prof;
     uint32_t rays = 0, deposits = 0;
-    const int64_t wave_id = ((int64_t)blockIdx.x * TRACE_BLOCK + tid) >> 6;
-    const int64_t wbegin = wave_id * P.wave_paths;
-    const int64_t wend = wbegin + P.wave_paths < P.path_count ? wbegin + P.wave_paths : P.path_count;
-    int64_t cursor = wbegin; /* wave-uniform: next unassigned path of the pool */
+    const int64_t path = (int64_t)blockIdx.x * TRACE_BLOCK + tid;
     PathState st;
     Held held;
     if (HOLD) /* after the stacks and the (16-B padded) scene blob */
         held.col = reinterpret_cast<uint32_t *>(stk + P.S.stack_depth * TRACE_BLOCK + (MODE != MODE_GLOBAL ? (int)((P.S.lds_bytes + 15u) / 4u & ~3u) : 0)) + tid;
-    bool alive = false;
     prof.begin();
-    while (true) {
-        const unsigned long long idle = __ballot(!alive);
-        const int nidle = __popcll(idle);
-        if (cursor < wend && (nidle >= P.refill_min || nidle == 64)) {
-            const int64_t mine = cursor + __popcll(idle & ((1ull << lane) - 1ull));
-            if (!alive && mine < wend) {
-                if (HOLD) held_clear(held);
-                alive = emit_path(P, S, perm, (uint32_t)(P.path_begin + mine), st);
-                if (!alive) finish_path<HOLD>(P, st, &held);
-            }
-            cursor = cursor + nidle < wend ? cursor + nidle : wend;
-        }
+    if (path < P.path_count) {
+        if (HOLD) held_clear(held);
+        bool alive = emit_path(P, S, perm, (uint32_t)(P.path_begin + path), st);
         prof.mark(0);
-        if (!__ballot(alive)) {
-            if (cursor >= wend) break;
-            continue;
-        }
-        if (alive) {
+        while (alive) {
             ++rays;
             alive = path_step<MODE, HOLD>(P, S, stack, st, cen, prof, held);
-            if (!alive) {
-                if (COUNT) deposits += st.stored;
-                finish_path<HOLD>(P, st, &held);
-            }
+            prof.mark(2);
         }
-        prof.mark(2);
+        if (COUNT) deposits += st.stored;
+        finish_path<HOLD>(P, st, &held);
     }
     prof.flush(P.prof);
     if (COUNT) {
@@ -661,80 +537,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
 constexpr int POOL_STEPS = PM_POOL_STEPS, POOL_SHADE_MIN = PM_POOL_SHADE_MIN;
 enum { PHASE_DEAD = 0, PHASE_TRAV = 1, PHASE_SHADE = 2 };
 
-/* Wavefront mode (TraceParams::wf): the pooled kernel runs one bounce per
- * launch. A path whose ray continues leaves the kernel through a queue
- * instead of tracing on in the same lane; between launches the queue is
- * ordered by (origin cell, direction octant) (launch_wf_order), so the rays a
- * wave takes next start close together and head the same way — they walk
- * the same subtrees (shared L2 lines, similar traversal lengths). The path
- * math is the per-lane kernel's (slots bit-identical); only the order in
- * which rays run changes. */
-PMD void wf_load(const TraceParams &P, uint32_t i, PathState &st) {
-    const float4 *q = P.wf_q_in + (size_t)i * WF_ENTRY_F4;
-    const float4 a = q[0], b = q[1], c = q[2];
-    st.ray.o = mk(a.x, a.y, a.z);
-    st.ray.tmin = a.w;
-    st.ray.tmax = RT_DEFAULT_MAX;
-    st.ray.d = mk(b.x, b.y, b.z);
-    st.pid = __float_as_uint(b.w);
-    st.alpha = mk(c.x, c.y, c.z);
-    const uint32_t w = __float_as_uint(c.w);
-    st.nI = w & 0xffu; st.stored = (w >> 8) & 0xffu; st.spec = w >> 16;
-    st.pslot = PSLOT_NONE;
-}
-PMD uint32_t wf_spread(uint32_t v) { /* 10 bits -> every third bit */
-    v = (v | (v << 16)) & 0x030000ffu;
-    v = (v | (v << 8)) & 0x0300f00fu;
-    v = (v | (v << 4)) & 0x030c30c3u;
-    v = (v | (v << 2)) & 0x09249249u;
-    return v;
-}
-/* reorder key: Morton code of the origin's cell (2^wf_bits per axis over the
- * scene box) above the direction octant */
-PMD uint32_t wf_sort_key(const TraceParams &P, v3 o, v3 d) {
-    const float top = (float)((1 << P.wf_bits) - 1);
-    const float v[3] = {o.x, o.y, o.z};
-    uint32_t c[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) c[a] = (uint32_t)fminf(fmaxf((v[a] - P.wf_lo[a]) * P.wf_scale[a], 0.f), top); /* NaN -> 0 */
-    const uint32_t oct = (d.x < 0.f ? 1u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 4u : 0u);
-    return ((wf_spread(c[0]) | (wf_spread(c[1]) << 1) | (wf_spread(c[2]) << 2)) << 3) | oct;
-}
-/* append the continuing path of every calling lane (wave-aggregated: one
- * counter atomic per wave), with its reorder key and rank in the key's bin */
-PMD void wf_push(const TraceParams &P, const PathState &st) {
-    const unsigned long long m = __ballot(1);
-    const int lane = threadIdx.x & 63, leader = __builtin_ctzll(m);
-    uint32_t base = 0u;
-    if (lane == leader) base = atomicAdd(P.wf_n_out, (uint32_t)__popcll(m));
-    base = (uint32_t)__shfl((int)base, leader);
-    const uint32_t i = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    float4 *q = P.wf_q_out + (size_t)i * WF_ENTRY_F4;
-    q[0] = make_float4(st.ray.o.x, st.ray.o.y, st.ray.o.z, st.ray.tmin);
-    q[1] = make_float4(st.ray.d.x, st.ray.d.y, st.ray.d.z, __uint_as_float(st.pid));
-    q[2] = make_float4(st.alpha.x, st.alpha.y, st.alpha.z, __uint_as_float(st.nI | (st.stored << 8) | (st.spec << 16)));
-    if (P.wf_bins) {
-        /* one bin atomic per distinct key of the wave (rays of one wave share
-         * keys once sorted: per-lane atomics serialize on the same word) */
-        const uint32_t k = wf_sort_key(P, st.ray.o, st.ray.d);
-        P.wf_key[i] = k;
-        unsigned long long pend = m;
-        uint32_t rank = 0u;
-        while (pend) {
-            const int l = __builtin_ctzll(pend);
-            const uint32_t kk = (uint32_t)__builtin_amdgcn_readlane((int)k, l);
-            const unsigned long long same = __ballot(k == kk);
-            uint32_t b = 0u;
-            if (lane == l) b = atomicAdd(&P.wf_bins[kk], (uint32_t)__popcll(same));
-            b = (uint32_t)__shfl((int)b, l);
-            if (k == kk) rank = b + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
-            pend &= ~same;
-        }
-        P.wf_rank[i] = rank;
-    }
-}
-
-template <int COUNT, int HOLD, int WF>
+template <int COUNT, int HOLD>
 /* 5 waves/SIMD: 96 VGPRs (102 unconstrained -> 4 waves), no scratch; with
  * the LDS stacks capped at 31 entries (PM_POOL_STACK, the rest spilled) five
  * 256-thread blocks fit a CU. C3 trace (same box): 4.59-4.61 ms at 4 waves,
@@ -762,32 +565,13 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
     TProf prof;
     uint32_t rays = 0, deposits = 0;
     const int64_t wave_id = ((int64_t)blockIdx.x * TRACE_BLOCK + tid) >> 6;
-    int64_t wbegin, wend;
-    if (WF == 2) {
-        /* the queue's rays in its (sorted) order, handed out dynamically: a
-         * refill takes the next run of positions from P.wf_next, so a wave's
-         * lanes get neighbouring rays and no wave is left with a static share
-         * of expensive ones (contiguous static pools of a sorted queue made
-         * the launch wait for the waves that drew the costly regions) */
-        wbegin = 0;
-        wend = (int64_t)*P.wf_n_in;
-    } else {
-        wbegin = wave_id * P.wave_paths;
-        wend = wbegin + P.wave_paths < P.path_count ? wbegin + P.wave_paths : P.path_count;
-    }
+    const int64_t wbegin = wave_id * P.pool_paths;
+    const int64_t wend = wbegin + P.pool_paths < P.path_count ? wbegin + P.pool_paths : P.path_count;
     int64_t cursor = wbegin; /* wave-uniform: next unassigned path of the pool */
     PathState st;
     TravState tr;
     Held held;
     if (HOLD) held.col = reinterpret_cast<uint32_t *>(stk + lstk * TRACE_BLOCK) + tid; /* after the stacks */
-    /* nodelets after the stacks (and the held deposits): the BVH's top levels */
-    const int n_lds = PM_BVH4_QUANT ? S.nodelets : 0;
-    uint4 *lnodes = reinterpret_cast<uint4 *>(stk + lstk * TRACE_BLOCK + (HOLD ? HOLD_WORDS * TRACE_BLOCK : 0));
-    if (n_lds > 0) {
-        const uint4 *g = reinterpret_cast<const uint4 *>(S.wnodes);
-        for (int i = tid; i < 4 * n_lds; i += TRACE_BLOCK) lnodes[i] = g[i];
-        __syncthreads();
-    }
     int phase = PHASE_DEAD;
     while (true) {
         const unsigned long long travm = __ballot(phase == PHASE_TRAV);
@@ -799,17 +583,8 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
         if (travm == 0ull || waiting >= POOL_SHADE_MIN) {
             if (phase == PHASE_SHADE) {
                 ++rays;
-                bool alive = tr.best.ref != 0xffffffffu && path_shade<HOLD>(P, S, st, tr.best, prof, held);
-                if (WF && alive) { /* the next bounce's launch continues the path */
-                    flush_rank(P, st);
-                    if (P.wf_q_out) {
-                        wf_push(P, st);
-                        phase = PHASE_DEAD;
-                    } else { /* past the last bounce a path can reach: never taken */
-                        finish_path<HOLD>(P, st, &held);
-                        phase = PHASE_DEAD;
-                    }
-                } else if (alive) {
+                const bool alive = tr.best.ref != 0xffffffffu && path_shade<HOLD>(P, S, st, tr.best, prof, held);
+                if (alive) {
                     trav_begin(st.ray, tr);
                     phase = PHASE_TRAV;
                 } else {
@@ -819,21 +594,11 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
                 }
             }
             const unsigned long long dm = __ballot(phase == PHASE_DEAD);
-            if (WF == 2 && cursor < wend && dm) {
-                uint32_t b = 0u;
-                if (lane == __builtin_ctzll(dm)) b = atomicAdd(P.wf_next, (uint32_t)__popcll(dm));
-                cursor = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)b, __builtin_ctzll(dm)));
-            }
             if (cursor < wend) {
                 const int64_t mine = cursor + __popcll(dm & ((1ull << lane) - 1ull));
-                if (WF == 2 && phase == PHASE_DEAD && mine < wend) {
-                    wf_load(P, P.wf_perm ? P.wf_perm[mine] : (uint32_t)mine, st);
-                    trav_begin(st.ray, tr);
-                    phase = PHASE_TRAV;
-                } else if (phase == PHASE_DEAD && mine < wend) {
+                if (phase == PHASE_DEAD && mine < wend) {
                     if (HOLD) held_clear(held);
-                    const uint32_t pid = P.order ? (uint32_t)P.path_begin + P.order[mine] : (uint32_t)(P.path_begin + mine);
-                    if (emit_path(P, S, perm, pid, st)) {
+                    if (emit_path(P, S, perm, (uint32_t)(P.path_begin + mine), st)) {
                         trav_begin(st.ray, tr);
                         phase = PHASE_TRAV;
                     } else {
@@ -846,7 +611,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
         }
 #pragma unroll 1
         for (int k = 0; k < POOL_STEPS; ++k)
-            if (phase == PHASE_TRAV && !trav_step(S, st.ray, tr, sstk, cen, lnodes, n_lds)) phase = PHASE_SHADE;
+            if (phase == PHASE_TRAV && !trav_step(S, st.ray, tr, sstk, cen)) phase = PHASE_SHADE;
     }
     if (COUNT) {
         uint32_t nodes = 0, prims = 0;
@@ -855,94 +620,14 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
     }
 }
 
-#define PM_LAUNCH_MODES(KERNEL, GRID, BLOCK, LDS, STREAM, PARAMS, COUNT)                                        \
-    switch (scene_mode((PARAMS).S)) {                                                                            \
-    case MODE_BRUTE:                                                                                             \
-        if (COUNT) pm_launch((KERNEL<1, MODE_BRUTE>), GRID, BLOCK, LDS, STREAM, PARAMS);                \
-        else pm_launch((KERNEL<0, MODE_BRUTE>), GRID, BLOCK, LDS, STREAM, PARAMS);                      \
-        break;                                                                                                   \
-    case MODE_LDS:                                                                                               \
-        if (COUNT) pm_launch((KERNEL<1, MODE_LDS>), GRID, BLOCK, LDS, STREAM, PARAMS);                  \
-        else pm_launch((KERNEL<0, MODE_LDS>), GRID, BLOCK, LDS, STREAM, PARAMS);                        \
-        break;                                                                                                   \
-    default:                                                                                                     \
-        if (COUNT) pm_launch((KERNEL<1, MODE_GLOBAL>), GRID, BLOCK, LDS, STREAM, PARAMS);               \
-        else pm_launch((KERNEL<0, MODE_GLOBAL>), GRID, BLOCK, LDS, STREAM, PARAMS);                     \
-        break;                                                                                                   \
-    }
-
 /* resident waves of the pooled kernel per CU at this LDS size (0 if unknown) */
-int trace_pool_waves_per_cu(size_t lds, int hold) { /* lds: stacks (+ nodelets) */
+int trace_pool_waves_per_cu(size_t lds, int hold) { /* lds: the stacks */
     int blocks = 0;
     if (hold) lds += (size_t)HOLD_WORDS * TRACE_BLOCK * 4;
-    const hipError_t e = hold ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0, 1, 0>, TRACE_BLOCK, lds)
-                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0, 0, 0>, TRACE_BLOCK, lds);
+    const hipError_t e = hold ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0, 1>, TRACE_BLOCK, lds)
+                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0, 0>, TRACE_BLOCK, lds);
     if (e != hipSuccess) return 0;
     return blocks * (TRACE_BLOCK / 64);
-}
-
-/* Path order for the pooled kernel (env PM_PATH_SORT): the launch's paths
- * counting-sorted by the direction of their first ray (octahedral map,
- * PATH_KEY_RES^2 cells), so that a wave's pool starts its rays in similar
- * directions from the light (and their hit points, and the subtrees they
- * visit, cluster). Keys: one emission per path (the same Halton sample and
- * Sample_L the trace recomputes). */
-constexpr int PATH_KEY_RES = 64;
-__global__ __launch_bounds__(256) void k_path_key(TraceParams P, uint32_t *count, uint32_t *key, uint32_t *rank) {
-    __shared__ uint32_t perm[28];
-    if (threadIdx.x < 28) perm[threadIdx.x] = P.perm[threadIdx.x];
-    __syncthreads();
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= P.path_count) return;
-    PathState st;
-    const bool ok = emit_path(P, P.S, perm, (uint32_t)(P.path_begin + i), st);
-    uint32_t k = 0u;
-    if (ok) {
-        const v3 d = st.ray.d;
-        const float l1 = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
-        float u = d.x / l1, v = d.z / l1;
-        if (d.y < 0.f) { const float uu = (1.f - fabsf(v)) * (u < 0.f ? -1.f : 1.f); v = (1.f - fabsf(u)) * (v < 0.f ? -1.f : 1.f); u = uu; }
-        const int iu = min(PATH_KEY_RES - 1, max(0, (int)((u * 0.5f + 0.5f) * PATH_KEY_RES)));
-        const int iv = min(PATH_KEY_RES - 1, max(0, (int)((v * 0.5f + 0.5f) * PATH_KEY_RES)));
-        k = (uint32_t)(iv * PATH_KEY_RES + iu);
-    }
-    key[i] = k;
-    rank[i] = atomicAdd(&count[k], 1u);
-}
-__global__ __launch_bounds__(256) void k_path_fill(int64_t n, const uint32_t *key, const uint32_t *rank,
-                                                   const uint32_t *start, uint32_t *order) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < n) order[start[key[i]] + rank[i]] = (uint32_t)i;
-}
-size_t path_order_scratch_words(int64_t n) {
-    return (size_t)(2 * n) + 2 * ((size_t)PATH_KEY_RES * PATH_KEY_RES + 1) + scan_scratch_words(PATH_KEY_RES * PATH_KEY_RES + 1);
-}
-hipError_t launch_path_order(const TraceParams &p, uint32_t *scratch, uint32_t *order, hipStream_t s) {
-    const int64_t n = p.path_count;
-    if (n <= 0) return hipSuccess;
-    const int64_t nk = (int64_t)PATH_KEY_RES * PATH_KEY_RES + 1;
-    uint32_t *key = scratch, *rank = scratch + n, *count = scratch + 2 * n, *start = count + nk, *sums = start + nk;
-    hipError_t e = hipMemsetAsync(count, 0, (size_t)nk * 4, s);
-    if (e != hipSuccess) return e;
-    const unsigned grid = (unsigned)((n + 255) / 256);
-    pm_launch(k_path_key, dim3(grid), dim3(256), 0, s, p, count, key, rank);
-    if ((e = launch_exclusive_scan(count, nk, start, sums, s)) != hipSuccess) return e;
-    pm_launch(k_path_fill, dim3(grid), dim3(256), 0, s, n, key, rank, start, order);
-    return hipGetLastError();
-}
-
-/* wavefront order: entry i of the queue goes to position start[key] + rank */
-__global__ __launch_bounds__(256) void k_wf_perm(const uint32_t *n, const uint32_t *key, const uint32_t *rank,
-                                                 const uint32_t *start, uint32_t *perm) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i < *n) perm[start[key[i]] + rank[i]] = i;
-}
-hipError_t launch_wf_order(const uint32_t *n, uint32_t cap, uint32_t *bins, uint32_t nbins, uint32_t *start,
-                           uint32_t *sums, const uint32_t *key, const uint32_t *rank, uint32_t *perm, hipStream_t s) {
-    hipError_t e = launch_exclusive_scan_clear(bins, nbins, start, sums, s);
-    if (e != hipSuccess || cap == 0) return e;
-    pm_launch(k_wf_perm, dim3((cap + 255u) / 256u), dim3(256), 0, s, n, key, rank, start, perm);
-    return hipGetLastError();
 }
 
 /* resident waves per CU of the per-lane kernel (scene mode of S) with or
@@ -995,44 +680,27 @@ static void launch_lane(const TraceParams &p, dim3 grid, size_t lds, int count, 
 
 hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s) {
     if (p.path_count <= 0) return hipSuccess;
-    const size_t lds = (size_t)p.S.stack_depth * TRACE_BLOCK * 4 + p.S.lds_bytes;
     if (p.pool_paths > 0 && scene_mode(p.S) == MODE_GLOBAL && p.S.wide) {
         const int lstk = p.pool_stack > 0 && p.pool_stack < p.S.stack_depth ? p.pool_stack : p.S.stack_depth;
         if (lstk < p.S.stack_depth && !p.spill) return hipErrorInvalidValue;
         const size_t lds = (size_t)lstk * TRACE_BLOCK * 4;
-        TraceParams q = p;
-        q.wave_paths = p.pool_paths;
-        const int64_t waves = (p.path_count + q.wave_paths - 1) / q.wave_paths;
+        const int64_t waves = (p.path_count + p.pool_paths - 1) / p.pool_paths;
         const unsigned grid = (unsigned)((waves + TRACE_BLOCK / 64 - 1) / (TRACE_BLOCK / 64));
         const bool hold = trace_hold(p);
-        const size_t lnl = (size_t)(PM_BVH4_QUANT ? p.S.nodelets : 0) * 64; /* nodelet bytes */
-        const size_t lds_h = lds + (hold ? (size_t)HOLD_WORDS * TRACE_BLOCK * 4 : 0) + lnl;
-        if (p.wf) { /* wavefront bounce: no held deposits (a path's state crosses launches) */
-            if (hold) return hipErrorInvalidValue;
-            if (count && p.wf == 1) pm_launch((k_trace_pool<1, 0, 1>), dim3(grid), dim3(TRACE_BLOCK), lds + lnl, s, q);
-            else if (count) pm_launch((k_trace_pool<1, 0, 2>), dim3(grid), dim3(TRACE_BLOCK), lds + lnl, s, q);
-            else if (p.wf == 1) pm_launch((k_trace_pool<0, 0, 1>), dim3(grid), dim3(TRACE_BLOCK), lds + lnl, s, q);
-            else pm_launch((k_trace_pool<0, 0, 2>), dim3(grid), dim3(TRACE_BLOCK), lds + lnl, s, q);
-        }
-        else if (count && hold) pm_launch((k_trace_pool<1, 1, 0>), dim3(grid), dim3(TRACE_BLOCK), lds_h, s, q);
-        else if (count) pm_launch((k_trace_pool<1, 0, 0>), dim3(grid), dim3(TRACE_BLOCK), lds + lnl, s, q);
-        else if (hold) pm_launch((k_trace_pool<0, 1, 0>), dim3(grid), dim3(TRACE_BLOCK), lds_h, s, q);
-        else pm_launch((k_trace_pool<0, 0, 0>), dim3(grid), dim3(TRACE_BLOCK), lds + lnl, s, q);
+        const size_t lds_h = lds + (hold ? (size_t)HOLD_WORDS * TRACE_BLOCK * 4 : 0);
+        if (count && hold) pm_launch((k_trace_pool<1, 1>), dim3(grid), dim3(TRACE_BLOCK), lds_h, s, p);
+        else if (count) pm_launch((k_trace_pool<1, 0>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
+        else if (hold) pm_launch((k_trace_pool<0, 1>), dim3(grid), dim3(TRACE_BLOCK), lds_h, s, p);
+        else pm_launch((k_trace_pool<0, 0>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
         return hipGetLastError();
     }
-    if (p.per_block == 0) {
-        if (p.wave_paths < 64 || p.refill_min < 1) return hipErrorInvalidValue;
-        const int64_t waves = (p.path_count + p.wave_paths - 1) / p.wave_paths;
-        const unsigned grid = (unsigned)((waves + TRACE_BLOCK / 64 - 1) / (TRACE_BLOCK / 64));
-        if (trace_hold(p))
-            launch_lane<1>(p, dim3(grid), lds + ((size_t)p.S.lds_bytes + 15u) / 16u * 16u - p.S.lds_bytes +
-                                              (size_t)HOLD_WORDS * TRACE_BLOCK * 4, count, s);
-        else launch_lane<0>(p, dim3(grid), lds, count, s);
-        return hipGetLastError();
-    }
-    if (p.per_block < 0) return hipErrorInvalidValue;
-    const unsigned grid = (unsigned)((p.path_count + p.per_block - 1) / p.per_block);
-    PM_LAUNCH_MODES(k_trace, dim3(grid), dim3(TRACE_BLOCK), lds, s, p, count);
+    /* one path per lane */
+    const size_t lds = (size_t)p.S.stack_depth * TRACE_BLOCK * 4 + p.S.lds_bytes;
+    const unsigned grid = (unsigned)((p.path_count + TRACE_BLOCK - 1) / TRACE_BLOCK);
+    if (trace_hold(p))
+        launch_lane<1>(p, dim3(grid), lds + ((size_t)p.S.lds_bytes + 15u) / 16u * 16u - p.S.lds_bytes +
+                                          (size_t)HOLD_WORDS * TRACE_BLOCK * 4, count, s);
+    else launch_lane<0>(p, dim3(grid), lds, count, s);
     return hipGetLastError();
 }
 
