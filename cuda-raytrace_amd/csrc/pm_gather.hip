@@ -178,6 +178,10 @@ PMD void lane_scan(const GatherParams &P, v3 p, float r2, v3 ns, v3 fv, uint32_t
     }
 }
 
+/* r' of a record's cell box [p - r', p + r']: hardware sqrt (<= 1 ulp), the
+ * 1e-4 relative margin covers it */
+PMD float box_reach(float r2) { return __builtin_amdgcn_sqrtf(r2) * 1.0001f + 1e-4f; }
+
 /* record prologue shared by the bucket kernels: flags, PPM state, BSDF, cell
  * box of [p - r', p + r'] (small: at most 2 x 2 rows, the grid's design case) */
 struct GatherRec {
@@ -196,20 +200,24 @@ struct GatherRec {
         if (r >= P.rec_end) return;
         const float4 pos = P.R.pos[r];
         const float4 st0 = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : P.R.state[r];
+        if (accept<PARTIAL>(P, r, pos, st0)) nrm = P.R.nrm[r];
+    }
+    /* the flags, PPM state and cell box of record r < rec_end from its loaded
+     * position and state; false: inactive (its partial written) */
+    template <int PARTIAL>
+    PMD bool accept(const GatherParams &P, int64_t r, float4 pos, float4 st0) {
         const uint32_t flags = (uint32_t)__float_as_int(pos.w);
         if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) {
             if (PARTIAL) write_partial(P, partial_index(P, r), 0, Fx3{0, 0, 0});
-            return;
+            return false;
         }
         live = true;
         st = st0;
-        nrm = P.R.nrm[r];
         r2 = st.w;
         p = xyz(pos);
         if (r2 > 0.f) {
             const GridDesc &g = P.grid;
-            /* hardware sqrt (<= 1 ulp): the 1e-4 relative margin covers it */
-            const float rq = __builtin_amdgcn_sqrtf(r2) * 1.0001f + 1e-4f;
+            const float rq = box_reach(r2);
             /* cells overlapping [p - r', p + r']: cell edge >= 2 r_max, so at
              * most 2 per axis -> at most 4 (y, z) rows of <= 2 cells in x */
             x0 = cell_axis(p.x - rq, g.gx, g.inv_cs, g.dx); x1 = cell_axis(p.x + rq, g.gx, g.inv_cs, g.dx);
@@ -218,6 +226,7 @@ struct GatherRec {
             small = y1 <= y0 + 1 && z1 <= z0 + 1;
             big = !small;
         }
+        return true;
     }
     /* phase 2: shading normal and BSDF (Kd / pi for matte, processPhoton) */
     PMD void shade(const GatherParams &P) {
@@ -361,6 +370,17 @@ PMD uint32_t wave_min_2x16(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane(m, 63);
 }
 PMD uint32_t uniform_u32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+/* wave-uniform float minimum / maximum (every lane active) */
+PMD float wave_min_f(float v) {
+    const int m = wave_scan_dpp(__float_as_int(v), __float_as_int(INFINITY),
+                                [](int a, int b) { return __float_as_int(fminf(__int_as_float(a), __int_as_float(b))); });
+    return __int_as_float(__builtin_amdgcn_readlane(m, 63));
+}
+PMD float wave_max_f(float v) {
+    const int m = wave_scan_dpp(__float_as_int(v), __float_as_int(-INFINITY),
+                                [](int a, int b) { return __float_as_int(fmaxf(__int_as_float(a), __int_as_float(b))); });
+    return __int_as_float(__builtin_amdgcn_readlane(m, 63));
+}
 
 /* one-wave blocks are dealt round-robin over the 8 XCDs: blocks b, b + 8, ...
  * (one XCD, dispatched close together) take PM_TILE_XCDG neighbouring entries
@@ -521,20 +541,58 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
     TileLds &T = tiles[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     int64_t r;
+    uint32_t tile = 0u;
     if (P.tiles) { /* only tiles with an active record (no block-level barrier below: a wave may leave) */
         int64_t w = (int64_t)blockIdx.x * (TILE_BLOCK / 64) + (threadIdx.x >> 6);
         const int64_t nt = P.n_tiles_dev ? (int64_t)*P.n_tiles_dev : P.n_tiles;
         if (w >= nt) return;
         if (TILE_BLOCK == 64) w = xcd_tile(w, nt);
-        r = P.rec_begin + (int64_t)P.tiles[w] * 64 + lane;
+        tile = uniform_u32(P.tiles[w]);
+        r = P.rec_begin + (int64_t)tile * 64 + lane;
     } else {
         r = P.rec_begin + (int64_t)blockIdx.x * TILE_BLOCK + threadIdx.x;
     }
     const GridDesc &g = P.grid;
     GProf gp;
     gp.begin();
+    /* the record's position, state and normal requested first (clamped
+     * index: no branch, so no wait before the loads below are issued) */
+    const int64_t rc = r < P.rec_end ? r : P.rec_end - 1;
+    const float4 pos0 = P.R.pos[rc], nrm0 = P.R.nrm[rc];
+    /* fresh: every lane reads record 0's state (one line) and drops it —
+     * an unconditional load, so that the wait for it is not merged with the
+     * row loads below (as a branch-guarded load's would be) */
+    float4 stm = P.R.state[P.fresh ? 0 : rc];
+    /* fresh gathers (P.tbox): the union box of every active record's cells
+     * from the tile's position box — cell_axis is monotone, so cell_axis(lo
+     * - r') is the least x0 of the records, and so on — and its row bounds
+     * requested with the records: the first group's row loads no longer wait
+     * for the record loads and the wave reductions behind them. The box is
+     * that of the lanes with a box (live, r2 > 0), a superset of the small
+     * lanes' union; a box beyond the row map leaves the ordinary groups. */
+    bool hinted = false, hrow = false;
+    uint32_t hX0 = 0u, hX1 = 0u, hY0 = 0u, hY1 = 0u, hZ0 = 0u, hZ1 = 0u, hLY = 0u, ha0 = 0u, ha1 = 0u;
+    if (P.tbox) {
+        const float4 lo = P.tbox[2 * (size_t)tile], hi = P.tbox[2 * (size_t)tile + 1];
+        const float rq = box_reach(P.r2init);
+        hX0 = cell_axis(lo.x - rq, g.gx, g.inv_cs, g.dx); hX1 = cell_axis(hi.x + rq, g.gx, g.inv_cs, g.dx);
+        hY0 = cell_axis(lo.y - rq, g.gy, g.inv_cs, g.dy); hY1 = cell_axis(hi.y + rq, g.gy, g.inv_cs, g.dy);
+        hZ0 = cell_axis(lo.z - rq, g.gz, g.inv_cs, g.dz); hZ1 = cell_axis(hi.z + rq, g.gz, g.inv_cs, g.dz);
+        hLY = hY1 > hY0 ? 32u - (uint32_t)__builtin_clz(hY1 - hY0) : 0u;
+        hinted = lo.w != 0.f && P.r2init > 0.f && hLY <= 6u && ((uint64_t)(hZ1 - hZ0 + 1u) << hLY) <= 64u;
+        const uint32_t cy = hY0 + ((uint32_t)lane & ((1u << (hLY & 31u)) - 1u)), cz = hZ0 + ((uint32_t)lane >> (hLY & 31u));
+        hrow = hinted && cy <= hY1 && cz <= hZ1;
+        const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+        ha0 = hrow ? row + hX0 : 0u;
+        ha1 = hrow ? row + hX1 + 1u : 0u;
+    }
+    /* every launch loads (cell_start[0] without a box): the same loads in
+     * flight on both paths, so the record's waits leave these outstanding */
+    const uint32_t hB = P.cell_start[ha0], hE = P.cell_start[ha1];
+    asm volatile("" : "+v"(stm.x), "+v"(stm.y), "+v"(stm.z), "+v"(stm.w));
+    const float4 st0 = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : stm;
     GatherRec R;
-    R.load<PARTIAL>(P, r);
+    if (r < P.rec_end && R.accept<PARTIAL>(P, r, pos0, st0)) R.nrm = nrm0;
     /* a box of <= KR cells per axis takes part in the LDS groups; larger
      * (radius above the grid's design radius) scans its own cells */
     const bool small = R.live && R.r2 > 0.f && R.y1 - R.y0 < (uint32_t)KR && R.z1 - R.z0 < (uint32_t)KR;
@@ -567,37 +625,43 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
         if (pm == 0ull) break;
         /* the box of all pending lanes when it fits the row map (the common,
          * coherent tile: one group), else the leader's neighbourhood */
-        uint32_t X0, X1, Y0, Y1, Z0, Z1;
+        uint32_t X0, X1, Y0, Y1, Z0, Z1, LY;
         bool mine = pend;
-        union_box(g, R, mine, X0, X1, Y0, Y1, Z0, Z1);
-        /* row pitch: NY rounded up to a power of two, 2^LY */
-        uint32_t LY = Y1 > Y0 ? 32u - (uint32_t)__builtin_clz(Y1 - Y0) : 0u;
-        if (LY > 6u || ((uint64_t)(Z1 - Z0 + 1u) << LY) > 64u) {
-            const int leader = __builtin_ctzll(pm);
-            const uint32_t lx = __builtin_amdgcn_readlane(R.x0, leader), ly = __builtin_amdgcn_readlane(R.y0, leader),
-                           lz = __builtin_amdgcn_readlane(R.z0, leader);
-            mine = pend && R.x0 + GR - lx <= 2u * GR && R.y0 + GR - ly <= 2u * GR && R.z0 + GR - lz <= 2u * GR;
-            /* an incoherent tile (lanes on many far-apart surfaces, e.g. a
-             * triangle soup) would need a group per few lanes: below
-             * GROUP_MIN lanes the rest scan their own cells per lane */
-            if (__builtin_popcountll(__ballot(mine)) < group_min) {
-                direct = direct || pend;
-                break;
-            }
-            union_box(g, R, mine, X0, X1, Y0, Y1, Z0, Z1);
-            LY = 3u;
-        }
-        pend = pend && !mine;
-        TILE_STAT(0, 1);
         /* 1. union row u = lane: photons [B, B + len); u = (cz - Z0) * 2^LY +
          * (cy - Y0) (no lane divides; padding rows are empty) */
         uint32_t B = 0u, len = 0u;
-        const uint32_t cy = Y0 + ((uint32_t)lane & ((1u << LY) - 1u)), cz = Z0 + ((uint32_t)lane >> LY);
-        if (cy <= Y1 && cz <= Z1) {
-            const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
-            B = P.cell_start[row + X0];
-            len = P.cell_start[row + X1 + 1u] - B;
+        if (hinted) { /* every pending lane, the tile box's rows already requested */
+            X0 = hX0; X1 = hX1; Y0 = hY0; Y1 = hY1; Z0 = hZ0; Z1 = hZ1; LY = hLY;
+            B = hrow ? hB : 0u; len = hrow ? hE - hB : 0u;
+            hinted = false;
+        } else {
+            union_box(g, R, mine, X0, X1, Y0, Y1, Z0, Z1);
+            /* row pitch: NY rounded up to a power of two, 2^LY */
+            LY = Y1 > Y0 ? 32u - (uint32_t)__builtin_clz(Y1 - Y0) : 0u;
+            if (LY > 6u || ((uint64_t)(Z1 - Z0 + 1u) << LY) > 64u) {
+                const int leader = __builtin_ctzll(pm);
+                const uint32_t lx = __builtin_amdgcn_readlane(R.x0, leader), ly = __builtin_amdgcn_readlane(R.y0, leader),
+                               lz = __builtin_amdgcn_readlane(R.z0, leader);
+                mine = pend && R.x0 + GR - lx <= 2u * GR && R.y0 + GR - ly <= 2u * GR && R.z0 + GR - lz <= 2u * GR;
+                /* an incoherent tile (lanes on many far-apart surfaces, e.g. a
+                 * triangle soup) would need a group per few lanes: below
+                 * GROUP_MIN lanes the rest scan their own cells per lane */
+                if (__builtin_popcountll(__ballot(mine)) < group_min) {
+                    direct = direct || pend;
+                    break;
+                }
+                union_box(g, R, mine, X0, X1, Y0, Y1, Z0, Z1);
+                LY = 3u;
+            }
+            const uint32_t cy = Y0 + ((uint32_t)lane & ((1u << LY) - 1u)), cz = Z0 + ((uint32_t)lane >> LY);
+            if (cy <= Y1 && cz <= Z1) {
+                const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+                B = P.cell_start[row + X0];
+                len = P.cell_start[row + X1 + 1u] - B;
+            }
         }
+        pend = pend && !mine;
+        TILE_STAT(0, 1);
         const uint32_t incl = wave_incl_sum_u32(len), pre = incl - len;
         const uint32_t U = uniform_u32(__builtin_amdgcn_readlane(incl, 63));
         if (U == 0u) continue;
@@ -1689,18 +1753,6 @@ __global__ __launch_bounds__(256) void k_knn_pack(const uint32_t *cell_start, ui
     pk_q[3 * k + 2] = make_float4(c0, c1, 0.f, 0.f);
 }
 
-
-/* wave-uniform float minimum / maximum (every lane active) */
-PMD float wave_min_f(float v) {
-    const int m = wave_scan_dpp(__float_as_int(v), __float_as_int(INFINITY),
-                                [](int a, int b) { return __float_as_int(fminf(__int_as_float(a), __int_as_float(b))); });
-    return __int_as_float(__builtin_amdgcn_readlane(m, 63));
-}
-PMD float wave_max_f(float v) {
-    const int m = wave_scan_dpp(__float_as_int(v), __float_as_int(-INFINITY),
-                                [](int a, int b) { return __float_as_int(fmaxf(__int_as_float(a), __int_as_float(b))); });
-    return __int_as_float(__builtin_amdgcn_readlane(m, 63));
-}
 /* gap (cell units) between [lo, hi] and cell c of an axis of dim cells —
  * the border cells extend to infinity (cell_axis clamps) — less a 1e-3
  * margin for the rounding of the cell-unit coordinates */
@@ -2400,12 +2452,29 @@ __global__ __launch_bounds__(256) void k_final(FinalParams P) {
     P.out[3 * o + 2] = out.z;
 }
 
-__global__ __launch_bounds__(256) void k_tile_flags(RecordsDev R, uint8_t *flags) {
+/* tile flags (any active record) and the tile's position box
+ * (GatherParams::tbox): (lo.xyz, 1) (hi.xyz, 0) over its active records, or
+ * lo.w = 0 when it has none or one with a non-finite coordinate */
+__global__ __launch_bounds__(256) void k_tile_flags(RecordsDev R, uint8_t *flags, float4 *tbox) {
     const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
     bool act = false;
-    if (r < R.count) act = !((uint32_t)__float_as_int(R.pos[r].w) & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID));
+    float4 pos = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < R.count) {
+        pos = R.pos[r];
+        act = !((uint32_t)__float_as_int(pos.w) & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID));
+    }
     const unsigned long long m = __ballot(act);
-    if ((threadIdx.x & 63) == 0 && r < R.count) flags[r >> 6] = m != 0ull ? 1 : 0;
+    const bool fin = isfinite(pos.x) && isfinite(pos.y) && isfinite(pos.z);
+    const bool ok = m != 0ull && __ballot(act && !fin) == 0ull;
+    const float lx = wave_min_f(act ? pos.x : INFINITY), ly = wave_min_f(act ? pos.y : INFINITY),
+                lz = wave_min_f(act ? pos.z : INFINITY);
+    const float hx = wave_max_f(act ? pos.x : -INFINITY), hy = wave_max_f(act ? pos.y : -INFINITY),
+                hz = wave_max_f(act ? pos.z : -INFINITY);
+    if ((threadIdx.x & 63) == 0 && r < R.count) {
+        flags[r >> 6] = m != 0ull ? 1 : 0;
+        tbox[2 * (r >> 6)] = make_float4(lx, ly, lz, ok ? 1.f : 0.f);
+        tbox[2 * (r >> 6) + 1] = make_float4(hx, hy, hz, 0.f);
+    }
 }
 /* one block compacts the flags in order: 1024 tiles per step, ballot ranks
  * inside each wave, wave totals through LDS */
@@ -2435,9 +2504,10 @@ __global__ __launch_bounds__(1024) void k_tile_compact(const uint8_t *flags, int
     }
     if (threadIdx.x == 0) *count = base;
 }
-hipError_t launch_tile_list(const RecordsDev &R, uint8_t *flags, uint32_t *list, uint32_t *count, hipStream_t s) {
+hipError_t launch_tile_list(const RecordsDev &R, uint8_t *flags, uint32_t *list, uint32_t *count, float4 *tbox,
+                            hipStream_t s) {
     if (R.count <= 0) return hipSuccess;
-    pm_launch(k_tile_flags, dim3((unsigned)((R.count + 255) / 256)), dim3(256), 0, s, R, flags);
+    pm_launch(k_tile_flags, dim3((unsigned)((R.count + 255) / 256)), dim3(256), 0, s, R, flags, tbox);
     pm_launch(k_tile_compact, dim3(1), dim3(1024), 0, s, (const uint8_t *)flags, (R.count + 63) / 64, list, count);
     return hipGetLastError();
 }

@@ -307,6 +307,51 @@ def test_tile_gather_nan_photons(oracle_mod, hip_mod, monkeypatch):
     assert_bitexact(outs["tile"][0], outs["lane"][0], "tile vs per-lane gather with NaN photons")
 
 
+@pytest.mark.parametrize("scene", ["cornell", "caustic", "soup"])
+def test_tile_box_fresh_gather(scene, oracle_mod, hip_mod, monkeypatch):
+    """Fresh gathers (after pm_reset_records) take a tile's first union box
+    from its records' position box (launch_tile_list) and load its rows
+    before the records: records equal those of the gather without the box
+    (PM_TILE_BOX=0) and the per-lane kernel bit for bit, with a few records
+    at non-finite or far-away positions (their tiles' boxes invalid or too
+    large: ordinary groups), over two reset + gather rounds, and the fresh
+    pass matches the oracle's single pass."""
+    sc = {"cornell": lambda: scenes.cornell_box(96, 72), "caustic": lambda: scenes.caustic_scene(96, 72),
+          "soup": lambda: scenes.triangle_soup(20000, 64, 48)}[scene]()
+    orc = sc.load_into(oracle_mod.Oracle())
+    p, recs, slots = _gather_inputs(orc, radius2=16.0, paths=32768)
+    odd = recs.copy()
+    act = np.nonzero((odd["flags"] & 7) == 0)[0]
+    odd["pos"][act[7]] = (np.nan, 1.0, 2.0)
+    odd["pos"][act[300]] = (np.inf, 0.0, 0.0)
+    odd["pos"][act[1000]] = odd["pos"][act[1000]] + np.float32(5000.0)
+    outs = {}
+    for name, kern, box in (("box", "tile", "1"), ("nobox", "tile", "0"), ("lane", "lane", "1")):
+        monkeypatch.setenv("PM_GATHER_KERNEL", kern)
+        monkeypatch.setenv("PM_TILE_BOX", box)
+        ctx = sc.load_into(hip_mod.Context(0))
+        try:
+            ctx.upload_slots(slots)
+            ctx.build_photon_map(p, len(slots))
+            got = []
+            for rr in (recs, odd):
+                ctx.upload_records(rr)
+                for _ in range(2):
+                    ctx.reset_records(p)
+                    ctx.gather(p)
+                got.append(ctx.download_records())
+            outs[name] = got
+        finally:
+            ctx.close()
+    for i in range(2):
+        assert_bitexact(outs["box"][i], outs["nobox"][i], f"tile box vs none ({scene}, set {i})")
+        assert_bitexact(outs["box"][i], outs["lane"][i], f"tile box vs per-lane ({scene}, set {i})")
+    ref = recs.copy()
+    orc.gather(orc.build_kdtree(slots), ref, p)
+    assert (ref["photon_count"] > 0).sum() > 500
+    compare_gathered_records(outs["box"][0], ref)
+
+
 def test_adaptive_grid_radius_progressive(oracle_mod, hip_mod, monkeypatch):
     """Progressive passes size the photon grid from the records' current
     radii (a histogram binned by the fused gather, PM_GRID_QUANTILE; records
