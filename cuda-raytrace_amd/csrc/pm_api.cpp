@@ -1479,7 +1479,7 @@ static int ensure_tiles(Ctx *c, hipStream_t s) {
         const int64_t nt = (c->nrec + 63) / 64;
         HIPCHK(c, c->d_tile_flags.ensure(std::max<int64_t>(nt, 16)));
         HIPCHK(c, c->d_tiles.ensure(std::max<int64_t>(nt * 4, 16)));
-        HIPCHK(c, c->d_tbox.ensure(std::max<int64_t>(nt * 32, 32)));
+        HIPCHK(c, c->d_tbox.ensure(std::max<int64_t>(nt * 64, 64)));
         HIPCHK(c, c->d_tile_count.ensure(16));
         if (!c->h_tile_count) HIPCHK(c, hipHostMalloc((void **)&c->h_tile_count, 4, hipHostMallocDefault));
         if (!c->tile_event) HIPCHK(c, hipEventCreateWithFlags(&c->tile_event, hipEventDisableTiming));
@@ -1534,7 +1534,8 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
         if (c->tile_count_known) { G.n_tiles = c->n_tiles; G.n_tiles_dev = nullptr; }
         else { G.n_tiles = (c->nrec + 63) / 64; G.n_tiles_dev = c->d_tile_count.as<uint32_t>(); }
         /* fresh PPM gather: every radius is r2init, the first group's box comes from the tile's position box */
-        if (G.fresh && !partial && !split && p->estimator == PM_ESTIMATOR_PPM && c->tile_box) G.tbox = c->d_tbox.as<float4>();
+        G.tbox = c->d_tbox.as<float4>();
+        G.tbox_use = G.fresh && !partial && !split && p->estimator == PM_ESTIMATOR_PPM && c->tile_box;
     }
     if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters.p, 0, 32, s));
     /* a fused full PPM tile gather bins the updated radii (grid_radius2) */

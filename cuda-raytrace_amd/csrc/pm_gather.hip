@@ -541,14 +541,23 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
     TileLds &T = tiles[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     int64_t r;
-    uint32_t tile = 0u;
+    int64_t w = 0;
+    float4 blo = make_float4(0.f, 0.f, 0.f, 0.f), bhi = blo;
     if (P.tiles) { /* only tiles with an active record (no block-level barrier below: a wave may leave) */
-        int64_t w = (int64_t)blockIdx.x * (TILE_BLOCK / 64) + (threadIdx.x >> 6);
+        w = (int64_t)blockIdx.x * (TILE_BLOCK / 64) + (threadIdx.x >> 6);
         const int64_t nt = P.n_tiles_dev ? (int64_t)*P.n_tiles_dev : P.n_tiles;
         if (w >= nt) return;
         if (TILE_BLOCK == 64) w = xcd_tile(w, nt);
-        tile = uniform_u32(P.tiles[w]);
-        r = P.rec_begin + (int64_t)tile * 64 + lane;
+        w = uniform_u32((uint32_t)w); /* < 2^26 tiles: the entry through the scalar cache */
+        uint32_t t;
+        if (P.tbox) { /* the entry's box and tile in one 32-B scalar load */
+            blo = P.tbox[2 * w];
+            bhi = P.tbox[2 * w + 1];
+            t = __float_as_uint(bhi.w);
+        } else {
+            t = P.tiles[w];
+        }
+        r = P.rec_begin + (int64_t)t * 64 + lane;
     } else {
         r = P.rec_begin + (int64_t)blockIdx.x * TILE_BLOCK + threadIdx.x;
     }
@@ -563,8 +572,9 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
      * an unconditional load, so that the wait for it is not merged with the
      * row loads below (as a branch-guarded load's would be) */
     float4 stm = P.R.state[P.fresh ? 0 : rc];
-    /* fresh gathers (P.tbox): the union box of every active record's cells
-     * from the tile's position box — cell_axis is monotone, so cell_axis(lo
+    /* fresh gathers (P.tbox_use): the union box of every active record's cells
+     * from the tile's position box (stored in list order, so it is requested
+     * with the list entry) — cell_axis is monotone, so cell_axis(lo
      * - r') is the least x0 of the records, and so on — and its row bounds
      * requested with the records: the first group's row loads no longer wait
      * for the record loads and the wave reductions behind them. The box is
@@ -572,8 +582,8 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
      * lanes' union; a box beyond the row map leaves the ordinary groups. */
     bool hinted = false, hrow = false;
     uint32_t hX0 = 0u, hX1 = 0u, hY0 = 0u, hY1 = 0u, hZ0 = 0u, hZ1 = 0u, hLY = 0u, ha0 = 0u, ha1 = 0u;
-    if (P.tbox) {
-        const float4 lo = P.tbox[2 * (size_t)tile], hi = P.tbox[2 * (size_t)tile + 1];
+    if (P.tbox_use) {
+        const float4 lo = blo, hi = bhi;
         const float rq = box_reach(P.r2init);
         hX0 = cell_axis(lo.x - rq, g.gx, g.inv_cs, g.dx); hX1 = cell_axis(hi.x + rq, g.gx, g.inv_cs, g.dx);
         hY0 = cell_axis(lo.y - rq, g.gy, g.inv_cs, g.dy); hY1 = cell_axis(hi.y + rq, g.gy, g.inv_cs, g.dy);
@@ -2453,7 +2463,7 @@ __global__ __launch_bounds__(256) void k_final(FinalParams P) {
 }
 
 /* tile flags (any active record) and the tile's position box
- * (GatherParams::tbox): (lo.xyz, 1) (hi.xyz, 0) over its active records, or
+ * (GatherParams::tbox): (lo.xyz, 1) (hi.xyz, tile) over its active records, or
  * lo.w = 0 when it has none or one with a non-finite coordinate */
 __global__ __launch_bounds__(256) void k_tile_flags(RecordsDev R, uint8_t *flags, float4 *tbox) {
     const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -2479,7 +2489,7 @@ __global__ __launch_bounds__(256) void k_tile_flags(RecordsDev R, uint8_t *flags
 /* one block compacts the flags in order: 1024 tiles per step, ballot ranks
  * inside each wave, wave totals through LDS */
 __global__ __launch_bounds__(1024) void k_tile_compact(const uint8_t *flags, int64_t nt, uint32_t *list,
-                                                       uint32_t *count) {
+                                                       uint32_t *count, const float4 *box_tile, float4 *box_list) {
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t base;
     if (threadIdx.x == 0) base = 0u;
@@ -2493,7 +2503,14 @@ __global__ __launch_bounds__(1024) void k_tile_compact(const uint8_t *flags, int
         __syncthreads();
         uint32_t off = base;
         for (uint32_t k = 0; k < w; ++k) off += wsum[k];
-        if (f) list[off + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull))] = (uint32_t)t;
+        if (f) {
+            const uint32_t o = off + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+            list[o] = (uint32_t)t;
+            box_list[2 * o] = box_tile[2 * t];
+            float4 hi = box_tile[2 * t + 1];
+            hi.w = __uint_as_float((uint32_t)t); /* the tile, beside its box */
+            box_list[2 * o + 1] = hi;
+        }
         __syncthreads();
         if (threadIdx.x == 0) {
             uint32_t tot = 0u;
@@ -2507,8 +2524,10 @@ __global__ __launch_bounds__(1024) void k_tile_compact(const uint8_t *flags, int
 hipError_t launch_tile_list(const RecordsDev &R, uint8_t *flags, uint32_t *list, uint32_t *count, float4 *tbox,
                             hipStream_t s) {
     if (R.count <= 0) return hipSuccess;
-    pm_launch(k_tile_flags, dim3((unsigned)((R.count + 255) / 256)), dim3(256), 0, s, R, flags, tbox);
-    pm_launch(k_tile_compact, dim3(1), dim3(1024), 0, s, (const uint8_t *)flags, (R.count + 63) / 64, list, count);
+    const int64_t nt = (R.count + 63) / 64;
+    pm_launch(k_tile_flags, dim3((unsigned)((R.count + 255) / 256)), dim3(256), 0, s, R, flags, tbox + 2 * nt);
+    pm_launch(k_tile_compact, dim3(1), dim3(1024), 0, s, (const uint8_t *)flags, nt, list, count,
+              (const float4 *)(tbox + 2 * nt), tbox);
     return hipGetLastError();
 }
 
