@@ -92,6 +92,7 @@ struct Ctx {
     DevBuf d_count, d_cell_start, d_scratch, d_pha, d_phb;
     DevBuf d_knnpk, d_knnovf; /* kNN scalar stream: photon pairs, handed-back tiles (+ count) */
     bool knn_ss = true;       /* kNN: k_gather_knn_ss first (PM_KNN_SS=0: k_gather_knn_tile alone) */
+    bool fuse_ok = true;      /* trace may fuse the bucket counting (off for the sub-contexts of a multi-device group) */
     bool tile_box = true;     /* fresh PPM tile gathers: first group from the tile's position box (PM_TILE_BOX=0: off) */
     struct { bool valid = false; int64_t n = 0; GridDesc grid{}; float r2 = 0.f; int64_t key_np = 0; int mpc = 1; } fused; /* counts made by the last trace (keys plane-major when key_np > 0) */
     GridDesc grid{};
@@ -276,11 +277,13 @@ double pair_ms(const Timer &t) {
     if (hipEventElapsedTime(&ms, t.a, t.b) != hipSuccess) return -1.0;
     return ms;
 }
-/* duration of the most recent launch of a stage */
-double timer_ms(Ctx *c, const char *name) {
+/* duration of the most recent launch of a stage (k > 1: the sum of the last k) */
+double timer_ms(Ctx *c, const char *name, size_t k = 1) {
     auto it = c->timers.find(name);
     if (it == c->timers.end() || it->second.used == 0) return -1.0;
-    return pair_ms(it->second.ev[it->second.used - 1]);
+    double ms = 0;
+    for (size_t i = it->second.used - std::min(k, it->second.used); i < it->second.used; ++i) ms += pair_ms(it->second.ev[i]);
+    return ms;
 }
 
 inline float4 f4(float x, float y, float z, float w) { return make_float4(x, y, z, w); }
@@ -684,6 +687,9 @@ int pm_create(void **out, const pm_config *cfg) {
                 FAIL((Ctx *)nullptr, PM_ERR_HIP, "device %d: %s", cfg->devices[i], e.c_str());
             }
             for (int d : G.devs) distinct = distinct && d != one.device;
+            /* a device's trace covers one shard of the all-gathered slots, so
+             * counts fused into it would never match the build: not made */
+            if (cfg->n_devices > 1) ((Ctx *)sub)->fuse_ok = false;
             G.subs.push_back((Ctx *)sub);
             G.devs.push_back(one.device);
             hipEvent_t ev = nullptr;
@@ -1386,7 +1392,7 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
      * of the bucket build (keys, ranks, per-cell counts) at deposit time; the
      * build then skips it (c->fused). Any other slot producer invalidates it. */
     c->fused.valid = false;
-    const bool fuse = p->gather_structure == PM_GATHER_GRID && path_begin == slot_path_base;
+    const bool fuse = c->fuse_ok && p->gather_structure == PM_GATHER_GRID && path_begin == slot_path_base;
     if (fuse) {
         c->fused.r2 = grid_radius2(c, p, true);
         const GridDesc g = make_grid(c, p, c->fused.r2);
@@ -1782,7 +1788,6 @@ static int group_render(Ctx *gc, const pm_render_params *p, float *out_rgb, pm_s
             if (cnt < chunk) /* padding slots of a short shard: invalid */
                 HIPCHK(gc, hipMemsetAsync(slots[d] + (b + cnt) * mpc, 0, (size_t)((chunk - cnt) * mpc) * sizeof(pm_photon),
                                           c->stream));
-            if (d == 0) t_trace += timer_ms(c, "trace");
         }
         /* all-gather of the shards: every buffer gets every device's chunk */
         if (!G.comms.empty()) {
@@ -1819,7 +1824,6 @@ static int group_render(Ctx *gc, const pm_render_params *p, float *out_rgb, pm_s
                 if (rc == PM_ERR_NO_PHOTONS) FAIL(gc, PM_ERR_NO_PHOTONS, "0 valid photons (photonmappingrenderer.cpp:165-167)");
                 return sub_fail(c, rc);
             }
-            if (d == 0) t_build += timer_ms(c, "build");
         }
         if (p->gather_structure == PM_GATHER_GRID) {
             uint32_t nv = 0;
@@ -1834,13 +1838,22 @@ static int group_render(Ctx *gc, const pm_render_params *p, float *out_rgb, pm_s
         for (int d = 0; d < n; ++d) {
             Ctx *c = G.subs[d];
             (void)hipSetDevice(c->device);
-            for (const auto &bc : bands[d]) {
+            for (const auto &bc : bands[d])
                 if ((rc = pm_gather_range(c, p, bc.first, bc.second, nullptr))) return sub_fail(c, rc);
-                if (d == 0) t_gather += timer_ms(c, "gather");
-            }
         }
         /* the next pass overwrites the slot buffers the peers read */
         for (int d = 0; d < n; ++d) { (void)hipSetDevice(G.subs[d]->device); HIPCHK(gc, hipStreamSynchronize(G.subs[d]->stream)); }
+        /* stage times of the slowest device, read once the pass is done (a
+         * read inside the loops would wait for one device before the next
+         * one's launch) */
+        double tt = 0, tb = 0, tg = 0;
+        for (int d = 0; d < n; ++d) {
+            Ctx *c = G.subs[d];
+            if (std::min(chunk, P - d * chunk) > 0) tt = std::max(tt, timer_ms(c, "trace"));
+            tb = std::max(tb, timer_ms(c, "build"));
+            if (!bands[d].empty()) tg = std::max(tg, timer_ms(c, "gather", bands[d].size()));
+        }
+        t_trace += tt; t_build += tb; t_gather += tg;
     }
     /* final radiance of each device's bands, straight into the host image */
     const double emitted = (double)P * p->passes;
@@ -2144,7 +2157,11 @@ int pm_scene_info(void *ptr, int64_t out[7]) {
     GETCTX(ptr);
     if (!c->S.blob) FAIL(c, PM_ERR_INVALID, "no scene committed");
     const SceneDev &S = c->S;
-    out[0] = S.n_tris; out[1] = S.n_disks; out[2] = S.n_spheres; out[3] = S.n_nodes; out[4] = c->bvh_depth;
+    out[0] = S.n_tris; out[1] = S.n_disks; out[2] = S.n_spheres;
+    /* the tree the kernels traverse: the 4-wide BVH when the scene has one
+     * (either builder), else the binary SAH tree */
+    out[3] = S.wide ? c->bvh4_nodes : S.n_nodes;
+    out[4] = S.wide ? c->bvh4_depth : c->bvh_depth;
     out[5] = scene_mode(S) == MODE_BRUTE ? 2 : scene_mode(S) == MODE_LDS ? 1 : 0;
     out[6] = S.blob_bytes;
     return PM_OK;

@@ -299,7 +299,11 @@ int pm_gather_counters(void *ctx, int64_t out[4]);
 int pm_trace_counters(void *ctx, int64_t out[4]);
 /* the loaded scene as the traversal kernels see it: [0] triangles, [1] disks,
  * [2] spheres, [3] BVH nodes, [4] BVH depth, [5] traversal mode (0 BVH in
- * HBM, 1 BVH in LDS, 2 brute force over an LDS-sized scene), [6] scene bytes */
+ * HBM, 1 BVH in LDS, 2 brute force over an LDS-sized scene), [6] scene bytes.
+ * [3] / [4] describe the tree the kernels traverse: with mode 0 that is the
+ * 4-wide quantized BVH (its node count and its depth in 4-wide levels),
+ * whichever builder made it (device PLOC for >= 65,536 primitives, else the
+ * host SAH build collapsed); with mode 1 the binary SAH tree */
 int pm_scene_info(void *ctx, int64_t out[7]);
 /* diagnostics: one section of the committed scene as the kernels read it
  * (refs; per storage slot the triangle records geo 48 B, shade 32 B, id,

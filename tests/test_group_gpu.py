@@ -87,3 +87,26 @@ def test_plugin_on_device_list(tmp_path, hip_mod):
         assert r.returncode == 0, r.stderr
         imgs.append(out.read_bytes())
     assert imgs[0] == imgs[1]
+
+
+def _n_gpus():
+    try:
+        import torch
+        return torch.cuda.device_count()
+    except Exception:
+        return 0
+
+
+@pytest.mark.skipif(_n_gpus() < 2, reason="needs two GPUs (the one-GPU boxes run the same-device branches above)")
+@pytest.mark.parametrize("rccl", ["1", "0"])
+def test_group_distinct_devices(rccl, hip_mod, monkeypatch):
+    """The branches only a node with distinct devices takes: ncclCommInitAll
+    over devices [0, 1] with the in-place all-gather, and (PM_GROUP_RCCL=0)
+    hipMemcpyPeerAsync between them — the image equals one context's."""
+    monkeypatch.setenv("PM_GROUP_RCCL", rccl)
+    sc = scenes.cornell_box(80, 56)
+    p = RenderParams.defaults(paths_per_pass=10001, passes=2, initial_radius2=25.0)
+    want, st_want = _render(sc, hip_mod, None, p)
+    got, st = _render(sc, hip_mod, [0, 1], p)
+    assert st["photons_valid"] == st_want["photons_valid"] > 0
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
