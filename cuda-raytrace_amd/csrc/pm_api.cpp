@@ -1544,11 +1544,14 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
         G.tbox_use = G.fresh && !partial && !split && p->estimator == PM_ESTIMATOR_PPM && c->tile_box;
     }
     if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters.p, 0, 32, s));
-    /* a fused full PPM tile gather bins the updated radii (grid_radius2) */
+    /* a fused PPM tile gather bins the updated radii (grid_radius2) — over
+     * all records, or over a band of them (a device's bands in a group render
+     * or an all-gather rank: interleaved rows, a sample of the image's radii;
+     * the grid only sets the cost, never the sums) */
     /* (not while the previous histogram's copy is in flight: the pinned
      * buffer is reused, and a stale histogram only overestimates radii) */
     const bool hist = p->estimator == PM_ESTIMATOR_PPM && p->gather_structure == PM_GATHER_GRID && !partial &&
-                      !split && rec_begin == 0 && rec_count == c->nrec && c->gather_kernel == PM_GK_TILE &&
+                      !split && c->gather_kernel == PM_GK_TILE &&
                       !c->counting && c->grid_quantile > 0.0 && c->r2_wanted &&
                       !(c->r2_pending && hipEventQuery(c->r2_event) != hipSuccess);
     if (hist) {
