@@ -442,11 +442,16 @@ struct GProf {
 #endif
 };
 
-#ifdef PM_TILE_WAVES
-#define TILE_OCC __attribute__((amdgpu_waves_per_eu(PM_TILE_WAVES, PM_TILE_WAVES)))
-#else
-#define TILE_OCC
+/* the default instance (span 2, non-negative sums) at 5 waves/SIMD, the
+ * LDS limit (TileLds): unbounded, the compiler takes 106 VGPRs since the
+ * cooperative direct scan (4 waves); bounded, 94 and no scratch. The other
+ * instances keep the compiler's choice (96; bounded they spill) */
+#ifndef PM_TILE_WAVES
+#define PM_TILE_WAVES 5
 #endif
+template <int NN, int KR>
+constexpr int tile_waves() { return NN && KR == 2 ? PM_TILE_WAVES : 1; }
+#define TILE_OCC __attribute__((amdgpu_waves_per_eu(tile_waves<NN, KR>(), 8)))
 /* the cell box [X0, X1] x [Y0, Y1] x [Z0, Z1] of the lanes with `in` set */
 PMD void union_box6(const GridDesc &g, bool in, uint32_t x0, uint32_t x1, uint32_t y0, uint32_t y1, uint32_t z0,
                     uint32_t z1, uint32_t &X0, uint32_t &X1, uint32_t &Y0, uint32_t &Y1, uint32_t &Z0, uint32_t &Z1) {
@@ -531,8 +536,82 @@ hipError_t launch_r2hist_reduce(uint32_t *hist, uint32_t *out_mapped, hipStream_
  * cell-edge sweep of DESIGN.md §5). A lane reads KR z-layers, each one
  * contiguous run of <= KR rows of the union; its group radius keeps the union
  * inside the 64-lane row map (2 GR + KR <= 8 rows per axis). */
+/* The direct lanes of a tile, when at most COOP_MAX: for each in turn, the
+ * wave loads the bounds of its rows (lane = row), concatenates them with a
+ * prefix sum and tests 64 positions per step, lane t the t-th photon (its
+ * row from the T.mark max-scan, as k_gather_tile stages); each lane adds its
+ * hits with add_hit — lane_scan's terms — and the int64 sums are reduced
+ * over the wave (exact, order-free), so M and L equal lane_scan's bit for
+ * bit. Every lane must be active. */
+#ifndef PM_COOP_MAX
+#define PM_COOP_MAX 8
+#endif
+constexpr int COOP_MAX = PM_COOP_MAX;
+PMD long long wave_sum_i64(long long v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+struct TileLds;
+PMD void coop_scan(const GatherParams &P, TileLds &T, int lane, const GatherRec &R, bool &direct, int &M, Fx3 &Lf);
 template <int KR>
 constexpr uint32_t tile_group_r() { return KR == 2 ? GROUP_R : (8u - (uint32_t)KR) / 2u; }
+PMD void coop_scan(const GatherParams &P, TileLds &T, int lane, const GatherRec &R, bool &direct, int &M, Fx3 &Lf) {
+    const GridDesc &g = P.grid;
+    const float sc = P.fx_scale;
+    const float *phb = reinterpret_cast<const float *>(P.ph_b);
+    unsigned long long dm = __ballot(direct);
+    while (dm) {
+        const int d = __builtin_ctzll(dm);
+        dm &= dm - 1ull;
+        auto rl = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), d)); };
+        auto ru = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, d); };
+        const v3 p = mk(rl(R.p.x), rl(R.p.y), rl(R.p.z)), ns = mk(rl(R.ns.x), rl(R.ns.y), rl(R.ns.z)),
+                 fv = mk(rl(R.fv.x), rl(R.fv.y), rl(R.fv.z));
+        const float r2 = rl(R.r2);
+        const uint32_t x0 = ru(R.x0), x1 = ru(R.x1), y0 = ru(R.y0), y1 = ru(R.y1), z0 = ru(R.z0), z1 = ru(R.z1);
+        const uint32_t ny = y1 - y0 + 1u, nrows = ny * (z1 - z0 + 1u);
+        int m = 0;
+        Fx3 L{0, 0, 0};
+        for (uint32_t r0 = 0; r0 < nrows; r0 += 64u) {
+            const uint32_t j = r0 + (uint32_t)lane;
+            uint32_t B = 0u, len = 0u;
+            if (j < nrows) {
+                const uint32_t cz = z0 + j / ny, cy = y0 + j % ny;
+                const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+                B = P.cell_start[row + x0];
+                len = P.cell_start[row + x1 + 1u] - B;
+            }
+            const uint32_t incl = wave_incl_sum_u32(len), pre = incl - len;
+            const uint32_t U = uniform_u32(__builtin_amdgcn_readlane(incl, 63));
+            const uint32_t gofs = B - pre;
+            for (uint32_t t0 = 0; t0 < U; t0 += 64u) {
+                T.mark[lane] = -1;
+                wave_lds_sync();
+                if (len > 0u) {
+                    if (pre >= t0 && pre < t0 + 64u) T.mark[pre - t0] = lane;
+                    else if (pre < t0 && pre + len > t0) T.mark[0] = lane; /* row running into the step */
+                }
+                wave_lds_sync();
+                const int u = wave_incl_max_i32(T.mark[lane]);
+                wave_lds_sync(); /* read before the next step's writes */
+                const uint32_t t = t0 + (uint32_t)lane;
+                const uint32_t gi = t + (uint32_t)__shfl((int)gofs, u);
+                if (t < U) {
+                    const float4 a = P.ph_a[gi];
+                    if (in_radius(p, a, r2)) {
+                        m++;
+                        add_hit(L, ns, fv, a, P.ph_b[2 * (size_t)gi], phb[8 * (size_t)gi + 4], sc);
+                    }
+                }
+            }
+        }
+        const int mt = (int)wave_sum_i64(m);
+        const long long lx = wave_sum_i64(L.x), ly = wave_sum_i64(L.y), lz = wave_sum_i64(L.z);
+        if (lane == d) { M = mt; Lf = Fx3{lx, ly, lz}; direct = false; }
+    }
+}
+
 template <int PARTIAL, int NN, int KR>
 __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParams P) {
     static_assert(KR >= 2 && KR <= 5 && 2 * tile_group_r<KR>() + KR <= 8, "lane box / group radius");
@@ -903,6 +982,10 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
         }
     }
     gp.mark(4);
+    /* a few direct lanes (an incoherent tile's stragglers): the whole wave
+     * scans each one's cells in turn, 64 photons per load; many (a dense
+     * union's group): each lane its own, side by side */
+    if (__builtin_popcountll(__ballot(direct)) <= COOP_MAX) coop_scan(P, T, lane, R, direct, M, Lf);
     if (direct) lane_scan<0>(P, R.p, R.r2, R.ns, R.fv, R.x0, R.x1, R.y0, R.y1, R.z0, R.z1, M, Lf, nv, nr);
     gp.mark(5);
     R.store<PARTIAL>(P, r, M, Lf);
