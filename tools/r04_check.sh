@@ -10,6 +10,7 @@ case $rc in 0|1) ;; *) exit $rc ;; esac   # a crash or time limit: nothing more 
 for c in c2 c3 c5; do
   timeout -k 10 300 python bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_$c.json 2> $O/bench_$c.err || exit $?
 done
+PM_OVERLAP=0 timeout -k 10 300 python bench.py --config c2 --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_c2_noovl.json 2> $O/bench_c2_noovl.err || exit $?
 PM_TILE_BOX=0 timeout -k 10 300 python bench.py --config c2 --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_c2_nobox.json 2> $O/bench_c2_nobox.err || exit $?
 V=$R/cuda-raytrace_amd/lib/variants/libpmhip_nocoop.so
 if [ -f $V ]; then
