@@ -297,10 +297,6 @@ def main():
         # N > 1: each pass's exchange also timed here, run to completion at
         # once (in the timed steps it overlaps the next pass's trace + build)
         runner.time_exchange = world > 1
-        # and one stream: each stage's kernels alone on the GPU (in the timed
-        # steps the next pass's trace runs beside the gather)
-        overlapped = runner.overlap
-        runner.overlap = False
         for _ in range(min(args.steps, 10)):
             step()
         runner.flush()
@@ -387,7 +383,6 @@ def main():
                       "photons_tested": vis, "photons_found" if knn else "photons_in_radius": hits},
             "avg_launch_ms": round(gather_ms, 5),
             "launches_timed": gather_launches,
-            "timed_with_overlap": overlapped,
             # the per-lane kernel's operand bytes (16 B per photon each lane
             # tests): what the L1 / LDS deliver, not HBM traffic
             "l1_delivered": {"bytes_per_launch": int(l1_bytes), "formula": l1_formula,
@@ -401,16 +396,6 @@ def main():
                         "VALU issue + per-wave latency (profiles/r02 counters): the kernel reads each record "
                         "once and each tile's photons once, so HBM is not what bounds it"),
         }
-        if overlapped and "gather" in stages:
-            # the timed region runs pass k+1's trace beside pass k's gather
-            # (PassRunner overlap): the launch above shares the GPU; the same
-            # kernel alone (the stage-split passes after the timed region):
-            iso = stages["gather"]
-            roofline["isolated"] = {"avg_launch_ms": iso, "achieved": round(compulsory / (iso * 1e-3) / 1e9, 1),
-                                    "frac": round(compulsory / (iso * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                    "note": "the gather launch with no other kernel on the GPU (one-stream passes "
-                                            "after the timed region); avg_launch_ms above is timed in the steps, "
-                                            "where the next pass's trace runs beside it"}
         if traffic is not None:
             raw = load_pmc_traffic(kernel_name, args.config + ("_knn" if knn else ""), "hbm_bytes_uncorrected")[0]
             roofline["traffic_uncorrected"] = raw
@@ -493,7 +478,6 @@ def main():
             "radius2": radius2,
             "exchange": args.exchange if world > 1 else "none",
             "parallelism": f"photon-shard x{world}" if world > 1 else "single",
-            "streams": "trace of pass k+1 beside gather of pass k" if overlapped else "one",
         },
         "mgather_samples_per_s": round(g_points * args.steps / elapsed / 1e6, 3),
         "kernel_rates": {

@@ -39,7 +39,6 @@ CPU oracle engine in tests/) works on torch tensors so that the collective
 logic is identical for RCCL (GPU) and gloo (CPU tests).
 """
 import ctypes
-import os
 
 import torch
 import torch.distributed as dist
@@ -182,8 +181,7 @@ class HipEngine:
 
 
 class PassRunner:
-    def __init__(self, engine, params, rank=0, world=1, exchange="reduce", force_exchange=False, total_paths=None,
-                 overlap=None):
+    def __init__(self, engine, params, rank=0, world=1, exchange="reduce", force_exchange=False, total_paths=None):
         """force_exchange: run the N > 1 code path (record view, collectives,
         owned chunks / bands) even at world size 1 — how a 1-GPU box executes
         the RCCL branch of the exchange (tests/test_dist_gpu.py).
@@ -191,14 +189,7 @@ class PassRunner:
         all ranks (rank r traces global paths [r*per, min(total, (r+1)*per)),
         per = ceil(total / world); the last rank's short chunk leaves its
         tail slots invalid); None: weak scaling, params.paths_per_pass per
-        rank.
-        overlap: trace each pass on a second stream that waits only for the
-        previous pass's bucket build (the last reader of the slots and of the
-        fused counts), so pass k+1's trace runs beside pass k's gather — the
-        trace reads no record and the gather no slot (it reads the bucket
-        copies ph_a / ph_b the build wrote). Default: on for the bucket grid
-        on a HIP engine (PM_OVERLAP=0 turns it off); the kd-tree build copies
-        the slots to the host synchronously, so it keeps one stream."""
+        rank."""
         if exchange not in ("reduce", "allgather"):
             raise ValueError(exchange)
         self.multi = world > 1 or force_exchange
@@ -220,12 +211,6 @@ class PassRunner:
         # to completion at once and record its GPU time (ms) per pass
         self.time_exchange = False
         self.exchange_ms = []
-        if overlap is None:
-            overlap = os.environ.get("PM_OVERLAP", "1") != "0"
-        self.overlap = (bool(overlap) and isinstance(engine, HipEngine) and torch.cuda.is_available()
-                        and int(getattr(params, "gather_structure", 0)) == 0)
-        self._tstream = torch.cuda.Stream() if self.overlap else None
-        self._ev_build = None          # after the last bucket build (main stream)
         n = engine.num_records()
         self.n_records = n
         self.rec_begin, self.rec_count, self.rec_per = _chunk(n, world, rank)   # final image split
@@ -296,44 +281,21 @@ class PassRunner:
         """Finish the exchange still in flight (call before reading records or timing)."""
         self._finish_exchange()
 
-    def _trace(self, pass_index, path_begin, path_count, slot_path_base):
-        """The pass's trace; with overlap on the trace stream, after the
-        previous build only, and the main stream waits for it."""
-        if not self.overlap:
-            self.e.trace_photons(self.p, pass_index, path_begin, path_count, slot_path_base)
-            return
-        main, ts = torch.cuda.current_stream(), self._tstream
-        if self._ev_build is None:
-            ts.wait_stream(main)           # first pass: after everything before it
-        else:
-            ts.wait_event(self._ev_build)
-        with torch.cuda.stream(ts):
-            self.e.trace_photons(self.p, pass_index, path_begin, path_count, slot_path_base)
-        done = torch.cuda.Event()
-        done.record(ts)
-        main.wait_event(done)
-
-    def _build(self, n_slots):
-        self.e.build_photon_map(self.p, n_slots)
-        if self.overlap:
-            self._ev_build = torch.cuda.Event()
-            self._ev_build.record(torch.cuda.current_stream())
-
     def step(self, pass_index, reset=False):
         """One PPM pass: trace this rank's paths, build, gather (+ exchange)."""
         e, p = self.e, self.p
         if not self.multi:
             if reset:
                 e.reset_records(p)
-            self._trace(pass_index, 0, self.paths, 0)
-            self._build(self.slots_mine)
+            e.trace_photons(p, pass_index, 0, self.paths, 0)
+            e.build_photon_map(p, self.slots_mine)
             e.gather(p)
             return
         if self.exchange == "reduce":
             # trace + build do not read records: they overlap the previous exchange
             if self.paths:
-                self._trace(pass_index, self.path_begin, self.paths, self.path_begin)
-            self._build(self.slots_mine)
+                e.trace_photons(p, pass_index, self.path_begin, self.paths, self.path_begin)
+            e.build_photon_map(p, self.slots_mine)
             self._finish_exchange()
             if reset:
                 e.reset_records(p)
@@ -345,11 +307,11 @@ class PassRunner:
             if reset:
                 e.reset_records(p)
             if self.paths:
-                self._trace(pass_index, self.path_begin, self.paths, 0)
+                e.trace_photons(p, pass_index, self.path_begin, self.paths, 0)
             mine = self.slot_buf[self.rank * self.slots_per_rank * PHOTON_DTYPE.itemsize:
                                  (self.rank + 1) * self.slots_per_rank * PHOTON_DTYPE.itemsize]
             self._timed(lambda: self._all_gather(self.slot_buf, mine))
-            self._build(self.world * self.slots_per_rank)
+            e.build_photon_map(p, self.world * self.slots_per_rank)
             for b, c in self.bands[self.rank]:                  # replicated map, owned bands
                 e.gather_range(p, b, c)
 

@@ -102,35 +102,3 @@ def test_rccl_world1_exchange_matches_single_context(exchange, tmp_path, hip_mod
     got = np.load(tmp_path / "img0.npy")
     assert (want > 0).any()
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"RCCL world-1 {exchange} image differs"
-
-
-@pytest.mark.parametrize("progressive", [True, False])
-def test_overlapped_trace_matches_one_stream(progressive, hip_mod):
-    """PassRunner at N = 1 traces pass k+1 on a second stream beside pass k's
-    gather (it waits only for pass k's bucket build): the records after five
-    passes — progressive, or each from the initial state like the bench's C2
-    step — equal those of the one-stream runner bit for bit, on the C2 scene
-    with several passes in flight."""
-    from pmrender import scenes
-    from pmrender.abi import RenderParams
-    from pmrender.dist import HipEngine, PassRunner
-    from parity_util import assert_bitexact
-    outs = {}
-    for overlap in (False, True):
-        ctx = scenes.cornell_box(256, 192).load_into(hip_mod.Context(0))
-        p = RenderParams.defaults(paths_per_pass=65536, initial_radius2=16.0)
-        try:
-            with torch.cuda.stream(torch.cuda.Stream()):
-                eng = HipEngine(ctx)
-                ctx.eye_pass(p, eng._s())
-                runner = PassRunner(eng, p, overlap=overlap)
-                assert runner.overlap == overlap
-                for k in range(5):
-                    runner.step(k if progressive else 0, reset=(k == 0) or not progressive)
-                runner.flush()
-                torch.cuda.synchronize()
-            outs[overlap] = ctx.download_records()
-        finally:
-            ctx.close()
-    assert (outs[False]["photon_count"] > 0).sum() > 1000
-    assert_bitexact(outs[True], outs[False], f"overlapped trace (progressive={progressive})")
