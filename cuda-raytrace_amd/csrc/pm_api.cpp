@@ -93,7 +93,6 @@ struct Ctx {
     DevBuf d_knnpk, d_knnovf; /* kNN scalar stream: photon pairs, handed-back tiles (+ count) */
     bool knn_ss = true;       /* kNN: k_gather_knn_ss first (PM_KNN_SS=0: k_gather_knn_tile alone) */
     bool fuse_ok = true;      /* trace may fuse the bucket counting (off for the sub-contexts of a multi-device group) */
-    bool tile_box = true;     /* fresh PPM tile gathers: first group from the tile's position box (PM_TILE_BOX=0: off) */
     struct { bool valid = false; int64_t n = 0; GridDesc grid{}; float r2 = 0.f; int64_t key_np = 0; int mpc = 1; } fused; /* counts made by the last trace (keys plane-major when key_np > 0) */
     GridDesc grid{};
     float grid_r2 = 0.f; /* radius^2 the photon map's grid is designed for */
@@ -113,7 +112,7 @@ struct Ctx {
     DevBuf d_vflags, d_vrank, d_vlist, d_vsums;
     /* tiles (64 records) holding an active record, in record order: full-range
      * tile gathers launch over these only (records fixed after the eye pass) */
-    DevBuf d_tiles, d_tile_flags, d_tile_count, d_tbox;
+    DevBuf d_tiles, d_tile_flags, d_tile_count;
     int64_t n_tiles = 0;           /* valid once tile_count_known */
     bool tiles_valid = false;      /* the list on the device matches the records */
     bool tile_count_known = false; /* its length read back (pinned copy + event, never waited on) */
@@ -730,7 +729,6 @@ int pm_create(void **out, const pm_config *cfg) {
     if (const char *e = getenv("PM_GATHER_KERNEL"))
         c->gather_kernel = !strcmp(e, "lane") ? PM_GK_LANE : PM_GK_TILE;
     if (const char *e = getenv("PM_KNN_SS")) c->knn_ss = atoi(e) != 0;
-    if (const char *e = getenv("PM_TILE_BOX")) c->tile_box = atoi(e) != 0;
     if (const char *e = getenv("PM_CELL_SPAN")) c->cell_span = std::max(2, std::min(5, atoi(e)));
     if (const char *e = getenv("PM_GRID_QUANTILE")) c->grid_quantile = atof(e);
     if (const char *e = getenv("PM_TRACE_HOLD")) c->trace_hold = atoi(e) != 0;
@@ -773,7 +771,7 @@ void pm_destroy(void *ptr) {
     DevBuf *bufs[] = {&c->d_scene, &c->d_rays, &c->d_rand2d, &c->d_pos, &c->d_nrm, &c->d_state, &c->d_n,
                       &c->d_dl, &c->d_slots, &c->d_count, &c->d_scratch, &c->d_vflags, &c->d_vrank, &c->d_vlist, &c->d_vsums,
                       &c->d_cell_start, &c->d_pha, &c->d_phb, &c->d_knnpk, &c->d_knnovf,
-                      &c->d_kd, &c->d_out, &c->d_counters, &c->d_tiles, &c->d_tile_flags, &c->d_tile_count, &c->d_tbox,
+                      &c->d_kd, &c->d_out, &c->d_counters, &c->d_tiles, &c->d_tile_flags, &c->d_tile_count,
                       &c->d_r2hist, &c->d_spill};
     for (DevBuf *b : bufs) b->release();
     if (c->tile_event) (void)hipEventDestroy(c->tile_event);
@@ -1485,7 +1483,6 @@ static int ensure_tiles(Ctx *c, hipStream_t s) {
         const int64_t nt = (c->nrec + 63) / 64;
         HIPCHK(c, c->d_tile_flags.ensure(std::max<int64_t>(nt, 16)));
         HIPCHK(c, c->d_tiles.ensure(std::max<int64_t>(nt * 4, 16)));
-        HIPCHK(c, c->d_tbox.ensure(std::max<int64_t>(nt * 64, 64)));
         HIPCHK(c, c->d_tile_count.ensure(16));
         if (!c->h_tile_count) HIPCHK(c, hipHostMalloc((void **)&c->h_tile_count, 4, hipHostMallocDefault));
         if (!c->tile_event) HIPCHK(c, hipEventCreateWithFlags(&c->tile_event, hipEventDisableTiming));
@@ -1493,7 +1490,7 @@ static int ensure_tiles(Ctx *c, hipStream_t s) {
          * any gather read it): let that copy land before the pinned word is reused */
         else if (!c->tile_count_known) HIPCHK(c, hipEventSynchronize(c->tile_event));
         HIPCHK(c, launch_tile_list(recs(c), c->d_tile_flags.as<uint8_t>(), c->d_tiles.as<uint32_t>(),
-                                   c->d_tile_count.as<uint32_t>(), c->d_tbox.as<float4>(), s));
+                                   c->d_tile_count.as<uint32_t>(), s));
         HIPCHK(c, hipMemcpyAsync(c->h_tile_count, c->d_tile_count.p, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipEventRecord(c->tile_event, s));
         c->tiles_valid = true;
@@ -1540,8 +1537,6 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
         if (c->tile_count_known) { G.n_tiles = c->n_tiles; G.n_tiles_dev = nullptr; }
         else { G.n_tiles = (c->nrec + 63) / 64; G.n_tiles_dev = c->d_tile_count.as<uint32_t>(); }
         /* fresh PPM gather: every radius is r2init, the first group's box comes from the tile's position box */
-        G.tbox = c->d_tbox.as<float4>();
-        G.tbox_use = G.fresh && !partial && !split && p->estimator == PM_ESTIMATOR_PPM && c->tile_box;
     }
     if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters.p, 0, 32, s));
     /* a fused PPM tile gather bins the updated radii (grid_radius2) — over

@@ -443,9 +443,9 @@ struct GProf {
 };
 
 /* the default instance (span 2, non-negative sums) at 5 waves/SIMD, the
- * LDS limit (TileLds): unbounded, the compiler takes 106 VGPRs since the
- * cooperative direct scan (4 waves); bounded, 94 and no scratch. The other
- * instances keep the compiler's choice (96; bounded they spill) */
+ * LDS limit (TileLds): unbounded, the compiler takes more than 102 VGPRs
+ * since the cooperative direct scan (4 waves); bounded, none spill. The
+ * other instances keep the compiler's choice (bounded they spill) */
 #ifndef PM_TILE_WAVES
 #define PM_TILE_WAVES 5
 #endif
@@ -620,68 +620,20 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
     TileLds &T = tiles[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     int64_t r;
-    int64_t w = 0;
-    float4 blo = make_float4(0.f, 0.f, 0.f, 0.f), bhi = blo;
     if (P.tiles) { /* only tiles with an active record (no block-level barrier below: a wave may leave) */
-        w = (int64_t)blockIdx.x * (TILE_BLOCK / 64) + (threadIdx.x >> 6);
+        int64_t w = (int64_t)blockIdx.x * (TILE_BLOCK / 64) + (threadIdx.x >> 6);
         const int64_t nt = P.n_tiles_dev ? (int64_t)*P.n_tiles_dev : P.n_tiles;
         if (w >= nt) return;
         if (TILE_BLOCK == 64) w = xcd_tile(w, nt);
-        w = uniform_u32((uint32_t)w); /* < 2^26 tiles: the entry through the scalar cache */
-        uint32_t t;
-        if (P.tbox) { /* the entry's box and tile in one 32-B scalar load */
-            blo = P.tbox[2 * w];
-            bhi = P.tbox[2 * w + 1];
-            t = __float_as_uint(bhi.w);
-        } else {
-            t = P.tiles[w];
-        }
-        r = P.rec_begin + (int64_t)t * 64 + lane;
+        r = P.rec_begin + (int64_t)P.tiles[w] * 64 + lane;
     } else {
         r = P.rec_begin + (int64_t)blockIdx.x * TILE_BLOCK + threadIdx.x;
     }
     const GridDesc &g = P.grid;
     GProf gp;
     gp.begin();
-    /* the record's position, state and normal requested first (clamped
-     * index: no branch, so no wait before the loads below are issued) */
-    const int64_t rc = r < P.rec_end ? r : P.rec_end - 1;
-    const float4 pos0 = P.R.pos[rc], nrm0 = P.R.nrm[rc];
-    /* fresh: every lane reads record 0's state (one line) and drops it —
-     * an unconditional load, so that the wait for it is not merged with the
-     * row loads below (as a branch-guarded load's would be) */
-    float4 stm = P.R.state[P.fresh ? 0 : rc];
-    /* fresh gathers (P.tbox_use): the union box of every active record's cells
-     * from the tile's position box (stored in list order, so it is requested
-     * with the list entry) — cell_axis is monotone, so cell_axis(lo
-     * - r') is the least x0 of the records, and so on — and its row bounds
-     * requested with the records: the first group's row loads no longer wait
-     * for the record loads and the wave reductions behind them. The box is
-     * that of the lanes with a box (live, r2 > 0), a superset of the small
-     * lanes' union; a box beyond the row map leaves the ordinary groups. */
-    bool hinted = false, hrow = false;
-    uint32_t hX0 = 0u, hX1 = 0u, hY0 = 0u, hY1 = 0u, hZ0 = 0u, hZ1 = 0u, hLY = 0u, ha0 = 0u, ha1 = 0u;
-    if (P.tbox_use) {
-        const float4 lo = blo, hi = bhi;
-        const float rq = box_reach(P.r2init);
-        hX0 = cell_axis(lo.x - rq, g.gx, g.inv_cs, g.dx); hX1 = cell_axis(hi.x + rq, g.gx, g.inv_cs, g.dx);
-        hY0 = cell_axis(lo.y - rq, g.gy, g.inv_cs, g.dy); hY1 = cell_axis(hi.y + rq, g.gy, g.inv_cs, g.dy);
-        hZ0 = cell_axis(lo.z - rq, g.gz, g.inv_cs, g.dz); hZ1 = cell_axis(hi.z + rq, g.gz, g.inv_cs, g.dz);
-        hLY = hY1 > hY0 ? 32u - (uint32_t)__builtin_clz(hY1 - hY0) : 0u;
-        hinted = lo.w != 0.f && P.r2init > 0.f && hLY <= 6u && ((uint64_t)(hZ1 - hZ0 + 1u) << hLY) <= 64u;
-        const uint32_t cy = hY0 + ((uint32_t)lane & ((1u << (hLY & 31u)) - 1u)), cz = hZ0 + ((uint32_t)lane >> (hLY & 31u));
-        hrow = hinted && cy <= hY1 && cz <= hZ1;
-        const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
-        ha0 = hrow ? row + hX0 : 0u;
-        ha1 = hrow ? row + hX1 + 1u : 0u;
-    }
-    /* every launch loads (cell_start[0] without a box): the same loads in
-     * flight on both paths, so the record's waits leave these outstanding */
-    const uint32_t hB = P.cell_start[ha0], hE = P.cell_start[ha1];
-    asm volatile("" : "+v"(stm.x), "+v"(stm.y), "+v"(stm.z), "+v"(stm.w));
-    const float4 st0 = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : stm;
     GatherRec R;
-    if (r < P.rec_end && R.accept<PARTIAL>(P, r, pos0, st0)) R.nrm = nrm0;
+    R.load<PARTIAL>(P, r);
     /* a box of <= KR cells per axis takes part in the LDS groups; larger
      * (radius above the grid's design radius) scans its own cells */
     const bool small = R.live && R.r2 > 0.f && R.y1 - R.y0 < (uint32_t)KR && R.z1 - R.z0 < (uint32_t)KR;
@@ -719,35 +671,29 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
         /* 1. union row u = lane: photons [B, B + len); u = (cz - Z0) * 2^LY +
          * (cy - Y0) (no lane divides; padding rows are empty) */
         uint32_t B = 0u, len = 0u;
-        if (hinted) { /* every pending lane, the tile box's rows already requested */
-            X0 = hX0; X1 = hX1; Y0 = hY0; Y1 = hY1; Z0 = hZ0; Z1 = hZ1; LY = hLY;
-            B = hrow ? hB : 0u; len = hrow ? hE - hB : 0u;
-            hinted = false;
-        } else {
+        union_box(g, R, mine, X0, X1, Y0, Y1, Z0, Z1);
+        /* row pitch: NY rounded up to a power of two, 2^LY */
+        LY = Y1 > Y0 ? 32u - (uint32_t)__builtin_clz(Y1 - Y0) : 0u;
+        if (LY > 6u || ((uint64_t)(Z1 - Z0 + 1u) << LY) > 64u) {
+            const int leader = __builtin_ctzll(pm);
+            const uint32_t lx = __builtin_amdgcn_readlane(R.x0, leader), ly = __builtin_amdgcn_readlane(R.y0, leader),
+                           lz = __builtin_amdgcn_readlane(R.z0, leader);
+            mine = pend && R.x0 + GR - lx <= 2u * GR && R.y0 + GR - ly <= 2u * GR && R.z0 + GR - lz <= 2u * GR;
+            /* an incoherent tile (lanes on many far-apart surfaces, e.g. a
+             * triangle soup) would need a group per few lanes: below
+             * GROUP_MIN lanes the rest scan their own cells per lane */
+            if (__builtin_popcountll(__ballot(mine)) < group_min) {
+                direct = direct || pend;
+                break;
+            }
             union_box(g, R, mine, X0, X1, Y0, Y1, Z0, Z1);
-            /* row pitch: NY rounded up to a power of two, 2^LY */
-            LY = Y1 > Y0 ? 32u - (uint32_t)__builtin_clz(Y1 - Y0) : 0u;
-            if (LY > 6u || ((uint64_t)(Z1 - Z0 + 1u) << LY) > 64u) {
-                const int leader = __builtin_ctzll(pm);
-                const uint32_t lx = __builtin_amdgcn_readlane(R.x0, leader), ly = __builtin_amdgcn_readlane(R.y0, leader),
-                               lz = __builtin_amdgcn_readlane(R.z0, leader);
-                mine = pend && R.x0 + GR - lx <= 2u * GR && R.y0 + GR - ly <= 2u * GR && R.z0 + GR - lz <= 2u * GR;
-                /* an incoherent tile (lanes on many far-apart surfaces, e.g. a
-                 * triangle soup) would need a group per few lanes: below
-                 * GROUP_MIN lanes the rest scan their own cells per lane */
-                if (__builtin_popcountll(__ballot(mine)) < group_min) {
-                    direct = direct || pend;
-                    break;
-                }
-                union_box(g, R, mine, X0, X1, Y0, Y1, Z0, Z1);
-                LY = 3u;
-            }
-            const uint32_t cy = Y0 + ((uint32_t)lane & ((1u << LY) - 1u)), cz = Z0 + ((uint32_t)lane >> LY);
-            if (cy <= Y1 && cz <= Z1) {
-                const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
-                B = P.cell_start[row + X0];
-                len = P.cell_start[row + X1 + 1u] - B;
-            }
+            LY = 3u;
+        }
+        const uint32_t cy = Y0 + ((uint32_t)lane & ((1u << LY) - 1u)), cz = Z0 + ((uint32_t)lane >> LY);
+        if (cy <= Y1 && cz <= Z1) {
+            const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+            B = P.cell_start[row + X0];
+            len = P.cell_start[row + X1 + 1u] - B;
         }
         pend = pend && !mine;
         TILE_STAT(0, 1);
@@ -2545,34 +2491,17 @@ __global__ __launch_bounds__(256) void k_final(FinalParams P) {
     P.out[3 * o + 2] = out.z;
 }
 
-/* tile flags (any active record) and the tile's position box
- * (GatherParams::tbox): (lo.xyz, 1) (hi.xyz, tile) over its active records, or
- * lo.w = 0 when it has none or one with a non-finite coordinate */
-__global__ __launch_bounds__(256) void k_tile_flags(RecordsDev R, uint8_t *flags, float4 *tbox) {
+__global__ __launch_bounds__(256) void k_tile_flags(RecordsDev R, uint8_t *flags) {
     const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
     bool act = false;
-    float4 pos = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (r < R.count) {
-        pos = R.pos[r];
-        act = !((uint32_t)__float_as_int(pos.w) & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID));
-    }
+    if (r < R.count) act = !((uint32_t)__float_as_int(R.pos[r].w) & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID));
     const unsigned long long m = __ballot(act);
-    const bool fin = isfinite(pos.x) && isfinite(pos.y) && isfinite(pos.z);
-    const bool ok = m != 0ull && __ballot(act && !fin) == 0ull;
-    const float lx = wave_min_f(act ? pos.x : INFINITY), ly = wave_min_f(act ? pos.y : INFINITY),
-                lz = wave_min_f(act ? pos.z : INFINITY);
-    const float hx = wave_max_f(act ? pos.x : -INFINITY), hy = wave_max_f(act ? pos.y : -INFINITY),
-                hz = wave_max_f(act ? pos.z : -INFINITY);
-    if ((threadIdx.x & 63) == 0 && r < R.count) {
-        flags[r >> 6] = m != 0ull ? 1 : 0;
-        tbox[2 * (r >> 6)] = make_float4(lx, ly, lz, ok ? 1.f : 0.f);
-        tbox[2 * (r >> 6) + 1] = make_float4(hx, hy, hz, 0.f);
-    }
+    if ((threadIdx.x & 63) == 0 && r < R.count) flags[r >> 6] = m != 0ull ? 1 : 0;
 }
 /* one block compacts the flags in order: 1024 tiles per step, ballot ranks
  * inside each wave, wave totals through LDS */
 __global__ __launch_bounds__(1024) void k_tile_compact(const uint8_t *flags, int64_t nt, uint32_t *list,
-                                                       uint32_t *count, const float4 *box_tile, float4 *box_list) {
+                                                       uint32_t *count) {
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t base;
     if (threadIdx.x == 0) base = 0u;
@@ -2586,14 +2515,7 @@ __global__ __launch_bounds__(1024) void k_tile_compact(const uint8_t *flags, int
         __syncthreads();
         uint32_t off = base;
         for (uint32_t k = 0; k < w; ++k) off += wsum[k];
-        if (f) {
-            const uint32_t o = off + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
-            list[o] = (uint32_t)t;
-            box_list[2 * o] = box_tile[2 * t];
-            float4 hi = box_tile[2 * t + 1];
-            hi.w = __uint_as_float((uint32_t)t); /* the tile, beside its box */
-            box_list[2 * o + 1] = hi;
-        }
+        if (f) list[off + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull))] = (uint32_t)t;
         __syncthreads();
         if (threadIdx.x == 0) {
             uint32_t tot = 0u;
@@ -2604,13 +2526,10 @@ __global__ __launch_bounds__(1024) void k_tile_compact(const uint8_t *flags, int
     }
     if (threadIdx.x == 0) *count = base;
 }
-hipError_t launch_tile_list(const RecordsDev &R, uint8_t *flags, uint32_t *list, uint32_t *count, float4 *tbox,
-                            hipStream_t s) {
+hipError_t launch_tile_list(const RecordsDev &R, uint8_t *flags, uint32_t *list, uint32_t *count, hipStream_t s) {
     if (R.count <= 0) return hipSuccess;
-    const int64_t nt = (R.count + 63) / 64;
-    pm_launch(k_tile_flags, dim3((unsigned)((R.count + 255) / 256)), dim3(256), 0, s, R, flags, tbox + 2 * nt);
-    pm_launch(k_tile_compact, dim3(1), dim3(1024), 0, s, (const uint8_t *)flags, nt, list, count,
-              (const float4 *)(tbox + 2 * nt), tbox);
+    pm_launch(k_tile_flags, dim3((unsigned)((R.count + 255) / 256)), dim3(256), 0, s, R, flags);
+    pm_launch(k_tile_compact, dim3(1), dim3(1024), 0, s, (const uint8_t *)flags, (R.count + 63) / 64, list, count);
     return hipGetLastError();
 }
 

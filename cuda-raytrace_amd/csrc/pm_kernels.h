@@ -179,13 +179,6 @@ struct GatherParams {
     /* non-null: the list's length is this device word (the host has not read
      * it back yet); n_tiles then bounds the grid (every tile) */
     const uint32_t *n_tiles_dev;
-    /* with the tile list: per entry (lo.xyz, valid) (hi.xyz, tile bits), the box
-     * of its tile's active records' positions (launch_tile_list). tbox_use
-     * (fresh gathers: every radius is r2init): k_gather_tile takes the union
-     * box of its first group from it and loads that group's row bounds with
-     * the records */
-    const float4 *tbox;
-    int tbox_use;
     /* kNN scalar-stream kernel (k_gather_knn_ss): photon pairs (k_knn_pack,
      * knn_pk_pairs of them: 2 float4 + 3 float4 per pair) and the list of
      * tiles it hands back to k_gather_knn_tile (knn_ovf, length *knn_ovf_n) */
@@ -245,9 +238,7 @@ hipError_t launch_ppm_update_split(const GatherParams &p, const int *count, cons
 hipError_t launch_final(const FinalParams &p, hipStream_t s);
 /* list[0 .. *count) = the tiles (records [64 t, 64 t + 64)) holding an
  * active record, ascending, built on the device (flags: one byte per tile) */
-/* tile list + its entries' position boxes: tbox 4 float4 per tile (list order, then scratch by tile) */
-hipError_t launch_tile_list(const RecordsDev &R, uint8_t *flags, uint32_t *list, uint32_t *count, float4 *tbox,
-                            hipStream_t s);
+hipError_t launch_tile_list(const RecordsDev &R, uint8_t *flags, uint32_t *list, uint32_t *count, hipStream_t s);
 hipError_t launch_radius2_io(const RecordsDev &R, float *buf, int64_t rec_begin, int64_t rec_count, int to_records,
                              const uint32_t *view, hipStream_t s);
 /* exclusive scan of n uint32 (pm_bucket.hip); in/out 16-B aligned; sums: scan_scratch_words(n) */

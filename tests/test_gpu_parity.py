@@ -308,14 +308,13 @@ def test_tile_gather_nan_photons(oracle_mod, hip_mod, monkeypatch):
 
 
 @pytest.mark.parametrize("scene", ["cornell", "caustic", "soup"])
-def test_tile_box_fresh_gather(scene, oracle_mod, hip_mod, monkeypatch):
-    """Fresh gathers (after pm_reset_records) take a tile's first union box
-    from its records' position box (launch_tile_list) and load its rows
-    before the records: records equal those of the gather without the box
-    (PM_TILE_BOX=0) and the per-lane kernel bit for bit, with a few records
-    at non-finite or far-away positions (their tiles' boxes invalid or too
-    large: ordinary groups), over two reset + gather rounds, and the fresh
-    pass matches the oracle's single pass."""
+def test_fresh_gather_tile_vs_lane(scene, oracle_mod, hip_mod, monkeypatch):
+    """Fresh gathers (after pm_reset_records: every radius the initial one,
+    read from the gather's parameters, not memory): the tile kernel — groups,
+    and on the soup the wave-cooperative scan of a tile's few direct lanes —
+    equals the per-lane kernel bit for bit, also with a few records at
+    non-finite or far-away positions, over two reset + gather rounds; the
+    fresh pass matches the oracle's single pass."""
     sc = {"cornell": lambda: scenes.cornell_box(96, 72), "caustic": lambda: scenes.caustic_scene(96, 72),
           "soup": lambda: scenes.triangle_soup(20000, 64, 48)}[scene]()
     orc = sc.load_into(oracle_mod.Oracle())
@@ -326,9 +325,8 @@ def test_tile_box_fresh_gather(scene, oracle_mod, hip_mod, monkeypatch):
     odd["pos"][act[300]] = (np.inf, 0.0, 0.0)
     odd["pos"][act[1000]] = odd["pos"][act[1000]] + np.float32(5000.0)
     outs = {}
-    for name, kern, box in (("box", "tile", "1"), ("nobox", "tile", "0"), ("lane", "lane", "1")):
-        monkeypatch.setenv("PM_GATHER_KERNEL", kern)
-        monkeypatch.setenv("PM_TILE_BOX", box)
+    for name in ("tile", "lane"):
+        monkeypatch.setenv("PM_GATHER_KERNEL", name)
         ctx = sc.load_into(hip_mod.Context(0))
         try:
             ctx.upload_slots(slots)
@@ -344,12 +342,11 @@ def test_tile_box_fresh_gather(scene, oracle_mod, hip_mod, monkeypatch):
         finally:
             ctx.close()
     for i in range(2):
-        assert_bitexact(outs["box"][i], outs["nobox"][i], f"tile box vs none ({scene}, set {i})")
-        assert_bitexact(outs["box"][i], outs["lane"][i], f"tile box vs per-lane ({scene}, set {i})")
+        assert_bitexact(outs["tile"][i], outs["lane"][i], f"fresh tile vs per-lane gather ({scene}, set {i})")
     ref = recs.copy()
     orc.gather(orc.build_kdtree(slots), ref, p)
     assert (ref["photon_count"] > 0).sum() > 500
-    compare_gathered_records(outs["box"][0], ref)
+    compare_gathered_records(outs["tile"][0], ref)
 
 
 def test_adaptive_grid_radius_progressive(oracle_mod, hip_mod, monkeypatch):

@@ -1,6 +1,5 @@
-# full GPU suite + C2 / C3 / C5 / C2-kNN bench lines at the current sources,
-# the C2 line without the fresh-gather tile box (PM_TILE_BOX=0) and the
-# C3 / C5 lines of the no-cooperative-scan variant (lib/variants, if built)
+# full GPU suite + C2 / C3 / C5 / C2-kNN bench lines at the current sources
+# and the C3 / C5 lines of the no-cooperative-scan variant (lib/variants, if built)
 set -u
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${1:-r04_check}; mkdir -p $O; cd $R
 timeout -k 10 900 python -u -m pytest tests -x -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
@@ -10,8 +9,6 @@ case $rc in 0|1) ;; *) exit $rc ;; esac   # a crash or time limit: nothing more 
 for c in c2 c3 c5; do
   timeout -k 10 300 python bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_$c.json 2> $O/bench_$c.err || exit $?
 done
-PM_OVERLAP=0 timeout -k 10 300 python bench.py --config c2 --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_c2_noovl.json 2> $O/bench_c2_noovl.err || exit $?
-PM_TILE_BOX=0 timeout -k 10 300 python bench.py --config c2 --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_c2_nobox.json 2> $O/bench_c2_nobox.err || exit $?
 V=$R/cuda-raytrace_amd/lib/variants/libpmhip_nocoop.so
 if [ -f $V ]; then
   for c in c3 c5; do
