@@ -76,6 +76,7 @@ struct Ctx {
     bool committed = false;
     /* device scene */
     DevBuf d_scene, d_rays, d_rand2d; /* d_scene: the scene blob (SceneDev) */
+    DevBuf d_tripairs;                /* brute-force scenes: triangle pairs interleaved (SceneDev::tri_pairs_g) */
     SceneDev S{};
     float bbox_lo[3] = {0, 0, 0}, bbox_hi[3] = {0, 0, 0};
     double emit_max = 1.0, kd_max = 1.0; /* bounds for the fixed-point flux scale */
@@ -1131,6 +1132,19 @@ int pm_commit(void *ptr) {
         blob.resize(std::max<size_t>((blob.size() + 15) & ~(size_t)15, 16), 0);
         const auto t_u0 = tnow();
         if ((rc = upload(c, c->d_scene, blob))) return rc;
+        if (id_order) {
+            /* triangle pairs for the brute-force loop: pair j = storage slots
+             * 2j, 2j + 1, each of the 12 (p0, e0, e1, n) components as two
+             * adjacent floats, so a scalar load puts the packed operand of
+             * both triangles in an aligned SGPR pair */
+            const int64_t np = nst / 2;
+            std::vector<float> pairs((size_t)std::max<int64_t>(np, 1) * 24, 0.f);
+            const float *geo = reinterpret_cast<const float *>(tri_geo.data());
+            for (int64_t j = 0; j < np; ++j)
+                for (int q = 0; q < 12; ++q)
+                    for (int h = 0; h < 2; ++h) pairs[(size_t)j * 24 + 2 * q + h] = geo[(size_t)(2 * j + h) * 12 + q];
+            if ((rc = upload(c, c->d_tripairs, pairs))) return rc;
+        }
         if (ptimes) fprintf(stderr, "pm_commit: upload %.1f ms (%zu bytes), total %.1f ms\n", tms(t_u0, tnow()), blob.size(),
                             tms(t_commit0, tnow()));
         L.bytes = blob.size();
@@ -1155,6 +1169,7 @@ int pm_commit(void *ptr) {
     S.n_refs = (int)L.n_refs;
     S.n_tris = (int)L.n_tris; S.n_disks = (int)nd; S.n_spheres = (int)ns;
     S.tri_geo_g = S.tri_geo; S.tri_id_g = S.tri_id;
+    S.tri_pairs_g = L.id_order ? c->d_tripairs.as<float>() : nullptr;
     S.brute = (S.lds_bytes > 0 && L.id_order) ? 1 : 0;
     /* a push happens only when descending a level, so depth + 1 entries suffice;
      * sizing the LDS stack by the actual tree keeps occupancy VGPR-bound */

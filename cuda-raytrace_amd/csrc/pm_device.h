@@ -93,6 +93,10 @@ struct SceneDev {
      * them with wave-uniform indices through the scalar cache into SGPRs */
     const float4 *tri_geo_g;
     const uint32_t *tri_id_g;
+    /* brute-force scenes: triangles 2j, 2j + 1 interleaved component by
+     * component (24 floats per pair, pm_commit), so each packed operand of
+     * isect_tri_pair is one aligned SGPR pair of a scalar load */
+    const float *tri_pairs_g;
     /* 4-wide BVH (4 uint4 per quantized node, pm_build.h quantize_bvh4; 8
      * float4 per node in PM_BVH4_QUANT=0 builds, collapse_bvh4) for scenes
      * traversed from HBM (MODE_GLOBAL) when wide != 0; the binary nodes stay
@@ -389,23 +393,25 @@ PMD f2 bc2(float x) { return f2{x, x}; }
  * bit-identical to the scalar test. */
 /* two triangles' (p0, e0, e1, n) as packed pairs, wave-uniform */
 struct TriPair { f2 p0x, p0y, p0z, e0x, e0y, e0z, e1x, e1y, e1z, nx, ny, nz; };
-PMD TriPair load_pair(const_f32_ptr qa, const_f32_ptr qb) {
-    TriPair q;
-    q.p0x = f2{qa[0], qb[0]}; q.p0y = f2{qa[1], qb[1]}; q.p0z = f2{qa[2], qb[2]};
-    q.e0x = f2{qa[3], qb[3]}; q.e0y = f2{qa[4], qb[4]}; q.e0z = f2{qa[5], qb[5]};
-    q.e1x = f2{qa[6], qb[6]}; q.e1y = f2{qa[7], qb[7]}; q.e1z = f2{qa[8], qb[8]};
-    q.nx = f2{qa[9], qb[9]}; q.ny = f2{qa[10], qb[10]}; q.nz = f2{qa[11], qb[11]};
-    return q;
+/* the ray's origin and direction as packed splats. The components pass
+ * through an empty asm first: splatting a value loaded from the path state
+ * otherwise became a <2 x float> load of the state, which kept the ray in
+ * scratch memory (5 scratch loads per ray in k_trace_lane) */
+struct RaySplat { f2 ox, oy, oz, dx, dy, dz; };
+PMD RaySplat splat_ray(const Ray &r) {
+    float ox = r.o.x, oy = r.o.y, oz = r.o.z, dx = r.d.x, dy = r.d.y, dz = r.d.z;
+    asm("" : "+v"(ox), "+v"(oy), "+v"(oz), "+v"(dx), "+v"(dy), "+v"(dz));
+    return RaySplat{bc2(ox), bc2(oy), bc2(oz), bc2(dx), bc2(dy), bc2(dz)};
 }
-PMD void isect_tri_pair(const TriPair &q, const Ray &ray, f2 &t, f2 &beta, f2 &gamma) {
+PMD void isect_tri_pair(const TriPair &q, const RaySplat &ray, f2 &t, f2 &beta, f2 &gamma) {
     const f2 p0x = q.p0x, p0y = q.p0y, p0z = q.p0z, e0x = q.e0x, e0y = q.e0y, e0z = q.e0z;
     const f2 e1x = q.e1x, e1y = q.e1y, e1z = q.e1z, nx = q.nx, ny = q.ny, nz = q.nz;
-    const f2 dx = bc2(ray.d.x), dy = bc2(ray.d.y), dz = bc2(ray.d.z);
+    const f2 dx = ray.dx, dy = ray.dy, dz = ray.dz;
     const f2 den = (nx * dx + ny * dy) + nz * dz; /* dot(n, d) */
     f2 inv;
     inv.x = rcp_exact(den.x);
     inv.y = rcp_exact(den.y);
-    const f2 e2x = inv * (p0x - bc2(ray.o.x)), e2y = inv * (p0y - bc2(ray.o.y)), e2z = inv * (p0z - bc2(ray.o.z));
+    const f2 e2x = inv * (p0x - ray.ox), e2y = inv * (p0y - ray.oy), e2z = inv * (p0z - ray.oz);
     const f2 ix = dy * e2z - dz * e2y, iy = dz * e2x - dx * e2z, iz = dx * e2y - dy * e2x; /* cross(d, e2) */
     beta = (ix * e1x + iy * e1y) + iz * e1z;
     gamma = (ix * e0x + iy * e0y) + iz * e0z;
@@ -420,9 +426,20 @@ PMD void isect_tri_pair(const TriPair &q, const Ray &ray, f2 &t, f2 &beta, f2 &g
 PMD void take(Hit &best, float t, float b, float g, uint32_t ref) {
     best.t = t; best.beta = b; best.gamma = g; best.ref = ref;
 }
+/* a pair of SceneDev::tri_pairs_g: component c of triangle h at q[2c + h] */
+PMD TriPair load_pair_il(const_f32_ptr q) {
+    TriPair t;
+    t.p0x = f2{q[0], q[1]}; t.p0y = f2{q[2], q[3]}; t.p0z = f2{q[4], q[5]};
+    t.e0x = f2{q[6], q[7]}; t.e0y = f2{q[8], q[9]}; t.e0z = f2{q[10], q[11]};
+    t.e1x = f2{q[12], q[13]}; t.e1y = f2{q[14], q[15]}; t.e1z = f2{q[16], q[17]};
+    t.nx = f2{q[18], q[19]}; t.ny = f2{q[20], q[21]}; t.nz = f2{q[22], q[23]};
+    return t;
+}
 template <bool ANY, class C>
 PMD bool brute_isect(const SceneDev &S, const Ray &ray, Hit &best, C &cen) {
     const const_f32_ptr tg = (const_f32_ptr)S.tri_geo_g; /* constant address space: s_load */
+    const const_f32_ptr tp = (const_f32_ptr)S.tri_pairs_g;
+    const RaySplat rs = splat_ray(ray);
     int k = 0;
     /* (software-pipelining the next pair's scalar loads measured slower:
      * C2 trace 91 vs 86 us — more live SGPRs, no unroll) */
@@ -430,7 +447,7 @@ PMD bool brute_isect(const SceneDev &S, const Ray &ray, Hit &best, C &cen) {
     for (; k + 1 < S.n_tris; k += 2) {
         cen.prim(); cen.prim();
         f2 t, b, g;
-        isect_tri_pair(load_pair(tg + 12 * k, tg + 12 * (k + 1)), ray, t, b, g);
+        isect_tri_pair(load_pair_il(tp + 12 * k), rs, t, b, g); /* pair k / 2: 24 floats */
         const bool ok0 = (t.x < ray.tmax) & (t.x > ray.tmin) & (b.x >= 0.0f) & (g.x >= 0.0f) & (b.x + g.x <= 1);
         const bool ok1 = (t.y < ray.tmax) & (t.y > ray.tmin) & (b.y >= 0.0f) & (g.y >= 0.0f) & (b.y + g.y <= 1);
         if (ANY) { if (ok0 | ok1) return true; continue; }
