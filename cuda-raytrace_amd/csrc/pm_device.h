@@ -387,9 +387,6 @@ PMD float4 ldc4(const_f32_ptr q) { return make_float4(q[0], q[1], q[2], q[3]); }
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 PMD f2 bc2(float x) { return f2{x, x}; }
-#ifndef PM_BRUTE_VLOAD
-#define PM_BRUTE_VLOAD 0
-#endif
 
 /* isect_tri_v for two triangles at once (packed v_pk_mul/add_f32): the same
  * per-component IEEE operations in the same order, so each lane of the pair is
@@ -444,37 +441,13 @@ PMD bool brute_isect(const SceneDev &S, const Ray &ray, Hit &best, C &cen) {
     const RaySplat rs = splat_ray(ray);
     int k = 0;
     /* (software-pipelining the next pair's scalar loads measured slower:
-     * C2 trace 91 vs 86 us — more live SGPRs, no unroll) */
-#if PM_BRUTE_VLOAD
-    /* pairs through vector loads (the pointer hidden from the uniformity
-     * analysis), the next pair requested before this one is tested */
-    const float4 *vp = reinterpret_cast<const float4 *>(S.tri_pairs_g);
-    asm("" : "+v"(vp));
-    auto ldv = [&](int j) {
-        const float4 *q = vp + 6 * j;
-        const float4 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4], f = q[5];
-        TriPair r;
-        r.p0x = f2{a.x, a.y}; r.p0y = f2{a.z, a.w}; r.p0z = f2{b.x, b.y}; r.e0x = f2{b.z, b.w};
-        r.e0y = f2{c.x, c.y}; r.e0z = f2{c.z, c.w}; r.e1x = f2{d.x, d.y}; r.e1y = f2{d.z, d.w};
-        r.e1z = f2{e.x, e.y}; r.nx = f2{e.z, e.w}; r.ny = f2{f.x, f.y}; r.nz = f2{f.z, f.w};
-        return r;
-    };
-    const int npair = S.n_tris >> 1;
-    TriPair cur = ldv(0);
-    for (; k + 1 < S.n_tris; k += 2) {
-        TriPair nxt = cur;
-        if ((k >> 1) + 1 < npair) nxt = ldv((k >> 1) + 1);
-        cen.prim(); cen.prim();
-        f2 t, b, g;
-        isect_tri_pair(cur, rs, t, b, g);
-        cur = nxt;
-#else
+     * C2 trace 91 vs 86 us — more live SGPRs, no unroll; so did pipelined
+     * vector loads of the pairs into VGPRs: 73.5 -> 99 us, 111 VGPRs) */
 #pragma unroll 2
     for (; k + 1 < S.n_tris; k += 2) {
         cen.prim(); cen.prim();
         f2 t, b, g;
         isect_tri_pair(load_pair_il((const_f32_ptr)S.tri_pairs_g + 12 * k), rs, t, b, g); /* pair k / 2: 24 floats */
-#endif
         /* closest hit: t < best.t <= ray.tmax (traverse starts best.t at
          * tmax) implies t < tmax, so only the any-hit query tests tmax */
         const bool ok0 = (!ANY || t.x < ray.tmax) & (t.x > ray.tmin) & (b.x >= 0.0f) & (g.x >= 0.0f) & (b.x + g.x <= 1);
