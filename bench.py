@@ -297,16 +297,20 @@ def main():
         # N > 1: each pass's exchange also timed here, run to completion at
         # once (in the timed steps it overlaps the next pass's trace + build)
         runner.time_exchange = world > 1
-        for _ in range(min(args.steps, 10)):
+        split_passes = min(args.steps, 10)
+        for _ in range(split_passes):
             step()
         runner.flush()
         torch.cuda.synchronize()
         runner.time_exchange = False
+        # ms per pass (a stage may launch several times per pass: the
+        # all-gather mode gathers each of the rank's bands; a reset runs only
+        # on the passes that start from the initial state)
         stages = {}
         for name in ("reset", "trace", "build", "gather", "update"):
             n, ms = ctx.timing_total(name)
             if n:
-                stages[name] = round(ms / n, 5)
+                stages[name] = round(ms / (n if name == "reset" else split_passes), 5)
         if runner.exchange_ms:
             stages["exchange"] = round(sum(runner.exchange_ms) / len(runner.exchange_ms), 5)
 
