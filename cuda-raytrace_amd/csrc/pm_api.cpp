@@ -404,6 +404,16 @@ GatherParams gather_params(Ctx *c, const pm_render_params *p) {
     G.error = reinterpret_cast<unsigned int *>(c->d_counters.as<unsigned long long>() + 16);
     G.fx_nonneg = c->scene_nonneg && c->slots_nonneg ? 1 : 0;
     G.span = grid_span(c->grid, c->grid_r2 > 0.f ? c->grid_r2 : p->initial_radius2);
+    /* The cooperative scan of a tile's direct lanes costs the sum of their
+     * photons / 64 steps, the per-lane scans the largest lane's photons but
+     * one scattered line per lane and load. Scenes traversed from HBM (many
+     * small primitives: C3's 1M-triangle soup) give incoherent tiles whose
+     * lanes share no cells — the cooperative scan takes them all (same box:
+     * C3 gather 0.458 -> 0.216 ms); LDS-sized scenes (the Cornell family)
+     * give coherent direct lanes (a dense union's group, C5), which the
+     * per-lane scans serve from L1, so only light waves (<= 8 steps) go
+     * cooperative (C5: all 0.214 ms vs 0.170 bounded). */
+    G.coop_steps = scene_mode(c->S) == MODE_GLOBAL ? 0xffffffu : 8u;
     if (c->view_active) { G.view_rank = c->d_vrank.as<uint32_t>(); G.view_list = c->d_vlist.as<uint32_t>(); }
     /* fixed-point scale 2^S: a single contribution is bounded by
      * alpha_max * Kd_max / pi with alpha_max = emission * Kd_max^mpc (Lambert

@@ -536,80 +536,98 @@ hipError_t launch_r2hist_reduce(uint32_t *hist, uint32_t *out_mapped, hipStream_
  * cell-edge sweep of DESIGN.md §5). A lane reads KR z-layers, each one
  * contiguous run of <= KR rows of the union; its group radius keeps the union
  * inside the 64-lane row map (2 GR + KR <= 8 rows per axis). */
-/* The direct lanes of a tile, when at most COOP_MAX: for each in turn, the
- * wave loads the bounds of its rows (lane = row), concatenates them with a
- * prefix sum and tests 64 positions per step, lane t the t-th photon (its
- * row from the T.mark max-scan, as k_gather_tile stages); each lane adds its
- * hits with add_hit — lane_scan's terms — and the int64 sums are reduced
- * over the wave (exact, order-free), so M and L equal lane_scan's bit for
- * bit. Every lane must be active. */
-#ifndef PM_COOP_MAX
-#define PM_COOP_MAX 8
-#endif
-constexpr int COOP_MAX = PM_COOP_MAX;
-PMD long long wave_sum_i64(long long v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-struct TileLds;
-PMD void coop_scan(const GatherParams &P, TileLds &T, int lane, const GatherRec &R, bool &direct, int &M, Fx3 &Lf);
 template <int KR>
 constexpr uint32_t tile_group_r() { return KR == 2 ? GROUP_R : (8u - (uint32_t)KR) / 2u; }
-PMD void coop_scan(const GatherParams &P, TileLds &T, int lane, const GatherRec &R, bool &direct, int &M, Fx3 &Lf) {
+struct TileLds;
+/* The lanes of `sel` (small boxes: at most KR x KR rows each) all at once:
+ * their rows are concatenated (row slot = lane, its owner from a max-scan
+ * over the owners' first slots), the rows' photons concatenated again and
+ * tested 64 per step, each against its owner's query (shuffled from the
+ * owner); hits are added with add_hit — lane_scan's terms — into the
+ * owner's int64 sums in LDS (exact, order-free), so M and L equal
+ * lane_scan's bit for bit. A step costs the whole wave whatever the number
+ * of owners: the cost is ~ the lanes' photons / 64. Every lane active. */
+PMD void coop_batch(const GatherParams &P, TileLds &T, int lane, const GatherRec &R, bool &sel, int &M, Fx3 &Lf) {
     const GridDesc &g = P.grid;
     const float sc = P.fx_scale;
     const float *phb = reinterpret_cast<const float *>(P.ph_b);
-    unsigned long long dm = __ballot(direct);
-    while (dm) {
-        const int d = __builtin_ctzll(dm);
-        dm &= dm - 1ull;
-        auto rl = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), d)); };
-        auto ru = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, d); };
-        const v3 p = mk(rl(R.p.x), rl(R.p.y), rl(R.p.z)), ns = mk(rl(R.ns.x), rl(R.ns.y), rl(R.ns.z)),
-                 fv = mk(rl(R.fv.x), rl(R.fv.y), rl(R.fv.z));
-        const float r2 = rl(R.r2);
-        const uint32_t x0 = ru(R.x0), x1 = ru(R.x1), y0 = ru(R.y0), y1 = ru(R.y1), z0 = ru(R.z0), z1 = ru(R.z1);
-        const uint32_t ny = y1 - y0 + 1u, nrows = ny * (z1 - z0 + 1u);
-        int m = 0;
-        Fx3 L{0, 0, 0};
-        for (uint32_t r0 = 0; r0 < nrows; r0 += 64u) {
-            const uint32_t j = r0 + (uint32_t)lane;
-            uint32_t B = 0u, len = 0u;
-            if (j < nrows) {
-                const uint32_t cz = z0 + j / ny, cy = y0 + j % ny;
-                const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
-                B = P.cell_start[row + x0];
-                len = P.cell_start[row + x1 + 1u] - B;
+    /* per-owner sums (M, L.x, L.y, L.z) in the idle staging array: 64 x 32 B */
+    unsigned long long *acc = reinterpret_cast<unsigned long long *>(T.b);
+    static_assert(sizeof(T.b) >= 64 * 32, "owner sums fit the flux staging array");
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[4 * lane + q] = 0ull;
+    const uint32_t ny = sel ? R.y1 - R.y0 + 1u : 0u, nr = sel ? ny * (R.z1 - R.z0 + 1u) : 0u;
+    const uint32_t rin = wave_incl_sum_u32(nr), rpre = rin - nr;
+    const uint32_t RT = uniform_u32(__builtin_amdgcn_readlane(rin, 63));
+    for (uint32_t c0 = 0; c0 < RT; c0 += 64u) {
+        /* row slot c0 + lane: its owner, the lane whose slots [rpre, rin) hold it */
+        T.mark[lane] = -1;
+        wave_lds_sync();
+        if (nr > 0u) {
+            if (rpre >= c0 && rpre < c0 + 64u) T.mark[rpre - c0] = lane;
+            else if (rpre < c0 && rin > c0) T.mark[0] = lane;
+        }
+        wave_lds_sync();
+        const int o = wave_incl_max_i32(T.mark[lane]);
+        wave_lds_sync();
+        const int os = max(o, 0);
+        const uint32_t j = c0 + (uint32_t)lane;
+        const uint32_t ox0 = (uint32_t)__shfl((int)R.x0, os), ox1 = (uint32_t)__shfl((int)R.x1, os);
+        const uint32_t oy0 = (uint32_t)__shfl((int)R.y0, os), oz0 = (uint32_t)__shfl((int)R.z0, os);
+        const uint32_t ony = (uint32_t)__shfl((int)ny, os), orp = (uint32_t)__shfl((int)rpre, os);
+        uint32_t B = 0u, len = 0u;
+        if (j < RT && o >= 0) {
+            const uint32_t k = j - orp;
+            const uint32_t cy = oy0 + k % ony, cz = oz0 + k / ony;
+            const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+            B = P.cell_start[row + ox0];
+            len = P.cell_start[row + ox1 + 1u] - B;
+        }
+        const uint32_t incl = wave_incl_sum_u32(len), pre = incl - len;
+        const uint32_t U = uniform_u32(__builtin_amdgcn_readlane(incl, 63));
+        const uint32_t gofs = B - pre;
+        for (uint32_t t0 = 0; t0 < U; t0 += 64u) {
+            T.mark[lane] = -1;
+            wave_lds_sync();
+            if (len > 0u) {
+                if (pre >= t0 && pre < t0 + 64u) T.mark[pre - t0] = lane;
+                else if (pre < t0 && pre + len > t0) T.mark[0] = lane;
             }
-            const uint32_t incl = wave_incl_sum_u32(len), pre = incl - len;
-            const uint32_t U = uniform_u32(__builtin_amdgcn_readlane(incl, 63));
-            const uint32_t gofs = B - pre;
-            for (uint32_t t0 = 0; t0 < U; t0 += 64u) {
-                T.mark[lane] = -1;
-                wave_lds_sync();
-                if (len > 0u) {
-                    if (pre >= t0 && pre < t0 + 64u) T.mark[pre - t0] = lane;
-                    else if (pre < t0 && pre + len > t0) T.mark[0] = lane; /* row running into the step */
-                }
-                wave_lds_sync();
-                const int u = wave_incl_max_i32(T.mark[lane]);
-                wave_lds_sync(); /* read before the next step's writes */
-                const uint32_t t = t0 + (uint32_t)lane;
-                const uint32_t gi = t + (uint32_t)__shfl((int)gofs, u);
-                if (t < U) {
-                    const float4 a = P.ph_a[gi];
-                    if (in_radius(p, a, r2)) {
-                        m++;
-                        add_hit(L, ns, fv, a, P.ph_b[2 * (size_t)gi], phb[8 * (size_t)gi + 4], sc);
-                    }
+            wave_lds_sync();
+            const int u = max(wave_incl_max_i32(T.mark[lane]), 0);
+            wave_lds_sync();
+            const uint32_t t = t0 + (uint32_t)lane;
+            const uint32_t gi = t + (uint32_t)__shfl((int)gofs, u);
+            const int ow = __shfl(os, u);
+            const v3 p = mk(__shfl(R.p.x, ow), __shfl(R.p.y, ow), __shfl(R.p.z, ow));
+            const float r2 = __shfl(R.r2, ow);
+            float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+            bool h = false;
+            if (t < U) {
+                a = P.ph_a[gi];
+                h = in_radius(p, a, r2);
+            }
+            if (__ballot(h)) {
+                const v3 ns = mk(__shfl(R.ns.x, ow), __shfl(R.ns.y, ow), __shfl(R.ns.z, ow));
+                const v3 fv = mk(__shfl(R.fv.x, ow), __shfl(R.fv.y, ow), __shfl(R.fv.z, ow));
+                if (h) {
+                    Fx3 c{0, 0, 0};
+                    add_hit(c, ns, fv, a, P.ph_b[2 * (size_t)gi], phb[8 * (size_t)gi + 4], sc);
+                    atomicAdd(&acc[4 * ow], 1ull);
+                    atomicAdd(&acc[4 * ow + 1], (unsigned long long)c.x);
+                    atomicAdd(&acc[4 * ow + 2], (unsigned long long)c.y);
+                    atomicAdd(&acc[4 * ow + 3], (unsigned long long)c.z);
                 }
             }
         }
-        const int mt = (int)wave_sum_i64(m);
-        const long long lx = wave_sum_i64(L.x), ly = wave_sum_i64(L.y), lz = wave_sum_i64(L.z);
-        if (lane == d) { M = mt; Lf = Fx3{lx, ly, lz}; direct = false; }
     }
+    wave_lds_sync();
+    if (sel) {
+        M = (int)acc[4 * lane];
+        Lf = Fx3{(long long)acc[4 * lane + 1], (long long)acc[4 * lane + 2], (long long)acc[4 * lane + 3]};
+        sel = false;
+    }
+    wave_lds_sync(); /* the sums are read before anything else writes the array */
 }
 
 template <int PARTIAL, int NN, int KR>
@@ -928,10 +946,43 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
         }
     }
     gp.mark(4);
-    /* a few direct lanes (an incoherent tile's stragglers): the whole wave
-     * scans each one's cells in turn, 64 photons per load; many (a dense
-     * union's group): each lane its own, side by side */
-    if (__builtin_popcountll(__ballot(direct)) <= COOP_MAX) coop_scan(P, T, lane, R, direct, M, Lf);
+    /* Direct lanes with a small box whose cells hold few photons in all (an
+     * incoherent tile's lanes no group took, C3: ~12 per wave, ~20 photons
+     * each): the whole wave scans each one's cells in turn, 64 photons per
+     * load. Many photons (a dense union's group, C5; a tile of unrelated
+     * surfaces at a depth edge): each lane its own, side by side — the
+     * cooperative scan's time grows with the sum over the lanes, the
+     * per-lane scans' with the largest lane. */
+    if (__ballot(direct)) {
+        const bool cand = direct && small;
+        uint32_t own = 0u;
+        if (cand) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t cy = R.y0 + (uint32_t)(k & 1), cz = R.z0 + (uint32_t)(k >> 1);
+                if (cy <= R.y1 && cz <= R.z1) {
+                    const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
+                    own += P.cell_start[row + R.x1 + 1u] - P.cell_start[row + R.x0];
+                }
+            }
+        }
+        const uint32_t tot = uniform_u32(__builtin_amdgcn_readlane(wave_incl_sum_u32(own), 63));
+#ifdef PM_COOP_STATS
+        const uint32_t nc = (uint32_t)__builtin_popcountll(__ballot(cand)), nd = (uint32_t)__builtin_popcountll(__ballot(direct));
+        if (lane == 0 && P.counters) {
+            atomicAdd(&P.counters[8], 1ull); atomicAdd(&P.counters[9], (unsigned long long)nc);
+            atomicAdd(&P.counters[10], (unsigned long long)tot); atomicMax(&P.counters[11], (unsigned long long)tot);
+            atomicAdd(&P.counters[12], (unsigned long long)nd);
+            if (nc > 16) { atomicAdd(&P.counters[13], 1ull); atomicAdd(&P.counters[14], (unsigned long long)tot); }
+            atomicMax(&P.counters[15], (unsigned long long)nc);
+        }
+#endif
+        if (tot <= (uint32_t)P.coop_steps * 64u) {
+            bool sel = cand;
+            coop_batch(P, T, lane, R, sel, M, Lf);
+            direct = direct && !cand;
+        }
+    }
     if (direct) lane_scan<0>(P, R.p, R.r2, R.ns, R.fv, R.x0, R.x1, R.y0, R.y1, R.z0, R.z1, M, Lf, nv, nr);
     gp.mark(5);
     R.store<PARTIAL>(P, r, M, Lf);

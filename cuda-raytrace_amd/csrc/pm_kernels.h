@@ -159,6 +159,10 @@ struct GatherParams {
      * always run k_gather_grid */
     int kernel;
     int span; /* tile kernel: cells per axis of a lane box at the grid's design radius (2..5) */
+    /* tile kernel: a wave's direct lanes with small boxes are scanned by the
+     * whole wave together (coop_batch) when their cells hold at most
+     * 64 * coop_steps photons, else each lane scans its own */
+    uint32_t coop_steps;
     /* non-null: k_gather_tile bins every updated radius, R2_COPIES x R2_BINS
      * counters, bin = floor(-log2(r^2 * r2hist_inv) * R2_PER_OCTAVE) clamped */
     uint32_t *r2hist;

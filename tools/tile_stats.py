@@ -32,5 +32,8 @@ if KNN and os.environ.get("PM_KNN_SS", "1") != "0":  # k_gather_knn_ss (the defa
     names = ["tile_waves", "passes", "hist_passes", "rows", "hist_pairs", "collect_pairs", "sum_pairs", "sum_pairs_hit"]
 elif KNN:  # k_gather_knn_tile: per-wave sums
     names = ["groups", "passes", "windows", "staged", "hit_iters", "direct_lanes", "min_lane_passes", "rebin_lane_passes"]
+if os.environ.get("PM_COOP_STATS_NAMES"):
+    names = ["waves_direct", "sum_cand", "sum_tot", "max_tot", "sum_direct", "waves_cand16", "tot_cand16", "max_cand"]
+    print("map", ctx.map_info())
 for k, x in zip(names, v):
     print(f"{k:14s} {x:12d}  per tile wave {x / max(v[0], 1):8.2f}")
