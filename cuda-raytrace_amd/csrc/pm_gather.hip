@@ -1814,8 +1814,8 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
 #define PM_KS_WAVES 6
 #endif
 #define KS_OCC __attribute__((amdgpu_waves_per_eu(PM_KS_WAVES, PM_KS_WAVES)))
-constexpr int KS_NB = 32;   /* bins per histogram level (+1 sink), two 16-bit counters per word */
-constexpr int KS_HW = KS_NB / 2 + 1; /* histogram words per lane (the sink is bin KS_NB: word KS_HW - 1) */
+constexpr int KS_NB = 32;   /* bins per histogram level (+1 sink), 16-bit counters: two lanes per word */
+constexpr int KS_HW = KS_NB / 2 + 1; /* LDS words per lane: (KS_NB + 1) 16-bit counters, or KS_LIST + 1 list rows + a sink row */
 constexpr int KS_LIST = 12; /* values a COLLECT keeps per lane (rows 0..KS_LIST of the histogram, +1 scratch) */
 enum { KS_HIST = 0, KS_COLLECT = 1, KS_SUM = 2, KS_DONE = 3 };
 static_assert(KS_LIST + 1 < KS_HW, "the COLLECT list aliases histogram rows (not the sink's)");
@@ -1856,7 +1856,10 @@ PMD uint32_t cell_u(float u, int dim) {
     return (uint32_t)(c < 0 ? 0 : (c >= dim ? dim - 1 : c));
 }
 __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
-    __shared__ uint32_t H[KS_HW * 64]; /* [word][lane]: bins 2w (low half), 2w + 1 (high half); 4.25 KB */
+    /* 4.25 KB: HIST counts 16-bit halves (bin h of lane l: half l & 1 of
+     * word 32 h + l / 2, bins 0..32); COLLECT lists 32-bit words (entry a of
+     * lane l: word 64 a + l, rows 0..KS_LIST, the sink row KS_HW - 1) */
+    __shared__ uint32_t H[KS_HW * 64];
     const int lane = threadIdx.x & 63;
     if (P.tiles && P.n_tiles_dev && (int64_t)blockIdx.x >= (int64_t)*P.n_tiles_dev) return;
     const uint32_t tile = P.tiles ? P.tiles[blockIdx.x] : blockIdx.x;
@@ -2010,6 +2013,11 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
             const f2 inv2 = {sinv, sinv}, sc2 = {ssc, ssc}, one2 = {1.f, 1.f}, c3 = {3.f * INV_PI, 3.f * INV_PI};
             const f2 nx2 = {nsx, nsx}, ny2 = {nsy, nsy}, nz2 = {nsz, nsz};
             uint32_t *hcol = H + lane;
+            /* HIST counters: bin h of lane l is the (l & 1) half of word
+             * h * 32 + l / 2 (lanes l, l ^ 1 share a word column), so a count
+             * is one address op and a per-lane constant increment */
+            uint32_t *hpair = H + (lane >> 1);
+            const uint32_t hinc = 1u << ((lane & 1) * 16);
             /* COLLECT: the lane's list rows (lanes outside the pass write the sink row) */
             uint32_t *lcol = hcol + (act ? 0 : (KS_HW - 1) * 64);
             uint32_t ccl = 0u;
@@ -2072,8 +2080,8 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
                             if constexpr (PT == KS_HIST) {
                                 const uint32_t h0 = min(max(__builtin_elementwise_sub_sat(u0, hA) >> hsh, hlo), (uint32_t)KS_NB);
                                 const uint32_t h1 = min(max(__builtin_elementwise_sub_sat(u1, hA) >> hsh, hlo), (uint32_t)KS_NB);
-                                atomicAdd(hcol + (h0 >> 1) * 64u, 1u << (h0 << 4)); /* shift mod 32: (h & 1) * 16 */
-                                atomicAdd(hcol + (h1 >> 1) * 64u, 1u << (h1 << 4));
+                                atomicAdd(hpair + h0 * 32u, hinc);
+                                atomicAdd(hpair + h1 * 32u, hinc);
                             } else if constexpr (PT == KS_COLLECT) {
                                 lcol[ccl * 64u] = u0;
                                 ccl += (u0 - clo) < cw ? 1u : 0u;
@@ -2113,18 +2121,18 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
                 /* the bin holding the K-th value; the column is left zeroed */
                 uint32_t cum = 0u, below = 0u, cntb = 0u;
                 int bs = -1;
+                /* both lanes of a word read it before either clears it (one
+                 * instruction each); a neighbour outside the pass counted only
+                 * into the sink, so its halves of bins 0..31 are zero anyway */
+                const uint32_t hs = (uint32_t)(lane & 1) * 16u;
 #pragma unroll 4
-                for (int w = 0; w < KS_NB / 2; ++w) {
-                    const uint32_t hw = hcol[w * 64];
-                    hcol[w * 64] = 0u;
-#pragma unroll
-                    for (int hh = 0; hh < 2; ++hh) {
-                        const uint32_t c = (hw >> (16 * hh)) & 0xffffu;
-                        if (bs < 0 && cum + c >= (uint32_t)K) { bs = 2 * w + hh; below = cum; cntb = c; }
-                        cum += c;
-                    }
+                for (int b = 0; b < KS_NB; ++b) {
+                    const uint32_t c = (hpair[b * 32] >> hs) & 0xffffu;
+                    hpair[b * 32] = 0u;
+                    if (bs < 0 && cum + c >= (uint32_t)K) { bs = b; below = cum; cntb = c; }
+                    cum += c;
                 }
-                hcol[(KS_HW - 1) * 64] = 0u;
+                hpair[KS_NB * 32] = 0u;
                 if (lvl0 && cum < (uint32_t)K) { /* fewer than K inside maxD: r_k^2 = maxD^2 */
                     full = false;
                     md2 = maxd2;
