@@ -92,6 +92,9 @@ struct Ctx {
     /* photon buckets */
     DevBuf d_count, d_cell_start, d_scratch, d_pha, d_phb;
     DevBuf d_knnpk, d_knnovf; /* kNN scalar stream: photon pairs, handed-back tiles (+ count) */
+    uint64_t map_gen = 0;      /* bumped by every bucket build */
+    uint64_t knn_pack_gen = ~0ull; /* the map d_knnpk's pairs were packed from */
+    void *knn_pack_ptr = nullptr;  /* ... and the pair buffer they were written to */
     bool knn_ss = true;       /* kNN: k_gather_knn_ss first (PM_KNN_SS=0: k_gather_knn_tile alone) */
     bool fuse_ok = true;      /* trace may fuse the bucket counting (off for the sub-contexts of a multi-device group) */
     struct { bool valid = false; int64_t n = 0; GridDesc grid{}; float r2 = 0.f; int64_t key_np = 0; int mpc = 1; } fused; /* counts made by the last trace (keys plane-major when key_np > 0) */
@@ -143,6 +146,9 @@ struct Ctx {
     uint32_t *h_r2hist = nullptr, *h_r2hist_dev = nullptr; /* host-mapped R2_BINS words, its device address */
     hipEvent_t r2_event = nullptr;
     bool r2_wanted = false;    /* a progressive pass asked for the radii (no histogram otherwise) */
+    bool r2_accum = false;     /* d_r2hist holds bins of this pass's gathers (every band), not yet reduced */
+    bool r2_dirty = false;     /* d_r2hist holds bins of invalidated radii: zero before binning again */
+    float r2_accum_init = 0.f; /* the r^2 the accumulated bins are relative to */
     bool r2_pending = false;   /* a histogram copy in flight */
     bool r2_valid = false;     /* the last landed / in-flight histogram describes the records */
     float r2_hist_init = 0.f;  /* the r^2 its bins are relative to */
@@ -351,6 +357,15 @@ void halton_perm(uint32_t seed, uint32_t out[28]) {
     }
 }
 
+/* the records' radii changed in a way that may raise them (eye pass, reset,
+ * upload, set_radius2, kNN radii): the adaptive grid falls back to the
+ * initial radius, and bins accumulated from the old radii are dropped */
+static void r2_invalidate(Ctx *c) {
+    c->r2_valid = false;
+    c->design_r2 = 0.f;
+    if (c->r2_accum) { c->r2_accum = false; c->r2_dirty = true; }
+}
+
 template <class T>
 int upload(Ctx *c, DevBuf &b, const std::vector<T> &v) {
     HIPCHK(c, b.ensure(std::max<size_t>(v.size() * sizeof(T), 16)));
@@ -368,8 +383,7 @@ int ensure_records(Ctx *c) {
     HIPCHK(c, c->d_dl.ensure(n * sizeof(float4)));
     c->nrec = n;
     c->tiles_valid = false;
-    c->r2_valid = false;
-    c->design_r2 = 0.f;
+    r2_invalidate(c);
     return PM_OK;
 }
 
@@ -1233,8 +1247,7 @@ int pm_eye_pass(void *ptr, const pm_render_params *p, void *stream) {
     timer_end(c, "eye", s);
     c->rec_fresh = false; /* the eye pass writes every record */
     c->tiles_valid = false;
-    c->r2_valid = false;
-    c->design_r2 = 0.f;
+    r2_invalidate(c);
     if (c->view_active && (rc = build_view(c, s))) return rc;
     return PM_OK;
 }
@@ -1284,30 +1297,49 @@ int pm_set_slot_buffer(void *ptr, void *d, int64_t n) {
  * initial radius. Refreshed only where a photon map's grid is chosen
  * (pm_trace_photons with fused counting, or pm_build_photon_map without), so
  * the trace and the build of one pass agree. */
-static float grid_radius2(Ctx *c, const pm_render_params *p, bool refresh) {
+static float grid_radius2(Ctx *c, const pm_render_params *p, bool refresh, hipStream_t s) {
     const float init = p->initial_radius2;
     if (p->estimator == PM_ESTIMATOR_KNN || c->grid_quantile <= 0.0) return init;
-    /* a pass that continues a render (no reset pending): the next fused
-     * gather bins its radii for the passes after it */
-    if (refresh && !c->rec_fresh) c->r2_wanted = true;
-    if (c->rec_fresh || !c->r2_valid || c->r2_hist_init != init) return init;
-    if (refresh && c->r2_pending && hipEventQuery(c->r2_event) == hipSuccess) {
-        c->r2_pending = false;
-        uint64_t cnt[R2_BINS] = {0}, total = 0;
-        for (int b = 0; b < R2_BINS; ++b) cnt[b] = ((volatile uint32_t *)c->h_r2hist)[b];
-        for (int b = 0; b < R2_BINS; ++b) total += cnt[b];
-        /* bins b.. hold t = r^2 / init <= 2^(-b/8): the largest b that still
-         * covers the quantile */
-        int best = 0;
-        uint64_t above = total;
-        for (int b = 0; b < R2_BINS; ++b) {
-            if ((double)above < c->grid_quantile * (double)total) break;
-            best = b;
-            above -= cnt[b];
+    if (refresh) {
+        /* a new pass. First a landed sum sets the grid radius (if it still
+         * describes the records) ... */
+        if (c->r2_pending && hipEventQuery(c->r2_event) == hipSuccess) {
+            c->r2_pending = false;
+            if (c->r2_valid && c->r2_hist_init == init) {
+                uint64_t cnt[R2_BINS] = {0}, total = 0;
+                for (int b = 0; b < R2_BINS; ++b) cnt[b] = ((volatile uint32_t *)c->h_r2hist)[b];
+                for (int b = 0; b < R2_BINS; ++b) total += cnt[b];
+                /* bins b.. hold t = r^2 / init <= 2^(-b/8): the largest b that still
+                 * covers the quantile */
+                int best = 0;
+                uint64_t above = total;
+                for (int b = 0; b < R2_BINS; ++b) {
+                    if ((double)above < c->grid_quantile * (double)total) break;
+                    best = b;
+                    above -= cnt[b];
+                }
+                /* the bins come from an approximate log2: a small margin */
+                c->design_r2 = total ? std::min(init, (float)(init * std::exp2(-best / (double)R2_PER_OCTAVE) * 1.01)) : 0.f;
+            }
         }
-        /* the bins come from an approximate log2: a small margin */
-        c->design_r2 = total ? std::min(init, (float)(init * std::exp2(-best / (double)R2_PER_OCTAVE) * 1.01)) : 0.f;
+        /* ... then the previous pass's gathers — all of its record ranges (a
+         * group device's or an all-gather rank's bands) — binned their radii
+         * into d_r2hist: sum them once, into host-mapped memory (not while a
+         * sum is in flight: the pinned buffer is reused; the bins keep
+         * accumulating, and older radii only overestimate) */
+        if (c->r2_accum && !c->r2_pending &&
+            launch_r2hist_reduce(c->d_r2hist.as<uint32_t>(), c->h_r2hist_dev, s) == hipSuccess &&
+            hipEventRecord(c->r2_event, s) == hipSuccess) {
+            c->r2_pending = true;
+            c->r2_accum = false;
+            c->r2_valid = true;
+            c->r2_hist_init = c->r2_accum_init;
+        }
+        /* a pass that continues a render (no reset pending): its gathers bin
+         * their radii for the passes after it */
+        c->r2_wanted = !c->rec_fresh;
     }
+    if (c->rec_fresh || !c->r2_valid || c->r2_hist_init != init) return init;
     return c->design_r2 > 0.f ? c->design_r2 : init;
 }
 
@@ -1417,7 +1449,7 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
     c->fused.valid = false;
     const bool fuse = c->fuse_ok && p->gather_structure == PM_GATHER_GRID && path_begin == slot_path_base;
     if (fuse) {
-        c->fused.r2 = grid_radius2(c, p, true);
+        c->fused.r2 = grid_radius2(c, p, true, s);
         const GridDesc g = make_grid(c, p, c->fused.r2);
         HIPCHK(c, c->d_count.ensure(((size_t)g.ncells + 1) * 4));
         HIPCHK(c, c->d_scratch.ensure(bucket_scratch_words(end_slot, g.ncells) * 4));
@@ -1474,7 +1506,7 @@ int pm_build_photon_map(void *ptr, const pm_render_params *p, int64_t n_slots, v
     GridDesc &g = c->grid;
     /* the grid of the trace's fused counts, if they cover these slots */
     const bool fused_ok = c->fused.valid && c->fused.n == n_slots;
-    c->grid_r2 = fused_ok ? c->fused.r2 : grid_radius2(c, p, true);
+    c->grid_r2 = fused_ok ? c->fused.r2 : grid_radius2(c, p, true, s);
     g = make_grid(c, p, c->grid_r2);
     const bool counted = fused_ok && same_grid(c->fused.grid, g);
     const size_t n = (size_t)n_slots;
@@ -1489,6 +1521,7 @@ int pm_build_photon_map(void *ptr, const pm_render_params *p, int64_t n_slots, v
     HIPCHK(c, launch_bucket_build(c->d_slots.as<pm_photon>(), n_slots, g, c->d_count.as<uint32_t>(),
                                   c->d_cell_start.as<uint32_t>(), c->d_scratch.as<uint32_t>(), c->d_pha.as<float4>(),
                                   c->d_phb.as<float4>(), counted, s, counted ? c->fused.key_np : 0, c->fused.mpc));
+    ++c->map_gen; /* kNN pairs repacked on the next kNN gather */
     /* the scan left the counters zeroed */
     c->count_zero_words = (size_t)g.ncells + 1;
     c->count_zero_ptr = c->d_count.p;
@@ -1565,19 +1598,23 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
     }
     if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters.p, 0, 32, s));
     /* a fused PPM tile gather bins the updated radii (grid_radius2) — over
-     * all records, or over a band of them (a device's bands in a group render
-     * or an all-gather rank: interleaved rows, a sample of the image's radii;
-     * the grid only sets the cost, never the sums) */
-    /* (not while the previous histogram's copy is in flight: the pinned
-     * buffer is reused, and a stale histogram only overestimates radii) */
+     * all records, or over each of a pass's bands (a device's bands in a
+     * group render or an all-gather rank): every gather of the pass adds to
+     * the same bins, summed once when the next pass chooses its grid, so the
+     * quantile describes every record the context gathers (the grid only
+     * sets the cost, never the sums) */
     const bool hist = p->estimator == PM_ESTIMATOR_PPM && p->gather_structure == PM_GATHER_GRID && !partial &&
                       !split && c->gather_kernel == PM_GK_TILE &&
-                      !c->counting && c->grid_quantile > 0.0 && c->r2_wanted &&
-                      !(c->r2_pending && hipEventQuery(c->r2_event) != hipSuccess);
+                      !c->counting && c->grid_quantile > 0.0 && c->r2_wanted;
     if (hist) {
+        if (c->r2_accum && c->r2_accum_init != p->initial_radius2) { c->r2_accum = false; c->r2_dirty = true; }
         if (!c->d_r2hist.p) {
             HIPCHK(c, c->d_r2hist.ensure(R2_COPIES * R2_BINS * 4));
-            HIPCHK(c, hipMemsetAsync(c->d_r2hist.p, 0, R2_COPIES * R2_BINS * 4, s)); /* the reduce re-zeroes it */
+            c->r2_dirty = true;
+        }
+        if (c->r2_dirty) { /* the reduce re-zeroes it; anything else left in it is dropped here */
+            HIPCHK(c, hipMemsetAsync(c->d_r2hist.p, 0, R2_COPIES * R2_BINS * 4, s));
+            c->r2_dirty = false;
         }
         if (!c->h_r2hist) {
             HIPCHK(c, hipHostMalloc((void **)&c->h_r2hist, R2_BINS * 4, hipHostMallocMapped));
@@ -1605,6 +1642,9 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
             G.knn_pk_p = c->d_knnpk.as<float4>();
             G.knn_pk_q = G.knn_pk_p + 2 * pairs;
             G.knn_pk_pairs = pairs;
+            G.knn_pack = c->knn_pack_gen != c->map_gen || c->knn_pack_ptr != c->d_knnpk.p;
+            c->knn_pack_gen = c->map_gen;
+            c->knn_pack_ptr = c->d_knnpk.p;
             G.knn_ovf_n = c->d_knnovf.as<uint32_t>();
             G.knn_ovf = G.knn_ovf_n + KNN_OVF_HDR;
         }
@@ -1642,17 +1682,13 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
     c->rec_estimator = p->estimator;
     if (consume) c->rec_fresh = false;
     if (hist) {
-        /* summed into host-mapped memory by a one-block kernel: no copy-engine
-         * transfer in the stream (a per-pass D2H copy cost ~0.5 ms of C2 step) */
-        HIPCHK(c, launch_r2hist_reduce(c->d_r2hist.as<uint32_t>(), c->h_r2hist_dev, s));
-        HIPCHK(c, hipEventRecord(c->r2_event, s));
-        c->r2_pending = true;
-        c->r2_wanted = false;
-        c->r2_valid = true;
-        c->r2_hist_init = p->initial_radius2;
+        /* summed by grid_radius2 at the next pass, into host-mapped memory by
+         * a one-block kernel: no copy-engine transfer in the stream (a
+         * per-pass D2H copy cost ~0.5 ms of C2 step) */
+        c->r2_accum = true;
+        c->r2_accum_init = p->initial_radius2;
     } else if (p->estimator == PM_ESTIMATOR_KNN) {
-        c->r2_valid = false; /* r_k^2 replaced the radii */
-        c->design_r2 = 0.f;
+        r2_invalidate(c); /* r_k^2 replaced the radii */
     }
     return PM_OK;
 }
@@ -1732,8 +1768,7 @@ int pm_set_radius2(void *ptr, const void *d_in, int64_t rec_begin, int64_t rec_c
     int rc;
     if ((rc = materialize_reset(c, pick(c, stream)))) return rc;
     HIPCHK(c, launch_radius2_io(recs(c), (float *)d_in, rec_begin, rec_count, 1, view_list(c), pick(c, stream)));
-    c->r2_valid = false; /* radii may have grown */
-    c->design_r2 = 0.f;
+    r2_invalidate(c); /* radii may have grown */
     return PM_OK;
 }
 
@@ -2122,8 +2157,7 @@ int pm_upload_records(void *ptr, const pm_record *in, int64_t n) {
     HIPCHK(c, hipMemcpy(c->d_n.p, N.data(), n * 4, hipMemcpyHostToDevice));
     c->rec_fresh = false; /* every record overwritten */
     c->tiles_valid = false;
-    c->r2_valid = false;
-    c->design_r2 = 0.f;
+    r2_invalidate(c);
     if (c->view_active && (rc = build_view(c, c->stream))) return rc;
     return PM_OK;
 }
@@ -2327,8 +2361,7 @@ int pm_reset_records(void *ptr, const pm_render_params *p, void *stream) {
      * other reader applies it first (materialize_reset) */
     c->rec_fresh = true;
     c->rec_fresh_r2 = p->initial_radius2;
-    c->r2_valid = false;
-    c->design_r2 = 0.f;
+    r2_invalidate(c);
     return PM_OK;
 }
 

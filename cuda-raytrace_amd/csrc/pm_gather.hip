@@ -956,15 +956,12 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
     if (__ballot(direct)) {
         const bool cand = direct && small;
         uint32_t own = 0u;
-        if (cand) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t cy = R.y0 + (uint32_t)(k & 1), cz = R.z0 + (uint32_t)(k >> 1);
-                if (cy <= R.y1 && cz <= R.z1) {
+        if (cand) { /* every row of the lane's box (up to KR x KR with finer cells) */
+            for (uint32_t cz = R.z0; cz <= R.z1; ++cz)
+                for (uint32_t cy = R.y0; cy <= R.y1; ++cy) {
                     const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
                     own += P.cell_start[row + R.x1 + 1u] - P.cell_start[row + R.x0];
                 }
-            }
         }
         const uint32_t tot = uniform_u32(__builtin_amdgcn_readlane(wave_incl_sum_u32(own), 63));
 #ifdef PM_COOP_STATS
@@ -2240,9 +2237,16 @@ hipError_t launch_gather_knn(const GatherParams &p, int count, hipStream_t s) {
         if (!g) return hipSuccess;
         if (p.knn_pk_p && p.knn_r2 > 1e-30f) { /* the level-0 bins need bits(maxD^2) >= 32 << sh */
             /* scalar stream, then k_gather_knn_tile over the tiles it handed back */
+            /* the pairs once per photon map (band gathers reuse them); the
+             * overflow counters of every gather */
             const int64_t np = p.knn_pk_pairs;
-            pm_launch(k_knn_pack, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, p.cell_start, p.grid.ncells,
-                      p.ph_a, p.ph_b, p.knn_pk_p, p.knn_pk_q, np, p.knn_ovf_n);
+            if (p.knn_pack)
+                pm_launch(k_knn_pack, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, p.cell_start, p.grid.ncells,
+                          p.ph_a, p.ph_b, p.knn_pk_p, p.knn_pk_q, np, p.knn_ovf_n);
+            else {
+                const hipError_t e = hipMemsetAsync(p.knn_ovf_n, 0, 64 * sizeof(uint32_t), s);
+                if (e != hipSuccess) return e;
+            }
             pm_launch(k_gather_knn_ss, dim3(g), dim3(64), 0, s, p);
             GatherParams q = p;
             q.tiles = p.knn_ovf;

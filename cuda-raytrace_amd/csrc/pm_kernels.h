@@ -188,6 +188,7 @@ struct GatherParams {
      * tiles it hands back to k_gather_knn_tile (knn_ovf, length *knn_ovf_n) */
     float4 *knn_pk_p, *knn_pk_q;
     int64_t knn_pk_pairs;
+    int knn_pack; /* 1: (re)write the pairs (the map changed since the last pack); else only clear the counters */
     uint32_t *knn_ovf, *knn_ovf_n;
 };
 /* knn_ovf_n[0] = handed-back tiles; [1..63] and the 16-word records at

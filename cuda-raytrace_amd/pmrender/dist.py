@@ -295,11 +295,18 @@ class PassRunner:
             # trace + build do not read records: they overlap the previous exchange
             if self.paths:
                 e.trace_photons(p, pass_index, self.path_begin, self.paths, self.path_begin)
-            e.build_photon_map(p, self.slots_mine)
+                e.build_photon_map(p, self.slots_mine)
             self._finish_exchange()
             if reset:
-                e.reset_records(p)
-            e.gather_split(p, self.count, self.flux)
+                e.reset_records(p)                  # deferred: the split update below consumes it
+            if self.paths:
+                e.gather_split(p, self.count, self.flux)
+            else:
+                # strong scaling with more ranks than chunks: no photons here, so
+                # this rank adds nothing to the sums (and builds no map, which
+                # would otherwise come from stale slots of an earlier pass)
+                self.count.zero_()
+                self.flux.zero_()
             self._start_exchange()
             if self.time_exchange:
                 self._timed(self._finish_exchange)

@@ -209,14 +209,16 @@ def _single_process_reference(world, total=None):
                                                   ("allgather", 3, None), ("reduce", 1, None), ("allgather", 1, None),
                                                   ("reduce", 8, None), ("allgather", 8, None),
                                                   ("reduce", 3, 3 * PATHS + 1001), ("allgather", 3, 3 * PATHS + 1001),
-                                                  ("allgather", 8, 8 * PATHS - 4093)])
+                                                  ("allgather", 8, 8 * PATHS - 4093),
+                                                  ("reduce", 4, 5), ("allgather", 8, 9)])
 def test_two_rank_pass_matches_single_process(exchange, world, total, tmp_path):
     """world-size 2 (and 3 / 4 / 8: view chunks and bands that do not divide
     evenly; 8 = the production rank count of one node) over gloo vs one
     process over the same global paths; world 1 with the exchange path forced
     (force_exchange: what the GPU test runs on RCCL); `total`: strong scaling
     (bench.py --total-paths), a fixed path count split over the ranks with a
-    short last chunk"""
+    short last chunk — or, for totals below the world size's chunks (4 ranks
+    / 5 paths, 8 / 9), ranks with no paths at all"""
     mp.start_processes(_worker, args=(world, _free_port(), exchange, str(tmp_path), total), nprocs=world, join=True,
                        start_method="spawn")
     ref_recs, ref_img = _single_process_reference(world, total)

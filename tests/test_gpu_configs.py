@@ -164,6 +164,89 @@ def test_c4_share(rank, oracle_mod, hip_mod):
         ctx.close()
 
 
+def test_c4_allgather_map(oracle_mod, hip_mod):
+    """C4 in north_star's all-gather form: after the RCCL
+    all-gather of the 8 ranks' slots every GPU holds all 4,194,304 paths'
+    16,777,216 slots, builds ONE photon map over them and gathers its own
+    interleaved 8-row bands of the 3840x2160 records (pmrender.dist._bands).
+    Here one context holds what every rank holds after the exchange (the 8
+    shards traced at their global path ids are the one 4,194,304-path trace,
+    slot for slot) and gathers the bands of ranks 0 and 7:
+      * slots bit-exact vs the oracle, map photons == valid slots;
+      * the bands' records vs the oracle's kd-tree gather over the same
+        slots (gathering.cu:104-126): M -> N', r^2 exact, flux <= 2e-5;
+        records outside the two ranks' bands untouched;
+      * the same bands after the reduce exchange's form — the 8 shards'
+        2,097,152-slot maps gathered one by one into per-record partial sums
+        (int32 M, int64 fixed-point flux), summed, then one split update —
+        are the full map's records bit for bit (exact fixed-point sums)."""
+    import torch
+    from pmrender.dist import _bands
+    W, H, world, per = 3840, 2160, 8, 524_288
+    total = world * per
+    sc = scenes.cornell_box(W, H)
+    p = RenderParams.defaults(paths_per_pass=total)
+    ctx, orc = make_pair(sc, oracle_mod, hip_mod)
+    try:
+        ctx.eye_pass(p)
+        ctx.trace_photons(p, 0, 0, total)
+        ctx.build_photon_map(p, total * 4)
+        n = ctx.num_records()
+        bands = _bands(n, ((W + 7) // 8) * 64, world)
+        mine = [bands[0], bands[world - 1]]
+        for runs in mine:
+            for b, c in runs:
+                ctx.gather_range(p, b, c)
+        info = ctx.map_info()
+        got = ctx.download_records()
+        slots = ctx.download_slots(total * 4)
+    finally:
+        ctx.close()
+    ref_slots = orc.trace_photons(p, 0, 0, total)
+    assert_bitexact(slots, ref_slots, "C4 all-gathered slots (16,777,216)")
+    del slots
+    nvalid = int((ref_slots["bits"] & 1).sum())
+    assert info["valid"] == nvalid > 8_000_000, (info, nvalid)
+    recs = orc.eye_pass(p)
+    idx = np.concatenate([np.arange(b, b + c) for runs in mine for b, c in runs])
+    assert len(idx) > 2_000_000
+    sub = recs[idx].copy()
+    orc.gather(orc.build_kdtree(ref_slots), sub, p)
+    del ref_slots
+    assert (sub["photon_count"] > 0).sum() > 500_000
+    compare_gathered_records(got[idx], sub)
+    rest = np.ones(n, bool)
+    rest[idx] = False
+    assert_bitexact(got[rest], recs[rest], "records outside ranks 0 and 7's bands")
+    del recs, sub
+
+    # the reduce exchange's form over the same paths: 8 shard maps, summed partials
+    ps = RenderParams.defaults(paths_per_pass=per)
+    ctx = sc.load_into(hip_mod.Context(0))
+    try:
+        ctx.eye_pass(ps)
+        nv = ctx.set_record_view(True)
+        dev = torch.device("cuda", 0)
+        cnt = torch.zeros(nv, dtype=torch.int32, device=dev)
+        flux = torch.zeros((nv, 3), dtype=torch.int64, device=dev)
+        cnt_sum, flux_sum = torch.zeros_like(cnt), torch.zeros_like(flux)
+        for r in range(world):
+            ctx.trace_photons(ps, 0, r * per, per, slot_path_base=r * per)
+            ctx.build_photon_map(ps, per * 4)
+            torch.cuda.synchronize()
+            ctx.gather_split(ps, cnt.data_ptr(), flux.data_ptr())
+            ctx.synchronize()
+            cnt_sum += cnt
+            flux_sum += flux
+        torch.cuda.synchronize()
+        ctx.ppm_update_split(ps, cnt_sum.data_ptr(), flux_sum.data_ptr(), 0, nv)
+        ctx.synchronize()
+        red = ctx.download_records()
+    finally:
+        ctx.close()
+    assert_bitexact(red[idx], got[idx], "bands: sum of the 8 reduce-mode shares vs the all-gathered map")
+
+
 def test_c3_full_workload(oracle_mod, hip_mod):
     """C3: Cornell enclosure + 1M-triangle soup, 1,048,576 paths, 1080p.
     Oracle: eye records and every photon slot bit-exact, per-record PPM

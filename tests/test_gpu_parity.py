@@ -383,6 +383,44 @@ def test_adaptive_grid_radius_progressive(oracle_mod, hip_mod, monkeypatch):
     compare_gathered_records(outs["0"][0], ref, flux_rtol=5e-5)
 
 
+def test_adaptive_grid_radius_from_bands(hip_mod):
+    """Band gathers (an all-gather rank's or a group device's record ranges)
+    bin their radii into one histogram per pass, summed once at the next
+    pass: a context that gathers every band of 4 ranks in turn
+    picks the same grid as full-range gathers, pass for pass, with the same
+    records; one rank's interleaved bands pick a grid within one histogram
+    bin of it."""
+    from pmrender.dist import HipEngine, _bands  # noqa: F401
+    sc = scenes.caustic_scene(96, 72)
+    p = RenderParams.defaults(paths_per_pass=32768, initial_radius2=25.0)
+    runs = {}
+    for mode in ("full", "all_bands", "rank0"):
+        ctx = sc.load_into(hip_mod.Context(0))
+        try:
+            ctx.eye_pass(p)
+            unit = ((ctx.width + 7) // 8) * 64 if ctx.pinhole else 512
+            bands = _bands(ctx.num_records(), unit, 4)
+            ranges = {"full": [(0, ctx.num_records())], "all_bands": [r for b in bands for r in b],
+                      "rank0": bands[0]}[mode]
+            cells = []
+            for k in range(8):
+                ctx.trace_photons(p, k, 0, p.paths_per_pass)
+                ctx.build_photon_map(p, p.paths_per_pass * 4)
+                cells.append(ctx.map_info()["cells"])
+                for b, c in ranges:
+                    ctx.gather_range(p, b, c)
+                ctx.synchronize()  # each histogram lands before the pass after next picks its grid
+            runs[mode] = (cells, ctx.download_records())
+        finally:
+            ctx.close()
+    assert runs["full"][0][-1] > runs["full"][0][0], "the grid did not follow the shrinking radii"
+    assert runs["all_bands"][0] == runs["full"][0], (runs["all_bands"][0], runs["full"][0])
+    assert_bitexact(runs["all_bands"][1], runs["full"][1], "records, band gathers vs full-range gathers")
+    # one bin of the histogram is 2^(1/8) in r^2: cells scale with r^-3 (1.30x per bin)
+    for a, b in zip(runs["rank0"][0], runs["full"][0]):
+        assert b / 1.31 <= a <= b * 1.31, (runs["rank0"][0], runs["full"][0])
+
+
 def test_soup_tile_gather(oracle_mod, hip_mod):
     """Incoherent tiles (a triangle soup: neighbouring pixels on unrelated
     triangles: leader groups and per-lane scans): two fused passes match the
