@@ -209,7 +209,7 @@ def test_c4_allgather_map(oracle_mod, hip_mod):
     assert info["valid"] == nvalid > 8_000_000, (info, nvalid)
     recs = orc.eye_pass(p)
     idx = np.concatenate([np.arange(b, b + c) for runs in mine for b, c in runs])
-    assert len(idx) > 2_000_000
+    assert len(idx) > 1_900_000  # 2 x 3,840 x 2,160 / 8 less the bands short of a whole run
     sub = recs[idx].copy()
     orc.gather(orc.build_kdtree(ref_slots), sub, p)
     del ref_slots
