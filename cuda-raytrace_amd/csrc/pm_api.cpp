@@ -92,6 +92,7 @@ struct Ctx {
     /* photon buckets */
     DevBuf d_count, d_cell_start, d_scratch, d_pha, d_phb;
     DevBuf d_knnpk, d_knnovf; /* kNN scalar stream: photon pairs, handed-back tiles (+ count) */
+    DevBuf d_tile_times;      /* PM_TILE_TIMES diagnostic builds */
     uint64_t map_gen = 0;      /* bumped by every bucket build */
     uint64_t knn_pack_gen = ~0ull; /* the map d_knnpk's pairs were packed from */
     void *knn_pack_ptr = nullptr;  /* ... and the pair buffer they were written to */
@@ -119,6 +120,11 @@ struct Ctx {
     DevBuf d_tiles, d_tile_flags, d_tile_count;
     int64_t n_tiles = 0;           /* valid once tile_count_known */
     bool tiles_valid = false;      /* the list on the device matches the records */
+    /* the list is reordered once by the measured cost of its tiles (the first
+     * full-range tile gather on it records them; launch_tile_sort); env
+     * PM_TILE_SORT=0 keeps record order */
+    DevBuf d_tile_cost, d_tiles2;
+    bool tile_sort = true, tiles_sorted = false;
     bool tile_count_known = false; /* its length read back (pinned copy + event, never waited on) */
     uint32_t *h_tile_count = nullptr;
     hipEvent_t tile_event = nullptr;
@@ -755,6 +761,7 @@ int pm_create(void **out, const pm_config *cfg) {
         c->gather_kernel = !strcmp(e, "lane") ? PM_GK_LANE : PM_GK_TILE;
     if (const char *e = getenv("PM_KNN_SS")) c->knn_ss = atoi(e) != 0;
     if (const char *e = getenv("PM_CELL_SPAN")) c->cell_span = std::max(2, std::min(5, atoi(e)));
+    if (const char *e = getenv("PM_TILE_SORT")) c->tile_sort = atoi(e) != 0;
     if (const char *e = getenv("PM_GRID_QUANTILE")) c->grid_quantile = atof(e);
     if (const char *e = getenv("PM_TRACE_HOLD")) c->trace_hold = atoi(e) != 0;
     if (const char *e = getenv("PM_POOL_STACK")) c->pool_stack = std::max(0, atoi(e));
@@ -795,7 +802,7 @@ void pm_destroy(void *ptr) {
         }
     DevBuf *bufs[] = {&c->d_scene, &c->d_rays, &c->d_rand2d, &c->d_pos, &c->d_nrm, &c->d_state, &c->d_n,
                       &c->d_dl, &c->d_slots, &c->d_count, &c->d_scratch, &c->d_vflags, &c->d_vrank, &c->d_vlist, &c->d_vsums,
-                      &c->d_cell_start, &c->d_pha, &c->d_phb, &c->d_knnpk, &c->d_knnovf,
+                      &c->d_cell_start, &c->d_pha, &c->d_phb, &c->d_knnpk, &c->d_knnovf, &c->d_tile_times, &c->d_tile_cost, &c->d_tiles2,
                       &c->d_kd, &c->d_out, &c->d_counters, &c->d_tiles, &c->d_tile_flags, &c->d_tile_count,
                       &c->d_r2hist, &c->d_spill};
     for (DevBuf *b : bufs) b->release();
@@ -1552,6 +1559,7 @@ static int ensure_tiles(Ctx *c, hipStream_t s) {
         HIPCHK(c, hipMemcpyAsync(c->h_tile_count, c->d_tile_count.p, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipEventRecord(c->tile_event, s));
         c->tiles_valid = true;
+        c->tiles_sorted = false;
         c->tile_count_known = false;
     }
     if (!c->tile_count_known && hipEventQuery(c->tile_event) == hipSuccess) {
@@ -1594,6 +1602,11 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
         G.tiles = c->d_tiles.as<uint32_t>();
         if (c->tile_count_known) { G.n_tiles = c->n_tiles; G.n_tiles_dev = nullptr; }
         else { G.n_tiles = (c->nrec + 63) / 64; G.n_tiles_dev = c->d_tile_count.as<uint32_t>(); }
+        if (c->tile_sort && !c->tiles_sorted && p->estimator == PM_ESTIMATOR_PPM) {
+            HIPCHK(c, c->d_tile_cost.ensure((size_t)((c->nrec + 63) / 64 + 8) * 2));
+            HIPCHK(c, c->d_tiles2.ensure(c->d_tiles.bytes));
+            G.tile_cost = c->d_tile_cost.as<uint16_t>();
+        }
         /* fresh PPM gather: every radius is r2init, the first group's box comes from the tile's position box */
     }
     if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters.p, 0, 32, s));
@@ -1667,7 +1680,36 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
         }
     } else {
         if (p->gather_structure == PM_GATHER_KDTREE) HIPCHK(c, hipMemsetAsync(G.error, 0, 4, s));
+#ifdef PM_TILE_TIMES
+        /* diagnostic builds: env PM_TILE_TIMES=file appends each tile launch's
+         * per-wave (start, end, XCC_ID, HW_ID) records (tools/tile_times.py) */
+        const char *tt_path = getenv("PM_TILE_TIMES");
+        const int64_t tt_n = (c->nrec + 63) / 64;
+        if (tt_path && G.tiles) {
+            HIPCHK(c, c->d_tile_times.ensure((size_t)tt_n * 64));
+            HIPCHK(c, hipMemsetAsync(c->d_tile_times.p, 0, (size_t)tt_n * 64, s));
+            G.tile_times = c->d_tile_times.as<unsigned long long>();
+        }
+#endif
         HIPCHK(c, launch_gather(G, p->gather_structure, partial != nullptr || split, c->counting, s));
+        if (G.tile_cost) { /* the measured costs reorder the list for the next gathers */
+            HIPCHK(c, launch_tile_sort(G.tiles, G.tile_cost, G.n_tiles_dev, G.n_tiles, c->d_tiles2.as<uint32_t>(), s));
+            std::swap(c->d_tiles, c->d_tiles2);
+            c->tiles_sorted = true;
+        }
+#ifdef PM_TILE_TIMES
+        if (G.tile_times) {
+            std::vector<unsigned long long> h((size_t)tt_n * 8);
+            HIPCHK(c, hipMemcpyAsync(h.data(), G.tile_times, h.size() * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            if (FILE *f = fopen(tt_path, "ab")) {
+                const unsigned long long hdr[4] = {0xffffffffffffffffull, (unsigned long long)tt_n, 0, 0};
+                fwrite(hdr, 8, 4, f);
+                fwrite(h.data(), 8, h.size(), f);
+                fclose(f);
+            }
+        }
+#endif
     }
     timer_end(c, "gather", s);
     if (p->estimator != PM_ESTIMATOR_KNN && p->gather_structure == PM_GATHER_KDTREE) {

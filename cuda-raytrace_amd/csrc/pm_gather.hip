@@ -311,9 +311,12 @@ constexpr int TILE_CAP = PM_TILE_CAP; /* photons per LDS window (two per lane) *
 #endif
 struct TileLds {
 #if PM_TILE_PAIRS
-    /* TILE_CAP + 2 pairs: a run's aligned pairs reach at most one pair past
-     * 2 x TILE_CAP positions' half (lanes beyond their run, masked) */
-    float4 pr[2 * (TILE_CAP + 2)];
+    /* TILE_CAP pairs: a run's aligned pairs reach at most one pair past
+     * them (lanes beyond their run, masked): that read lands in b[] below,
+     * inside the block's LDS. No padding pairs: 7,680 B per wave (the LDS
+     * allocation granule makes 7,744 B fit 18 one-wave blocks per CU, 7,680
+     * B 20, the VGPR limit): C2 gather 47.4-48.6 -> 44.4-46.3 us (same box) */
+    float4 pr[2 * TILE_CAP];
 #else
     /* positions SoA, so that a pair of neighbouring photons is one ds_read2;
      * 2 x TILE_CAP entries: the test loop reads up to TILE_CAP past a run's
@@ -412,6 +415,9 @@ PMD long long d2ll(double d) {
 #ifdef PM_TILE_STATS
 #define TILE_STAT(k, v) do { const unsigned long long tv_ = (unsigned long long)(v); \
     if ((threadIdx.x & 63) == 0) atomicAdd(&P.counters[8 + (k)], tv_); } while (0)
+#elif defined(PM_TILE_TIMES)
+/* per-wave counts for the wave timeline records (k_gather_tile only) */
+#define TILE_STAT(k, v) do { tstat[(k)] += (uint32_t)(v); } while (0)
 #else
 #define TILE_STAT(k, v) do { } while (0)
 #endif
@@ -637,9 +643,10 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
     __shared__ TileLds tiles[TILE_BLOCK / 64];
     TileLds &T = tiles[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
-    int64_t r;
+    int64_t r, w = 0;
+    const unsigned long long tc0 = P.tile_cost ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (P.tiles) { /* only tiles with an active record (no block-level barrier below: a wave may leave) */
-        int64_t w = (int64_t)blockIdx.x * (TILE_BLOCK / 64) + (threadIdx.x >> 6);
+        w = (int64_t)blockIdx.x * (TILE_BLOCK / 64) + (threadIdx.x >> 6);
         const int64_t nt = P.n_tiles_dev ? (int64_t)*P.n_tiles_dev : P.n_tiles;
         if (w >= nt) return;
         if (TILE_BLOCK == 64) w = xcd_tile(w, nt);
@@ -648,6 +655,10 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
         r = P.rec_begin + (int64_t)blockIdx.x * TILE_BLOCK + threadIdx.x;
     }
     const GridDesc &g = P.grid;
+#ifdef PM_TILE_TIMES
+    const unsigned long long tt0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t tstat[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     GProf gp;
     gp.begin();
     GatherRec R;
@@ -984,8 +995,24 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
     gp.mark(5);
     R.store<PARTIAL>(P, r, M, Lf);
     if (!PARTIAL && P.r2hist) r2_histogram(P, R.live, R.st.w);
+    if (P.tile_cost && lane == 0)
+        P.tile_cost[w] = (uint16_t)min(__builtin_amdgcn_s_memrealtime() - tc0, 65535ull);
     gp.mark(6);
     gp.flush(P.counters);
+#ifdef PM_TILE_TIMES
+    if (P.tile_times && lane == 0) {
+        uint32_t xcc, hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        unsigned long long *o = P.tile_times + 8 * (size_t)blockIdx.x;
+        o[0] = tt0; o[1] = __builtin_amdgcn_s_memrealtime(); o[2] = xcc; o[3] = hw;
+        /* groups | windows << 32, test pairs | hit iterations << 32, direct lanes | chunks << 32, staged | record << 32 */
+        o[4] = tstat[0] | ((unsigned long long)tstat[1] << 32);
+        o[5] = tstat[2] | ((unsigned long long)tstat[3] << 32);
+        o[6] = tstat[4] | ((unsigned long long)tstat[5] << 32);
+        o[7] = tstat[7] | ((unsigned long long)(r - lane) << 32);
+    }
+#endif
 }
 
 /* ---------------------------------------------------------------------- */
@@ -1299,6 +1326,10 @@ struct KnnSel {
 };
 
 __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
+#ifdef PM_TILE_TIMES
+    uint32_t tstat[8] = {0, 0, 0, 0, 0, 0, 0, 0}; /* TILE_STAT's sink (unused here) */
+    (void)tstat;
+#endif
     __shared__ KnnLds L;
     const int lane = threadIdx.x & 63;
     if (P.tiles && P.n_tiles_dev && (int64_t)blockIdx.x >= (int64_t)*P.n_tiles_dev) return; /* one wave per block */
@@ -1853,6 +1884,10 @@ PMD uint32_t cell_u(float u, int dim) {
     return (uint32_t)(c < 0 ? 0 : (c >= dim ? dim - 1 : c));
 }
 __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
+#ifdef PM_TILE_TIMES
+    uint32_t tstat[8] = {0, 0, 0, 0, 0, 0, 0, 0}; /* TILE_STAT's sink (unused here) */
+    (void)tstat;
+#endif
     /* 4.25 KB: HIST counts 16-bit halves (bin h of lane l: half l & 1 of
      * word 32 h + l / 2, bins 0..32); COLLECT lists 32-bit words (entry a of
      * lane l: word 64 a + l, rows 0..KS_LIST, the sink row KS_HW - 1) */
@@ -2589,6 +2624,49 @@ __global__ __launch_bounds__(1024) void k_tile_compact(const uint8_t *flags, int
     }
     if (threadIdx.x == 0) *count = base;
 }
+/* Cost-ordered tile list (one block): the tile gather's launch ends with
+ * the waves dispatched last (each a tile's whole lifetime, 9.5 us on average
+ * at C2, up to 35 us for the densest tiles), so the order of the list sets
+ * the drain. The groups of 8 entries a wave's XCD takes together (xcd_tile)
+ * are counting-sorted by the largest lifetime among them, heaviest first, in
+ * 256 log-spaced buckets (3 % each); the order inside a bucket is the atomics'
+ * (any order gives the same sums). */
+__global__ __launch_bounds__(1024) void k_tile_sort(const uint32_t *list, const uint16_t *cost, const uint32_t *n_dev,
+                                                    int64_t n_host, uint32_t *out) {
+    __shared__ uint32_t hist[256];
+    const int tid = threadIdx.x;
+    const int64_t n = n_dev ? (int64_t)*n_dev : n_host, S = n / 8;
+    if (tid < 256) hist[tid] = 0u;
+    __syncthreads();
+    auto bucket = [&](int64_t g) {
+        uint32_t c = 1u;
+        for (int k = 0; k < 8; ++k) c = max(c, (uint32_t)cost[8 * g + k]);
+        /* 24 buckets per octave from 16 ticks (0.16 us) up; heaviest -> 0 */
+        const int b = (int)(24.f * (__log2f((float)c) - 4.f));
+        return 255 - min(max(b, 0), 255);
+    };
+    for (int64_t g = tid; g < S; g += 1024) atomicAdd(&hist[bucket(g)], 1u);
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t run = 0u;
+        for (int b = 0; b < 256; ++b) { const uint32_t c = hist[b]; hist[b] = run; run += c; }
+    }
+    __syncthreads();
+    for (int64_t g = tid; g < S; g += 1024) {
+        const uint32_t pos = atomicAdd(&hist[bucket(g)], 1u);
+        const uint4 *src = reinterpret_cast<const uint4 *>(list + 8 * g);
+        uint4 *dst = reinterpret_cast<uint4 *>(out + 8 * (int64_t)pos);
+        dst[0] = src[0];
+        dst[1] = src[1];
+    }
+    for (int64_t i = 8 * S + tid; i < n; i += 1024) out[i] = list[i]; /* the partial group stays last */
+}
+hipError_t launch_tile_sort(const uint32_t *list, const uint16_t *cost, const uint32_t *n_dev, int64_t n, uint32_t *out,
+                            hipStream_t s) {
+    pm_launch(k_tile_sort, dim3(1), dim3(1024), 0, s, list, cost, n_dev, n, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_tile_list(const RecordsDev &R, uint8_t *flags, uint32_t *list, uint32_t *count, hipStream_t s) {
     if (R.count <= 0) return hipSuccess;
     pm_launch(k_tile_flags, dim3((unsigned)((R.count + 255) / 256)), dim3(256), 0, s, R, flags);

@@ -183,6 +183,13 @@ struct GatherParams {
     /* non-null: the list's length is this device word (the host has not read
      * it back yet); n_tiles then bounds the grid (every tile) */
     const uint32_t *n_tiles_dev;
+    /* non-null: each tile wave stores its lifetime (s_memrealtime ticks,
+     * saturated to 16 bits) at tile_cost[list entry], for the cost-ordered
+     * list of the next gathers (launch_tile_sort) */
+    uint16_t *tile_cost;
+    /* PM_TILE_TIMES diagnostic builds: per launched wave (start, end)
+     * s_memrealtime and (XCC_ID, HW_ID), 4 u64 at tile_times[4 * block] */
+    unsigned long long *tile_times;
     /* kNN scalar-stream kernel (k_gather_knn_ss): photon pairs (k_knn_pack,
      * knn_pk_pairs of them: 2 float4 + 3 float4 per pair) and the list of
      * tiles it hands back to k_gather_knn_tile (knn_ovf, length *knn_ovf_n) */
@@ -244,6 +251,11 @@ hipError_t launch_final(const FinalParams &p, hipStream_t s);
 /* list[0 .. *count) = the tiles (records [64 t, 64 t + 64)) holding an
  * active record, ascending, built on the device (flags: one byte per tile) */
 hipError_t launch_tile_list(const RecordsDev &R, uint8_t *flags, uint32_t *list, uint32_t *count, hipStream_t s);
+/* the tile list reordered by measured cost: groups of 8 consecutive entries
+ * (a wave's XCD group, xcd_tile) in descending order of their largest
+ * tile_cost, the last partial group kept last; n = *n_dev when non-null */
+hipError_t launch_tile_sort(const uint32_t *list, const uint16_t *cost, const uint32_t *n_dev, int64_t n, uint32_t *out,
+                            hipStream_t s);
 hipError_t launch_radius2_io(const RecordsDev &R, float *buf, int64_t rec_begin, int64_t rec_count, int to_records,
                              const uint32_t *view, hipStream_t s);
 /* exclusive scan of n uint32 (pm_bucket.hip); in/out 16-B aligned; sums: scan_scratch_words(n) */
