@@ -1602,7 +1602,8 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
         G.tiles = c->d_tiles.as<uint32_t>();
         if (c->tile_count_known) { G.n_tiles = c->n_tiles; G.n_tiles_dev = nullptr; }
         else { G.n_tiles = (c->nrec + 63) / 64; G.n_tiles_dev = c->d_tile_count.as<uint32_t>(); }
-        if (c->tile_sort && !c->tiles_sorted && p->estimator == PM_ESTIMATOR_PPM) {
+        /* the PPM tile gather and the kNN scalar-stream kernel record the costs */
+        if (c->tile_sort && !c->tiles_sorted && (p->estimator == PM_ESTIMATOR_PPM || c->knn_ss)) {
             HIPCHK(c, c->d_tile_cost.ensure((size_t)((c->nrec + 63) / 64 + 8) * 2));
             HIPCHK(c, c->d_tiles2.ensure(c->d_tiles.bytes));
             G.tile_cost = c->d_tile_cost.as<uint16_t>();
@@ -1692,11 +1693,6 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
         }
 #endif
         HIPCHK(c, launch_gather(G, p->gather_structure, partial != nullptr || split, c->counting, s));
-        if (G.tile_cost) { /* the measured costs reorder the list for the next gathers */
-            HIPCHK(c, launch_tile_sort(G.tiles, G.tile_cost, G.n_tiles_dev, G.n_tiles, c->d_tiles2.as<uint32_t>(), s));
-            std::swap(c->d_tiles, c->d_tiles2);
-            c->tiles_sorted = true;
-        }
 #ifdef PM_TILE_TIMES
         if (G.tile_times) {
             std::vector<unsigned long long> h((size_t)tt_n * 8);
@@ -1710,6 +1706,11 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
             }
         }
 #endif
+    }
+    if (G.tile_cost) { /* the measured wave lifetimes reorder the list for the next gathers */
+        HIPCHK(c, launch_tile_sort(G.tiles, G.tile_cost, G.n_tiles_dev, G.n_tiles, c->d_tiles2.as<uint32_t>(), s));
+        std::swap(c->d_tiles, c->d_tiles2);
+        c->tiles_sorted = true;
     }
     timer_end(c, "gather", s);
     if (p->estimator != PM_ESTIMATOR_KNN && p->gather_structure == PM_GATHER_KDTREE) {

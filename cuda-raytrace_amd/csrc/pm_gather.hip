@@ -1894,6 +1894,12 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
     __shared__ uint32_t H[KS_HW * 64];
     const int lane = threadIdx.x & 63;
     if (P.tiles && P.n_tiles_dev && (int64_t)blockIdx.x >= (int64_t)*P.n_tiles_dev) return;
+    const unsigned long long tc0 = P.tile_cost ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    /* the wave's lifetime for the cost-ordered tile list (k_tile_sort) */
+    auto record_cost = [&]() {
+        if (P.tile_cost && lane == 0)
+            P.tile_cost[blockIdx.x] = (uint16_t)min(__builtin_amdgcn_s_memrealtime() - tc0, 65535ull);
+    };
     const uint32_t tile = P.tiles ? P.tiles[blockIdx.x] : blockIdx.x;
     const int64_t r = P.rec_begin + (int64_t)tile * 64 + lane;
     const int K = P.knn_k;
@@ -2243,6 +2249,7 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
     }
     if (__ballot(defer)) { /* re-run by k_gather_knn_tile */
         if (lane == 0) P.knn_ovf[atomicAdd(P.knn_ovf_n, 1u)] = tile;
+        record_cost();
         return;
     }
 #ifdef PM_KNN_SS_DBG
@@ -2257,6 +2264,7 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
         P.R.state[r] = make_float4(flux.x, flux.y, flux.z, md2);
         P.R.n[r] = (float)cnt;
     }
+    record_cost();
     gp.mark(6);
     gp.flush(P.counters);
 }
