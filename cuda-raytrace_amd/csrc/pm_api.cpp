@@ -1662,7 +1662,29 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
             G.knn_ovf_n = c->d_knnovf.as<uint32_t>();
             G.knn_ovf = G.knn_ovf_n + KNN_OVF_HDR;
         }
+#ifdef PM_TILE_TIMES
+        const char *tt_path = getenv("PM_TILE_TIMES");
+        const int64_t tt_n = (c->nrec + 63) / 64;
+        if (tt_path && G.tiles) {
+            HIPCHK(c, c->d_tile_times.ensure((size_t)tt_n * 64));
+            HIPCHK(c, hipMemsetAsync(c->d_tile_times.p, 0, (size_t)tt_n * 64, s));
+            G.tile_times = c->d_tile_times.as<unsigned long long>();
+        }
+#endif
         HIPCHK(c, launch_gather_knn(G, c->counting, s));
+#ifdef PM_TILE_TIMES
+        if (G.tile_times) {
+            std::vector<unsigned long long> h((size_t)tt_n * 8);
+            HIPCHK(c, hipMemcpyAsync(h.data(), G.tile_times, h.size() * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            if (FILE *f = fopen(tt_path, "ab")) {
+                const unsigned long long hdr[4] = {0xffffffffffffffffull, (unsigned long long)tt_n, 0, 0};
+                fwrite(hdr, 8, 4, f);
+                fwrite(h.data(), 8, h.size(), f);
+                fclose(f);
+            }
+        }
+#endif
         if (G.knn_ovf_n && getenv("PM_KNN_SS_DEBUG")) { /* tiles handed back to k_gather_knn_tile */
             uint32_t nb = 0;
             HIPCHK(c, hipMemcpyAsync(&nb, G.knn_ovf_n, 4, hipMemcpyDeviceToHost, s));

@@ -1845,6 +1845,16 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
 constexpr int KS_NB = 32;   /* bins per histogram level (+1 sink), 16-bit counters: two lanes per word */
 constexpr int KS_HW = KS_NB / 2 + 1; /* LDS words per lane: (KS_NB + 1) 16-bit counters, or KS_LIST + 1 list rows + a sink row */
 constexpr int KS_LIST = 12; /* values a COLLECT keeps per lane (rows 0..KS_LIST of the histogram, +1 scratch) */
+/* (y, z) rows of a group's union box: two per lane. With 64, a tile across a
+ * corner of the room (lanes on two walls, the union deeper than 8 x 8 rows)
+ * split into leader groups, each running its own passes over nearly the same
+ * photons: those tiles took up to 19 passes against 3.65 on average and set
+ * the launch's length (tools/tile_times.py knn) */
+#ifndef PM_KS_ROWS
+#define PM_KS_ROWS 128
+#endif
+constexpr int KS_ROWS = PM_KS_ROWS;
+static_assert(KS_ROWS == 64 || KS_ROWS == 128, "one or two union rows per lane");
 enum { KS_HIST = 0, KS_COLLECT = 1, KS_SUM = 2, KS_DONE = 3 };
 static_assert(KS_LIST + 1 < KS_HW, "the COLLECT list aliases histogram rows (not the sink's)");
 
@@ -1894,7 +1904,11 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
     __shared__ uint32_t H[KS_HW * 64];
     const int lane = threadIdx.x & 63;
     if (P.tiles && P.n_tiles_dev && (int64_t)blockIdx.x >= (int64_t)*P.n_tiles_dev) return;
+#ifdef PM_TILE_TIMES
+    const unsigned long long tc0 = __builtin_amdgcn_s_memrealtime();
+#else
     const unsigned long long tc0 = P.tile_cost ? __builtin_amdgcn_s_memrealtime() : 0ull;
+#endif
     /* the wave's lifetime for the cost-ordered tile list (k_tile_sort) */
     auto record_cost = [&]() {
         if (P.tile_cost && lane == 0)
@@ -1962,15 +1976,23 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
         bool mine = pend;
         union_box6(g, mine, x0, x1, y0, y1, z0, z1, X0, X1, Y0, Y1, Z0, Z1);
         uint32_t LY = Y1 > Y0 ? 32u - (uint32_t)__builtin_clz(Y1 - Y0) : 0u;
-        if (LY > 6u || ((uint64_t)(Z1 - Z0 + 1u) << LY) > 64u) {
+        if (LY > 7u || ((uint64_t)(Z1 - Z0 + 1u) << LY) > (uint64_t)KS_ROWS) {
+            /* the first pending lane's neighbourhood: the lanes whose box
+             * starts within GRk cells of the leader's, for the widest GRk whose
+             * union still fits the row map (a surface seen at a grazing angle
+             * spreads its tile over several cells: wider groups, fewer of them,
+             * each with its own passes) */
             const int leader = __builtin_ctzll(pm);
             const uint32_t lx = __builtin_amdgcn_readlane(x0, leader), ly = __builtin_amdgcn_readlane(y0, leader),
                            lz = __builtin_amdgcn_readlane(z0, leader);
-            mine = pend && x0 + KT_GROUP_R - lx <= 2u * KT_GROUP_R && y0 + KT_GROUP_R - ly <= 2u * KT_GROUP_R &&
-                   z0 + KT_GROUP_R - lz <= 2u * KT_GROUP_R;
-            union_box6(g, mine, x0, x1, y0, y1, z0, z1, X0, X1, Y0, Y1, Z0, Z1);
-            LY = Y1 > Y0 ? 32u - (uint32_t)__builtin_clz(Y1 - Y0) : 0u;
-            if (LY > 6u || ((uint64_t)(Z1 - Z0 + 1u) << LY) > 64u) { defer = true; break; } /* grid too coarse */
+            bool fits = false;
+            for (uint32_t GRk = KS_ROWS > 64 ? 4u : KT_GROUP_R; !fits && GRk >= KT_GROUP_R; GRk >>= 1) {
+                mine = pend && x0 + GRk - lx <= 2u * GRk && y0 + GRk - ly <= 2u * GRk && z0 + GRk - lz <= 2u * GRk;
+                union_box6(g, mine, x0, x1, y0, y1, z0, z1, X0, X1, Y0, Y1, Z0, Z1);
+                LY = Y1 > Y0 ? 32u - (uint32_t)__builtin_clz(Y1 - Y0) : 0u;
+                fits = LY <= 7u && ((uint64_t)(Z1 - Z0 + 1u) << LY) <= (uint64_t)KS_ROWS;
+            }
+            if (!fits) { defer = true; break; } /* grid too coarse */
         }
         pend = pend && !mine;
         /* passes until every lane of the group has its estimate (a level
@@ -2020,10 +2042,13 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
             const float mnx = wave_min_f(act ? ux : INFINITY), mxx = wave_max_f(act ? ux : -INFINITY);
             const float mny = wave_min_f(act ? uy : INFINITY), mxy = wave_max_f(act ? uy : -INFINITY);
             const float mnz = wave_min_f(act ? uz : INFINITY), mxz = wave_max_f(act ? uz : -INFINITY);
-            /* union row u = lane: photons [Bu, Bu + Lu) of cells xa..xb of its (y, z) */
-            uint32_t Bu = 0u, Lu = 0u;
-            {
-                const uint32_t cy = PY0 + ((uint32_t)lane & ((1u << PLY) - 1u)), cz = PZ0 + ((uint32_t)lane >> PLY);
+            /* union rows u = lane and lane + 64: photons [Bu, Bu + Lu) of cells
+             * xa..xb of its (y, z) */
+            uint32_t Bu[2] = {0u, 0u}, Lu[2] = {0u, 0u};
+#pragma unroll
+            for (int h = 0; h < KS_ROWS / 64; ++h) {
+                const uint32_t u = (uint32_t)lane + 64u * (uint32_t)h;
+                const uint32_t cy = PY0 + (u & ((1u << PLY) - 1u)), cz = PZ0 + (u >> PLY);
                 if (cy <= PY1 && cz <= PZ1) {
                     const float gy = box_gap(mny, mxy, cy, g.dy), gz = box_gap(mnz, mxz, cz, g.dz);
                     const float rem = Rq * Rq - (gy * gy + gz * gz);
@@ -2032,17 +2057,17 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
                         const uint32_t xa = max(PX0, cell_u(mnx - sx, g.dx)), xb = min(PX1, cell_u(mxx + sx, g.dx));
                         if (xa <= xb) {
                             const uint32_t row = (cz * (uint32_t)g.dy + cy) * (uint32_t)g.dx;
-                            Bu = P.cell_start[row + xa];
-                            Lu = P.cell_start[row + xb + 1u] - Bu;
+                            Bu[h] = P.cell_start[row + xa];
+                            Lu[h] = P.cell_start[row + xb + 1u] - Bu[h];
                         }
                     }
                 }
             }
-            unsigned long long rows = __ballot(Lu > 0u);
+            const unsigned long long rows = __ballot(Lu[0] > 0u), rows_hi = KS_ROWS > 64 ? __ballot(Lu[1] > 0u) : 0ull;
             /* 16-bit bin counters: a union of >= 2^16 photons goes to k_gather_knn_tile */
-            if (uniform_u32(__builtin_amdgcn_readlane(wave_incl_sum_u32(Lu), 63)) >= 65536u) { defer = true; break; }
+            if (uniform_u32(__builtin_amdgcn_readlane(wave_incl_sum_u32(Lu[0] + Lu[1]), 63)) >= 65536u) { defer = true; break; }
 #ifdef PM_KNN_SS_DBG
-            const unsigned long long rows0 = rows;
+            const unsigned long long rows0 = rows | rows_hi;
 #endif
             /* per-lane constants of the pass (lanes outside it never hit) */
             const uint32_t hA = act ? A : 0u, hsh = act ? sh : 0u, hlo = act ? 0u : (uint32_t)KS_NB;
@@ -2067,12 +2092,16 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
             auto stream = [&](auto PT_) PM_INLINE {
                 constexpr int PT = decltype(PT_)::value;
                 constexpr int NP = PT == KS_SUM ? 2 : 4;
-                unsigned long long rm = rows;
-                while (rm) {
-                    const int u = __builtin_ctzll(rm);
-                    rm &= rm - 1ull;
-                    const uint32_t b = uniform_u32(__builtin_amdgcn_readlane(Bu, u));
-                    const uint32_t e = b + uniform_u32(__builtin_amdgcn_readlane(Lu, u));
+                unsigned long long rm = rows, rm_hi = rows_hi;
+                while (rm | rm_hi) {
+                    /* rows 0..63 (Bu[0] of lane u), then 64..127 (Bu[1]) */
+                    const bool hi = rm == 0ull;
+                    const unsigned long long cur = hi ? rm_hi : rm;
+                    const int u = __builtin_ctzll(cur);
+                    if (hi) rm_hi &= rm_hi - 1ull;
+                    else rm &= rm - 1ull;
+                    const uint32_t b = uniform_u32(__builtin_amdgcn_readlane(hi ? Bu[1] : Bu[0], u));
+                    const uint32_t e = b + uniform_u32(__builtin_amdgcn_readlane(hi ? Lu[1] : Lu[0], u));
                     const uint32_t k1 = (e + 1u) >> 1;
                     TILE_STAT(3, 1);
                     TILE_STAT(PT == KS_HIST ? 4 : PT == KS_COLLECT ? 5 : 6, k1 - (b >> 1));
@@ -2267,6 +2296,19 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
     record_cost();
     gp.mark(6);
     gp.flush(P.counters);
+#ifdef PM_TILE_TIMES
+    if (P.tile_times && lane == 0) {
+        uint32_t xcc, hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        unsigned long long *o = P.tile_times + 8 * (size_t)blockIdx.x;
+        o[0] = tc0; o[1] = __builtin_amdgcn_s_memrealtime(); o[2] = xcc; o[3] = hw;
+        o[4] = tstat[1] | ((unsigned long long)tstat[2] << 32);   /* passes | HIST passes */
+        o[5] = tstat[4] | ((unsigned long long)tstat[5] << 32);   /* HIST pairs | COLLECT pairs */
+        o[6] = tstat[6] | ((unsigned long long)tstat[3] << 32);   /* SUM pairs | rows */
+        o[7] = tstat[7] | ((unsigned long long)(r - lane) << 32); /* hit batches | record */
+    }
+#endif
 }
 
 hipError_t launch_gather_knn(const GatherParams &p, int count, hipStream_t s) {

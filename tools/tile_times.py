@@ -17,15 +17,19 @@ import torch  # noqa: F401,E402
 from pmrender import hip, scenes  # noqa: E402
 from pmrender.abi import RenderParams  # noqa: E402
 
-C5, C3 = "c5" in sys.argv[1:], "c3" in sys.argv[1:]
-name = "c5" if C5 else "c3" if C3 else "c2"
+C5, C3, KNN = "c5" in sys.argv[1:], "c3" in sys.argv[1:], "knn" in sys.argv[1:]
+name = ("c5" if C5 else "c3" if C3 else "c2") + ("_knn" if KNN else "")
 sc = (scenes.caustic_scene(1920, 1080) if C5 else
       scenes.triangle_soup(1_000_000, 1920, 1080) if C3 else scenes.cornell_box(1920, 1080))
 path = os.path.join(tempfile.mkdtemp(), "tt.bin")
 os.environ["PM_TILE_TIMES"] = path
 ctx = sc.load_into(hip.Context(0))
 PATHS = 1_048_576 if (C5 or C3) else 262144
-p = RenderParams.defaults(paths_per_pass=PATHS)
+if KNN:  # BASELINE C2 kNN line: K = 50, maxD^2 = 100 (k_gather_knn_ss)
+    from pmrender.abi import PM_ESTIMATOR_KNN
+    p = RenderParams.defaults(paths_per_pass=PATHS, initial_radius2=100.0, estimator=PM_ESTIMATOR_KNN, knn_lookup=50)
+else:
+    p = RenderParams.defaults(paths_per_pass=PATHS)
 ctx.eye_pass(p)
 for rep in range(4):
     ctx.reset_records(p)
@@ -51,7 +55,7 @@ out.append(f"{name}: {len(rec)} waves, launch span {span:.1f} us (first start ->
 q = np.percentile(life, [50, 90, 99])
 out.append(f"  wave lifetime: mean {life.mean():.2f} us, p50 {q[0]:.2f}, p90 {q[1]:.2f}, p99 {q[2]:.2f}, max {life.max():.2f}")
 out.append(f"  sum of lifetimes / span = {life.sum() / span:.0f} waves resident on average "
-           f"(limit {5 * 4 * 256} at 5 waves/SIMD)")
+           f"(limit {(6 if KNN else 5) * 4 * 256} at {6 if KNN else 5} waves/SIMD)")
 grid = np.arange(0, span + 1.0, 1.0)
 res = np.array([((s <= t) & (e > t)).sum() for t in grid])
 out.append("  resident waves per 1-us step: " + " ".join(str(int(x)) for x in res))
@@ -73,8 +77,13 @@ order = np.argsort(-life)[:10]
 blk = np.nonzero(last[:, 1] > 0)[0]
 lo32 = lambda v: v & 0xffffffff  # noqa: E731
 hi32 = lambda v: v >> 32  # noqa: E731
-st = {"groups": lo32(rec[:, 4]), "windows": hi32(rec[:, 4]), "pairs": lo32(rec[:, 5]), "hit_iters": hi32(rec[:, 5]),
-      "direct": lo32(rec[:, 6]), "chunks": hi32(rec[:, 6]), "staged": lo32(rec[:, 7])}
+if KNN:
+    st = {"passes": lo32(rec[:, 4]), "hist_passes": hi32(rec[:, 4]), "hist_pairs": lo32(rec[:, 5]),
+          "collect_pairs": hi32(rec[:, 5]), "sum_pairs": lo32(rec[:, 6]), "rows": hi32(rec[:, 6]),
+          "hit_batches": lo32(rec[:, 7])}
+else:
+    st = {"groups": lo32(rec[:, 4]), "windows": hi32(rec[:, 4]), "pairs": lo32(rec[:, 5]), "hit_iters": hi32(rec[:, 5]),
+          "direct": lo32(rec[:, 6]), "chunks": hi32(rec[:, 6]), "staged": lo32(rec[:, 7])}
 tile = hi32(rec[:, 7]) // 64
 out.append("  per-wave means: " + ", ".join(f"{k} {v.mean():.2f}" for k, v in st.items()))
 out.append("  slowest waves: block start life | tile (row, col of 240) | " + " ".join(st))
