@@ -114,7 +114,7 @@ def load_pmc_traffic(kernel_prefix, config, field="hbm_bytes_per_launch"):
     and this config; else (None, reason)."""
     sha = kernel_src_sha()
     path, d = None, None
-    for rnd in ("r04", "r03", "r02"):      # the newest committed profile of these sources
+    for rnd in ("r05", "r04", "r03", "r02"):      # the newest committed profile of these sources
         cand = os.path.join(ROOT, "profiles", rnd, "pmc_traffic_%s.json" % config)
         if os.path.exists(cand):
             with open(cand) as f:

@@ -89,6 +89,14 @@ struct Ctx {
     /* slots */
     DevBuf d_slots;
     int64_t slots_used = 0;
+    /* lazy zero fill (TraceParams::lazy_zero): slots [0, slots_dirty) may hold
+     * stale data where their fused-count key (d_scratch, dirty_key_np /
+     * dirty_mpc) is invalid; materialize_slots zeroes them before any reader
+     * but the bucket fill (env PM_LAZY_ZERO=0: the trace zeroes them itself) */
+    int64_t slots_dirty = 0, dirty_key_np = 0;
+    int dirty_mpc = 0;
+    hipEvent_t dirty_event = nullptr;
+    bool lazy_zero = true, slots_exposed = false;
     /* photon buckets */
     DevBuf d_count, d_cell_start, d_scratch, d_pha, d_phb;
     DevBuf d_knnpk, d_knnovf; /* kNN scalar stream: photon pairs, handed-back tiles (+ count) */
@@ -370,6 +378,20 @@ static void r2_invalidate(Ctx *c) {
     c->r2_valid = false;
     c->design_r2 = 0.f;
     if (c->r2_accum) { c->r2_accum = false; c->r2_dirty = true; }
+}
+
+/* the deferred zero fill of a lazy_zero trace, on stream s after the trace
+ * (s == nullptr: on the trace's own stream, waited for) */
+static int materialize_slots(Ctx *c, hipStream_t s) {
+    if (c->slots_dirty <= 0) return PM_OK;
+    const bool wait = s == nullptr;
+    if (wait) s = c->stream;
+    HIPCHK(c, hipStreamWaitEvent(s, c->dirty_event, 0));
+    HIPCHK(c, launch_zero_invalid_slots(c->d_slots.as<pm_photon>(), c->d_scratch.as<uint32_t>(), c->slots_dirty,
+                                        c->dirty_key_np, c->dirty_mpc, s));
+    c->slots_dirty = 0;
+    if (wait) HIPCHK(c, hipStreamSynchronize(s));
+    return PM_OK;
 }
 
 template <class T>
@@ -762,6 +784,7 @@ int pm_create(void **out, const pm_config *cfg) {
     if (const char *e = getenv("PM_KNN_SS")) c->knn_ss = atoi(e) != 0;
     if (const char *e = getenv("PM_CELL_SPAN")) c->cell_span = std::max(2, std::min(5, atoi(e)));
     if (const char *e = getenv("PM_TILE_SORT")) c->tile_sort = atoi(e) != 0;
+    if (const char *e = getenv("PM_LAZY_ZERO")) c->lazy_zero = atoi(e) != 0;
     if (const char *e = getenv("PM_GRID_QUANTILE")) c->grid_quantile = atof(e);
     if (const char *e = getenv("PM_TRACE_HOLD")) c->trace_hold = atoi(e) != 0;
     if (const char *e = getenv("PM_POOL_STACK")) c->pool_stack = std::max(0, atoi(e));
@@ -808,6 +831,7 @@ void pm_destroy(void *ptr) {
     for (DevBuf *b : bufs) b->release();
     if (c->tile_event) (void)hipEventDestroy(c->tile_event);
     if (c->r2_event) (void)hipEventDestroy(c->r2_event);
+    if (c->dirty_event) (void)hipEventDestroy(c->dirty_event);
     if (c->h_r2hist) (void)hipHostFree(c->h_r2hist);
     if (c->h_tile_count) (void)hipHostFree(c->h_tile_count);
     (void)hipStreamDestroy(c->stream);
@@ -1261,7 +1285,12 @@ int pm_eye_pass(void *ptr, const pm_render_params *p, void *stream) {
 
 int pm_reserve_slots(void *ptr, int64_t n, void **d_slots) {
     GETCTX(ptr);
+    int rc;
     if (n < 0) FAIL(c, PM_ERR_INVALID, "negative slot count");
+    if (d_slots) { /* the caller may read the buffer from now on: no lazy zero fill on it */
+        if ((rc = materialize_slots(c, nullptr))) return rc;
+        c->slots_exposed = true;
+    }
     if ((size_t)n * sizeof(pm_photon) > c->d_slots.bytes) {
         if (c->d_slots.external)
             FAIL(c, PM_ERR_INVALID, "external slot buffer holds %zu slots, %lld needed",
@@ -1283,6 +1312,8 @@ int pm_reserve_slots(void *ptr, int64_t n, void **d_slots) {
 
 int pm_set_slot_buffer(void *ptr, void *d, int64_t n) {
     GETCTX(ptr);
+    int rc;
+    if ((rc = materialize_slots(c, nullptr))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->d_slots.release();
     c->fused.valid = false;
@@ -1395,8 +1426,13 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
         FAIL(c, PM_ERR_INVALID, "photon slot index exceeds 32 bits (reference pm_index is a uint)");
     const int64_t mpc = p->max_photon_count;
     const int64_t end_slot = (path_begin + path_count - slot_path_base) * mpc;
-    if ((rc = pm_reserve_slots(c, end_slot, nullptr))) return rc;
     hipStream_t s = pick(c, stream);
+    const bool fuse = c->fuse_ok && p->gather_structure == PM_GATHER_GRID && path_begin == slot_path_base;
+    /* stale slots of an earlier lazy trace: zeroed now unless this fused
+     * trace rewrites (or re-marks) every one of them */
+    if (c->slots_dirty > 0 && !(fuse && end_slot >= c->slots_dirty) && (rc = materialize_slots(c, s))) return rc;
+    c->slots_dirty = 0;
+    if ((rc = pm_reserve_slots(c, end_slot, nullptr))) return rc;
     TraceParams T{};
     T.S = c->S;
     T.slots = c->d_slots.as<pm_photon>();
@@ -1454,7 +1490,6 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
      * of the bucket build (keys, ranks, per-cell counts) at deposit time; the
      * build then skips it (c->fused). Any other slot producer invalidates it. */
     c->fused.valid = false;
-    const bool fuse = c->fuse_ok && p->gather_structure == PM_GATHER_GRID && path_begin == slot_path_base;
     if (fuse) {
         c->fused.r2 = grid_radius2(c, p, true, s);
         const GridDesc g = make_grid(c, p, c->fused.r2);
@@ -1469,12 +1504,20 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
         /* plane-major keys / ranks; the held deposits write a path's four
          * keys as one 16-B store in slot order */
         T.key_np = !T.hold ? path_count : 0;
+        T.lazy_zero = c->lazy_zero && !T.hold && !c->d_slots.external && !c->slots_exposed ? 1 : 0;
     }
     timer_begin(c, "trace", s);
     /* the kernel writes all path_count * mpc slots: deposits, then zeros */
     HIPCHK(c, launch_trace(T, c->counting, s));
     timer_end(c, "trace", s);
     if (fuse) { c->fused.valid = true; c->fused.n = end_slot; c->fused.grid = T.grid; c->fused.key_np = T.key_np; c->fused.mpc = (int)mpc; c->count_zero_words = 0; }
+    if (T.lazy_zero) {
+        if (!c->dirty_event) HIPCHK(c, hipEventCreateWithFlags(&c->dirty_event, hipEventDisableTiming));
+        HIPCHK(c, hipEventRecord(c->dirty_event, s));
+        c->slots_dirty = end_slot;
+        c->dirty_key_np = T.key_np;
+        c->dirty_mpc = (int)mpc;
+    }
     /* traced photons carry the scene's signs (scene_nonneg); slots outside
      * the traced range keep theirs, so the flag is reset only when this
      * trace rewrote every slot in use */
@@ -1491,6 +1534,7 @@ int pm_build_photon_map(void *ptr, const pm_render_params *p, int64_t n_slots, v
     if ((size_t)n_slots * sizeof(pm_photon) > c->d_slots.bytes) FAIL(c, PM_ERR_INVALID, "n_slots beyond slot buffer");
     hipStream_t s = pick(c, stream);
     c->map_slots = n_slots;
+    if (p->gather_structure == PM_GATHER_KDTREE && (rc = materialize_slots(c, s))) return rc;
     if (p->gather_structure == PM_GATHER_KDTREE) {
         /* reference path (CreatePhotonMap): DtoH, CPU pbrt KdTree, HtoD */
         timer_begin(c, "build", s, true);
@@ -1516,6 +1560,8 @@ int pm_build_photon_map(void *ptr, const pm_render_params *p, int64_t n_slots, v
     c->grid_r2 = fused_ok ? c->fused.r2 : grid_radius2(c, p, true, s);
     g = make_grid(c, p, c->grid_r2);
     const bool counted = fused_ok && same_grid(c->fused.grid, g);
+    /* the counting pass below reads every slot's valid bit (and overwrites the keys) */
+    if (!counted && (rc = materialize_slots(c, s))) return rc;
     const size_t n = (size_t)n_slots;
     HIPCHK(c, c->d_count.ensure(((size_t)g.ncells + 1) * 4));
     HIPCHK(c, c->d_cell_start.ensure(((size_t)g.ncells + 1) * 4));
@@ -2154,7 +2200,9 @@ int pm_record_pixel(void *ptr, int64_t r, int64_t *pixel) {
 
 int pm_download_slots(void *ptr, pm_photon *out, int64_t n) {
     GETCTX(ptr);
+    int rc;
     if (!out || n < 0 || (size_t)n * sizeof(pm_photon) > c->d_slots.bytes) FAIL(c, PM_ERR_INVALID, "bad slot range");
+    if ((rc = materialize_slots(c, nullptr))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(out, c->d_slots.p, n * sizeof(pm_photon), hipMemcpyDeviceToHost));
     return PM_OK;
@@ -2164,6 +2212,7 @@ int pm_upload_slots(void *ptr, const pm_photon *in, int64_t n) {
     GETCTX(ptr);
     int rc;
     if (!in || n < 0) FAIL(c, PM_ERR_INVALID, "bad slots");
+    if ((rc = materialize_slots(c, nullptr))) return rc;
     if ((rc = pm_reserve_slots(c, n, nullptr))) return rc;
     c->fused.valid = false;
     HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -189,6 +189,24 @@ __global__ __launch_bounds__(256) void k_bucket_fill(const pm_photon *slots, int
  * eight equal-photon key ranges from the scan) left the write bytes at
  * ~58 MB and read every key 8x: 41 us vs 29 us, so not used. */
 
+__global__ __launch_bounds__(256) void k_zero_invalid_slots(pm_photon *slots, const uint32_t *key, int64_t n,
+                                                            int64_t key_np, int mpc) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int64_t ki = key_np > 0 ? (i % mpc) * key_np + i / mpc : i;
+    if (key[ki] != 0xffffffffu) return;
+    float2 *q = reinterpret_cast<float2 *>(slots + i);
+    const float2 z = make_float2(0.f, 0.f);
+    q[0] = z; q[1] = z; q[2] = z; q[3] = z; q[4] = z;
+}
+hipError_t launch_zero_invalid_slots(pm_photon *slots, const uint32_t *key, int64_t n, int64_t key_np, int mpc,
+                                     hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    pm_launch(k_zero_invalid_slots, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slots, key, n, key_np,
+              mpc > 0 ? mpc : 1);
+    return hipGetLastError();
+}
+
 size_t scan_scratch_words(int64_t n) { return (size_t)((n + SCAN_TILE - 1) / SCAN_TILE) + 16; }
 
 hipError_t launch_exclusive_scan(const uint32_t *in, int64_t n, uint32_t *out, uint32_t *sums, hipStream_t s) {

@@ -118,6 +118,10 @@ struct TraceParams {
     uint32_t spill_stride;
     /* fused counting: keys / ranks plane-major (deposit k of path i at k * key_np + i) when > 0, else at the slot index */
     int64_t key_np;
+    /* fused counting only: 1 = leave a path's unused slots as they are (their
+     * keys say invalid; pm_api zeroes them with launch_zero_invalid_slots
+     * before anything else reads the slot buffer) */
+    int lazy_zero;
 };
 
 struct GatherParams {
@@ -250,6 +254,11 @@ hipError_t launch_ppm_update_split(const GatherParams &p, const int *count, cons
 hipError_t launch_final(const FinalParams &p, hipStream_t s);
 /* list[0 .. *count) = the tiles (records [64 t, 64 t + 64)) holding an
  * active record, ascending, built on the device (flags: one byte per tile) */
+/* the slots of [0, n) whose fused-count key is invalid (0xffffffff) set to
+ * zero: the deferred zero fill of a lazy_zero trace (key index as the
+ * trace wrote it: plane-major k * key_np + path when key_np > 0) */
+hipError_t launch_zero_invalid_slots(pm_photon *slots, const uint32_t *key, int64_t n, int64_t key_np, int mpc,
+                                     hipStream_t s);
 hipError_t launch_tile_list(const RecordsDev &R, uint8_t *flags, uint32_t *list, uint32_t *count, hipStream_t s);
 /* the tile list reordered by measured cost: groups of 8 consecutive entries
  * (a wave's XCD group, xcd_tile) in descending order of their largest

@@ -467,7 +467,10 @@ PMD void finish_path(const TraceParams &P, PathState &st, const Held *held = nul
     const float2 z = make_float2(0.f, 0.f);
     for (uint32_t k = st.stored; k < mpc; ++k) {
         float2 *q = reinterpret_cast<float2 *>(slots + k);
-        q[0] = z; q[1] = z; q[2] = z; q[3] = z; q[4] = z;
+        /* lazy_zero (fused counting): the invalid key alone marks the slot;
+         * the bucket fill never reads it, and pm_api zeroes it before any
+         * other reader (C2 trace 75-79 -> 73-74 us: 20 MB of stores fewer) */
+        if (!P.lazy_zero) { q[0] = z; q[1] = z; q[2] = z; q[3] = z; q[4] = z; }
         if (P.bucket) P.key[key_index(P, st.pid, k)] = 0xffffffffu;
     }
 }

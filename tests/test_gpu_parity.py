@@ -383,6 +383,52 @@ def test_adaptive_grid_radius_progressive(oracle_mod, hip_mod, monkeypatch):
     compare_gathered_records(outs["0"][0], ref, flux_rtol=5e-5)
 
 
+def test_lazy_zero_fill_of_unused_slots(oracle_mod, hip_mod, monkeypatch):
+    """A fused-count trace leaves a path's unused slots stale (their keys mark
+    them invalid; PM_LAZY_ZERO) and the context zeroes them before any other
+    reader: slots read back, a kd-tree build, a smaller trace over part of the
+    range and a recount all see the eager trace's slots, bit for bit, and the
+    oracle's."""
+    sc = scenes.cornell_box(48, 32)
+    p = RenderParams.defaults(paths_per_pass=20000)
+    pk = RenderParams.defaults(paths_per_pass=20000, gather_structure=PM_GATHER_KDTREE)
+    out = {}
+    for lazy in ("0", "1"):
+        monkeypatch.setenv("PM_LAZY_ZERO", lazy)
+        ctx = sc.load_into(hip_mod.Context(0))
+        try:
+            ctx.eye_pass(p)
+            got = []
+            ctx.trace_photons(p, 1, 0, 20000)            # fused: slots [0, 80000) lazily zeroed
+            ctx.build_photon_map(p, 80000)
+            ctx.gather(p)
+            got.append(ctx.download_slots(80000))
+            ctx.trace_photons(p, 2, 0, 20000)
+            ctx.build_photon_map(pk, 80000)             # kd build reads every slot
+            got.append(ctx.download_slots(80000))
+            ctx.trace_photons(p, 3, 0, 20000)
+            ctx.trace_photons(p, 4, 0, 5000)             # covers a quarter: the stale tail is zeroed first
+            got.append(ctx.download_slots(80000))
+            ctx.trace_photons(p, 5, 0, 20000)
+            ctx.trace_photons(p, 6, 5000, 15000, slot_path_base=0)  # not fused: zeroes pass 5's stale slots first
+            ctx.build_photon_map(p, 80000)              # recount reads every slot's valid bit
+            ctx.gather(p)
+            got.append(ctx.download_slots(80000))
+            out[lazy] = (got, ctx.download_records())
+        finally:
+            ctx.close()
+    orc = sc.load_into(oracle_mod.Oracle())
+    ref = [orc.trace_photons(p, k, 0, 20000) for k in (1, 2)]
+    tail = orc.trace_photons(p, 3, 0, 20000)
+    head = orc.trace_photons(p, 4, 0, 5000)
+    ref.append(np.concatenate([head, tail[20000:]]))
+    ref.append(np.concatenate([orc.trace_photons(p, 5, 0, 20000)[:20000], orc.trace_photons(p, 6, 5000, 15000)]))
+    for k in range(4):
+        assert_bitexact(out["1"][0][k], out["0"][0][k], f"slots, step {k}: lazy vs eager zero fill")
+        assert_bitexact(out["1"][0][k], ref[k], f"slots, step {k}: vs oracle")
+    assert_bitexact(out["1"][1], out["0"][1], "records: lazy vs eager zero fill")
+
+
 def test_adaptive_grid_radius_from_bands(hip_mod):
     """Band gathers (an all-gather rank's or a group device's record ranges)
     bin their radii into one histogram per pass, summed once at the next
