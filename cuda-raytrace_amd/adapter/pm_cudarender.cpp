@@ -189,14 +189,39 @@ void CudaRender::createCudaShape(const std::string &name, const Shape &shape, co
 }
 
 /* The reference places an OptiX Transform over the instance's group
- * (cudarender.cpp:88-103); here the instance is flattened into world space:
- * triangle vertices / normals transformed, sphere and disk transforms
- * composed. (Instanced triangles are then intersected in world space — the
- * reference intersects them in instance space; see INTEGRATION.md.) */
+ * (cudarender.cpp:88-103). Here a triangle mesh of the group is stored once
+ * (pm_add_object_mesh, the first time the group is instanced) and each
+ * instance adds a two-level entry with the transform (pm_add_mesh_instance),
+ * whose hits equal those of the mesh flattened with this Transform (the
+ * device rebuilds each world triangle exactly as Transform::point does).
+ * Spheres and disks, and meshes under a projective transform, are flattened:
+ * their transforms composed, the vertices / normals transformed here. env
+ * PM_INSTANCING=0 flattens everything (the A/B of the two-level trees). */
 void CudaRender::objectInstance(const void *instance, const Transform &tr) {
     auto it = instances_.find(instance);
     if (it == instances_.end()) throw Error("Instance not found"); /* cudarender.cpp:96-98 Severe */
-    for (const Prim &p : it->second) {
+    const char *env = std::getenv("PM_INSTANCING");
+    const bool two_level = !(env && std::atoi(env) == 0) && tr.m[12] == 0.f && tr.m[13] == 0.f && tr.m[14] == 0.f &&
+                           tr.m[15] == 1.f;
+    for (size_t k = 0; k < it->second.size(); ++k) {
+        const Prim &p = it->second[k];
+        if (two_level && p.name == "trianglemesh") {
+            if (committed_) throw Error("shape added after the scene was committed");
+            auto ob = objects_.find({instance, k});
+            if (ob == objects_.end()) {
+                const Shape &s = p.shape;
+                const int nverts = (int)(s.P.size() / 3), ntris = (int)(s.indices.size() / 3);
+                const float *N = s.N.size() == s.P.size() && !s.N.empty() ? s.N.data() : nullptr;
+                const float *uv = s.uv.size() == 2 * (size_t)nverts && !s.uv.empty() ? s.uv.data() : nullptr;
+                int id = -1;
+                check(ctx_, pm_add_object_mesh(ctx_, s.P.data(), nverts, s.indices.data(), ntris, N, uv, p.material,
+                                               p.light, &id),
+                      "pm_add_object_mesh");
+                ob = objects_.emplace(std::make_pair(instance, k), id).first;
+            }
+            check(ctx_, pm_add_mesh_instance(ctx_, ob->second, tr.m, tr.minv), "pm_add_mesh_instance");
+            continue;
+        }
         Shape s = p.shape;
         if (p.name == "trianglemesh") {
             for (size_t v = 0; v + 2 < s.P.size(); v += 3) tr.point(&p.shape.P[v], &s.P[v]);

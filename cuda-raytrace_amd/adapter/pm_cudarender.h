@@ -188,6 +188,8 @@ private:
     CudaRenderer *renderer_ = nullptr;
     std::map<const Material *, int> materials_;
     std::map<const void *, std::vector<Prim>> instances_; /* pbrt ObjectBegin ... ObjectEnd */
+    /* the object meshes already stored (pm_add_object_mesh) per (instance key, prim) */
+    std::map<std::pair<const void *, size_t>, int> objects_;
     bool committed_ = false;
     bool lights_added_ = false;
 };

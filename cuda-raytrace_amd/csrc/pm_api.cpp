@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <functional>
 #include <mutex>
 #include <random>
 #include <string>
@@ -48,7 +49,16 @@ struct DevBuf {
 };
 
 struct HMesh { int material, light, has_n, has_uv; };
-struct HTri { int v[3]; int mesh; };
+struct HTri { int v[3]; int mesh; uint32_t gid; }; /* gid: global id (insertion order over all triangles) */
+/* two-level instancing: an object mesh stored once in object space, and its
+ * instances (pbrt ObjectBegin / ObjectInstance) */
+struct HObj {
+    std::vector<float> P, N, UV;
+    std::vector<int> idx;
+    int material = 0, light = -1;
+    bool has_n = false, has_uv = false;
+};
+struct HInst { int obj; float m[16], minv[16]; uint32_t gid_base; };
 struct Timer { hipEvent_t a = nullptr, b = nullptr; };
 struct TimerPool { std::vector<Timer> ev; size_t used = 0; };
 
@@ -63,6 +73,10 @@ struct Ctx {
     std::vector<float> P, N, UV;
     std::vector<HMesh> meshes;
     std::vector<HTri> tris;
+    uint32_t next_tri_id = 0;    /* global ids handed out to triangles (meshes and instances) */
+    std::vector<HObj> objs;
+    std::vector<HInst> insts;
+    int64_t obj_tris_stored = 0; /* object triangles in the committed scene (each mesh once) */
     std::vector<float4> disks;   /* 5 per disk */
     std::vector<float4> spheres; /* 4 per sphere */
     std::vector<float> sphere_o2w;
@@ -143,6 +157,7 @@ struct Ctx {
      * photon_count mean for the final pass (PPM state or kNN sums) */
     int rec_estimator = PM_ESTIMATOR_PPM;
     int kd_stack = KD_STACK;        /* kd gather stack entries (env PM_KD_STACK, tests only) */
+    bool trace_pool = true;         /* 4-wide scenes: the pooled trace kernel (env PM_TRACE_POOL=0: one path per lane) */
     bool trace_hold = true;         /* deposits written once per path where it costs no waves (env PM_TRACE_HOLD=0: per deposit) */
     int pool_stack = 31;            /* pooled kernel: LDS stack entries per lane (env PM_POOL_STACK; 0 = the exact bound): 31 lets five blocks share a CU's LDS */
     DevBuf d_spill;                 /* pooled kernel: stack entries beyond pool_stack */
@@ -522,6 +537,7 @@ int check_params(Ctx *c, const pm_render_params *p) {
 struct SceneLayout {
     size_t o_nodes = 0, o_refs = 0, o_geo = 0, o_shade = 0, o_tid = 0, o_info = 0, o_norms = 0, o_disks = 0,
            o_spheres = 0, o_mats = 0, o_lights = 0, o_wnodes = 0, bytes = 0;
+    size_t o_insts = 0, o_objv = 0, o_objinfo = 0, o_objn = 0, o_objuv = 0, o_objmesh = 0; /* instancing */
     int64_t n_nodes = 0, n_refs = 0, n_tris = 0;
     bool id_order = false;
     int wide = 0, wide_stack = 0;
@@ -787,6 +803,7 @@ int pm_create(void **out, const pm_config *cfg) {
     if (const char *e = getenv("PM_LAZY_ZERO")) c->lazy_zero = atoi(e) != 0;
     if (const char *e = getenv("PM_GRID_QUANTILE")) c->grid_quantile = atof(e);
     if (const char *e = getenv("PM_TRACE_HOLD")) c->trace_hold = atoi(e) != 0;
+    if (const char *e = getenv("PM_TRACE_POOL")) c->trace_pool = atoi(e) != 0;
     if (const char *e = getenv("PM_POOL_STACK")) c->pool_stack = std::max(0, atoi(e));
     if (const char *e = getenv("PM_KD_STACK")) c->kd_stack = std::max(1, std::min(KD_STACK, atoi(e)));
     if (const char *e = getenv("PM_STAGE_TIMERS")) if (atoi(e) == 0) c->timed_stages.clear();
@@ -886,9 +903,54 @@ int pm_add_trimesh(void *ptr, const float *P, int nverts, const int *idx, int nt
     int mid = (int)c->meshes.size();
     c->meshes.push_back(HMesh{material, light, N != nullptr, uv != nullptr});
     for (int t = 0; t < ntris; ++t)
-        c->tris.push_back(HTri{{(int)(base + idx[3 * t]), (int)(base + idx[3 * t + 1]), (int)(base + idx[3 * t + 2])}, mid});
+        c->tris.push_back(HTri{{(int)(base + idx[3 * t]), (int)(base + idx[3 * t + 1]), (int)(base + idx[3 * t + 2])}, mid,
+                               c->next_tri_id++});
     c->committed = false;
     return PM_OK;
+}
+
+int pm_add_object_mesh(void *ptr, const float *P, int nverts, const int *idx, int ntris, const float *N,
+                       const float *uv, int material, int light, int *out_object) {
+    GROUP_FWD(ptr, pm_add_object_mesh(sub, P, nverts, idx, ntris, N, uv, material, light, out_object));
+    GETCTX(ptr);
+    if (!P || !idx || nverts <= 0 || ntris <= 0) FAIL(c, PM_ERR_INVALID, "empty or null object mesh");
+    if (material < 0 || material >= (int)c->materials.size()) FAIL(c, PM_ERR_INVALID, "bad material id %d", material);
+    for (int64_t i = 0; i < 3 * (int64_t)ntris; ++i)
+        if (idx[i] < 0 || idx[i] >= nverts) FAIL(c, PM_ERR_INVALID, "vertex index %d out of range", idx[i]);
+    HObj o;
+    o.P.assign(P, P + 3 * (size_t)nverts);
+    if (N) o.N.assign(N, N + 3 * (size_t)nverts);
+    if (uv) o.UV.assign(uv, uv + 2 * (size_t)nverts);
+    o.idx.assign(idx, idx + 3 * (size_t)ntris);
+    o.material = material; o.light = light; o.has_n = N != nullptr; o.has_uv = uv != nullptr;
+    c->objs.push_back(std::move(o));
+    if (out_object) *out_object = (int)c->objs.size() - 1;
+    c->committed = false;
+    return PM_OK;
+}
+
+int pm_add_mesh_instance(void *ptr, int object, const float o2w[16], const float w2o[16]) {
+    GROUP_FWD(ptr, pm_add_mesh_instance(sub, object, o2w, w2o));
+    GETCTX(ptr);
+    if (object < 0 || object >= (int)c->objs.size()) FAIL(c, PM_ERR_INVALID, "bad object id %d", object);
+    if (!o2w || !w2o) FAIL(c, PM_ERR_INVALID, "null instance transform");
+    if (o2w[12] != 0.f || o2w[13] != 0.f || o2w[14] != 0.f || o2w[15] != 1.f)
+        FAIL(c, PM_ERR_INVALID, "instance transform is not affine (flatten it with pm_add_trimesh)");
+    HInst in;
+    in.obj = object;
+    std::memcpy(in.m, o2w, sizeof in.m);
+    std::memcpy(in.minv, w2o, sizeof in.minv);
+    in.gid_base = c->next_tri_id;
+    c->next_tri_id += (uint32_t)(c->objs[object].idx.size() / 3);
+    c->insts.push_back(in);
+    c->committed = false;
+    return PM_OK;
+}
+
+/* an instance's world vertex as pbrt's Transform::operator()(Point) computes
+ * it for an affine transform (w == 1): the device's inst_point, bit for bit */
+static inline void inst_point_h(const float *m, const float *p, float *o) {
+    for (int a = 0; a < 3; ++a) o[a] = m[4 * a] * p[0] + m[4 * a + 1] * p[1] + m[4 * a + 2] * p[2] + m[4 * a + 3];
 }
 
 int pm_add_sphere(void *ptr, float radius, const float o2w[16], const float w2o[16], int material, int light) {
@@ -987,17 +1049,131 @@ int pm_set_eye_rays(void *ptr, const float *rays, int64_t nrays, const float *ra
     return PM_OK;
 }
 
+/* the object meshes of an instanced scene (two-level trees) */
+struct InstLayout {
+    std::vector<uint32_t> qn;     /* every object's quantized 4-wide nodes, object 0 first (relocated by the caller) */
+    std::vector<float4> insts;    /* 8 per instance (SceneDev::insts) */
+    int max_stack = 0;            /* the deepest object tree's stack bound */
+    size_t o_objv = 0, o_objinfo = 0, o_objn = 0, o_objuv = 0, o_objmesh = 0;
+};
+
+/* quantized 4-wide nodes moved to start at node `base`: internal child codes shift */
+static void relocate_bvh4(std::vector<uint32_t> &q, uint32_t base) {
+    for (size_t nd = 0; nd + 16 <= q.size(); nd += 16)
+        for (int k = 0; k < 4; ++k) {
+            const int16_t cnt = (int16_t)((q[nd + 10 + k / 2] >> (16 * (k & 1))) & 0xffffu);
+            if (cnt == 0) q[nd + 12 + k] += base;
+        }
+}
+
+/* Each object mesh once: its triangles (object space) in the leaf order of
+ * its own binned-SAH tree, collapsed to 4-wide and quantized (every leaf a
+ * LEAF_TRIS run of object slots); the instance records point at them. */
+static int commit_objects(Ctx *c, std::vector<unsigned char> &blob,
+                          const std::function<size_t(const void *, size_t)> &put, InstLayout &IL) {
+    std::vector<float4> objv, objn, objuv;
+    std::vector<int4> objinfo, objmesh;
+    std::vector<uint32_t> root(c->objs.size()), slot0(c->objs.size());
+    std::vector<int> stack(c->objs.size());
+    uint32_t vbase = 0;
+    for (size_t oi = 0; oi < c->objs.size(); ++oi) {
+        const HObj &o = c->objs[oi];
+        const int nt = (int)(o.idx.size() / 3);
+        std::vector<BuildPrim> prims(nt);
+        for (int t = 0; t < nt; ++t) {
+            BuildPrim &bp = prims[t];
+            for (int a = 0; a < 3; ++a) {
+                const float v0 = o.P[3 * o.idx[3 * t] + a], v1 = o.P[3 * o.idx[3 * t + 1] + a], v2 = o.P[3 * o.idx[3 * t + 2] + a];
+                const float lo = std::min(v0, std::min(v1, v2)), hi = std::max(v0, std::max(v1, v2));
+                const float pad = 1e-4f * std::max(1.0f, std::max(fabsf(lo), fabsf(hi)));
+                bp.lo[a] = lo - pad; bp.hi[a] = hi + pad;
+            }
+            bp.ref = (PRIM_TRI << 30) | (uint32_t)t;
+        }
+        BvhOut bvh;
+        build_bvh(prims, BVH_STACK - 2, bvh);
+        Bvh4Out w;
+        collapse_bvh4(bvh, 1, w);
+        /* storage: the tree's leaf order, at global object slots */
+        const uint32_t s0 = (uint32_t)(objv.size() / 3);
+        std::vector<uint32_t> refs(bvh.refs.size());
+        for (size_t k = 0; k < bvh.refs.size(); ++k) {
+            const uint32_t t = bvh.refs[k] & 0x3fffffffu;
+            refs[k] = (PRIM_TRI << 30) | (s0 + (uint32_t)k);
+            for (int q = 0; q < 3; ++q) {
+                const float *v = &o.P[3 * (size_t)o.idx[3 * t + q]];
+                objv.push_back(f4(v[0], v[1], v[2], q == 0 ? ibits((int)t) : 0.f));
+            }
+            objinfo.push_back(make_int4((int)vbase + o.idx[3 * t], (int)vbase + o.idx[3 * t + 1], (int)vbase + o.idx[3 * t + 2],
+                                        (int)oi));
+        }
+        std::vector<uint32_t> qn;
+        if (!quantize_bvh4(w.nodes, refs, qn)) FAIL(c, PM_ERR_INVALID, "object mesh %zu: tree not codable", oi);
+        for (size_t nd = 0; nd + 16 <= qn.size(); nd += 16)
+            for (int k = 0; k < 4; ++k) {
+                const int16_t cnt = (int16_t)((qn[nd + 10 + k / 2] >> (16 * (k & 1))) & 0xffffu);
+                if (cnt > 0 && !(cnt & LEAF_TRIS)) FAIL(c, PM_ERR_INVALID, "object mesh %zu: a leaf is not a triangle run", oi);
+            }
+        const uint32_t at = (uint32_t)(IL.qn.size() / 16);
+        relocate_bvh4(qn, at);
+        root[oi] = at;
+        slot0[oi] = s0;
+        stack[oi] = w.max_stack;
+        IL.max_stack = std::max(IL.max_stack, w.max_stack);
+        IL.qn.insert(IL.qn.end(), qn.begin(), qn.end());
+        const int nv = (int)(o.P.size() / 3);
+        for (int v = 0; v < nv; ++v) {
+            objn.push_back(o.has_n ? f4(o.N[3 * v], o.N[3 * v + 1], o.N[3 * v + 2], 0.f) : f4(0.f, 0.f, 0.f, 0.f));
+            objuv.push_back(o.has_uv ? f4(o.UV[2 * v], o.UV[2 * v + 1], 0.f, 0.f) : f4(0.f, 0.f, 0.f, 0.f));
+        }
+        vbase += (uint32_t)nv;
+        objmesh.push_back(make_int4(o.material, o.light, o.has_n ? 1 : 0, o.has_uv ? 1 : 0));
+    }
+    for (const HInst &in : c->insts) {
+        for (int r = 0; r < 3; ++r) IL.insts.push_back(f4(in.m[4 * r], in.m[4 * r + 1], in.m[4 * r + 2], in.m[4 * r + 3]));
+        for (int r = 0; r < 3; ++r)
+            IL.insts.push_back(f4(in.minv[4 * r], in.minv[4 * r + 1], in.minv[4 * r + 2], in.minv[4 * r + 3]));
+        const int nt = (int)(c->objs[in.obj].idx.size() / 3);
+        IL.insts.push_back(f4(ibits((int)root[in.obj]), ibits((int)slot0[in.obj]), ibits((int)in.gid_base), ibits(nt)));
+        /* blas_isect's box pad, 1e-5 (a (2 |o| + W) + k B): a = |w2o|, W
+         * bounds the world extent by |o2w| B + |translation|, k = |o2w| |w2o|
+         * (infinity norms of the linear parts), B the object's extent */
+        double B = 0.0, nm = 0.0, ni_ = 0.0, tr = 0.0;
+        const std::vector<float> &P = c->objs[in.obj].P;
+        for (float v : P) B = std::max(B, (double)fabsf(v));
+        for (int r = 0; r < 3; ++r) {
+            nm = std::max(nm, fabs(in.m[4 * r]) + fabs(in.m[4 * r + 1]) + fabs(in.m[4 * r + 2]));
+            ni_ = std::max(ni_, fabs(in.minv[4 * r]) + fabs(in.minv[4 * r + 1]) + fabs(in.minv[4 * r + 2]));
+            tr = std::max(tr, (double)fabsf(in.m[4 * r + 3]));
+        }
+        const double W = nm * B + tr;
+        IL.insts.push_back(f4(ibits(stack[in.obj]), (float)(ni_ * 1.001), (float)((ni_ * W + nm * ni_ * B) * 1.001), 0.f));
+    }
+    IL.o_objv = put(objv.data(), objv.size() * sizeof(float4));
+    IL.o_objinfo = put(objinfo.data(), objinfo.size() * sizeof(int4));
+    IL.o_objn = put(objn.data(), objn.size() * sizeof(float4));
+    IL.o_objuv = put(objuv.data(), objuv.size() * sizeof(float4));
+    IL.o_objmesh = put(objmesh.data(), objmesh.size() * sizeof(int4));
+    c->obj_tris_stored = (int64_t)objinfo.size();
+    (void)blob;
+    return PM_OK;
+}
+
 int pm_commit(void *ptr) {
     GROUP_FWD(ptr, pm_commit(sub));
     GETCTX(ptr);
     if (c->lights.empty()) FAIL(c, PM_ERR_INVALID, "scene has no lights");
     const int64_t nt = (int64_t)c->tris.size(), nd = (int64_t)c->disks.size() / 5,
                   ns = (int64_t)c->spheres.size() / 4;
-    if (nt + nd + ns == 0) FAIL(c, PM_ERR_INVALID, "scene has no shapes");
+    if (nt + nd + ns + (int64_t)c->insts.size() == 0) FAIL(c, PM_ERR_INVALID, "scene has no shapes");
     if (nt >= (1 << 30) || nd >= (1 << 30) || ns >= (1 << 30)) FAIL(c, PM_ERR_INVALID, "too many primitives");
-    /* global ids: triangles, then disks, then spheres (tie-break order) */
-    for (int64_t i = 0; i < nd; ++i) c->disks[5 * i + 4].w = ibits((int)(nt + i));
-    for (int64_t i = 0; i < ns; ++i) c->spheres[4 * i + 3].w = ibits((int)(nt + nd + i));
+    /* global ids: triangles (meshes and instances, in insertion order), then
+     * disks, then spheres (tie-break order) */
+    const int64_t nt_ids = (int64_t)c->next_tri_id;
+    if (nt_ids + nd + ns >= (int64_t)1 << 31) FAIL(c, PM_ERR_INVALID, "too many primitives");
+    for (int64_t i = 0; i < nd; ++i) c->disks[5 * i + 4].w = ibits((int)(nt_ids + i));
+    for (int64_t i = 0; i < ns; ++i) c->spheres[4 * i + 3].w = ibits((int)(nt_ids + nd + i));
+    const int64_t ni = (int64_t)c->insts.size();
 
     const auto t_commit0 = std::chrono::steady_clock::now();
     std::vector<BuildPrim> prims(nt);
@@ -1057,6 +1233,18 @@ int pm_commit(void *ptr) {
         }
         add_box(lo, hi, (PRIM_SPHERE << 30) | (uint32_t)i);
     }
+    /* instances: the box of the world vertices the device rebuilds */
+    for (int64_t i = 0; i < ni; ++i) {
+        const HInst &in = c->insts[i];
+        const HObj &o = c->objs[in.obj];
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int v : o.idx) {
+            float w[3];
+            inst_point_h(in.m, &o.P[3 * (size_t)v], w);
+            for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], w[a]); hi[a] = std::max(hi[a], w[a]); }
+        }
+        add_box(lo, hi, (PRIM_INST << 30) | (uint32_t)i);
+    }
     /* env PM_COMMIT_TIMES=1: the build's phases on stderr (setup-time study) */
     const bool ptimes = getenv("PM_COMMIT_TIMES") != nullptr;
     auto tnow = [] { return std::chrono::steady_clock::now(); };
@@ -1066,7 +1254,7 @@ int pm_commit(void *ptr) {
     SceneLayout L;
     int rc;
     bool built = false;
-    if (gpu_bvh_wanted((int64_t)prims.size())) {
+    if (ni == 0 && gpu_bvh_wanted((int64_t)prims.size())) {
         if ((rc = commit_gpu_bvh(c, prims, nt, L, built, ptimes))) return rc;
         if (ptimes && built) fprintf(stderr, "pm_commit: device build, total %.1f ms\n", tms(t_commit0, tnow()));
     }
@@ -1093,7 +1281,7 @@ int pm_commit(void *ptr) {
         /* tiny LDS scenes skip the BVH (MODE_BRUTE). Their triangles are stored
          * in global-id order (brute_isect's tie-break relies on it), others in
          * leaf order. */
-        const bool id_order = (int64_t)bvh.refs.size() <= BRUTE_MAX_PRIMS;
+        const bool id_order = ni == 0 && (int64_t)bvh.refs.size() <= BRUTE_MAX_PRIMS;
         std::vector<uint32_t> tri_order; /* triangle ids in storage order */
         tri_order.reserve(nt);
         if (id_order) {
@@ -1120,7 +1308,7 @@ int pm_commit(void *ptr) {
         parallel_for(nst, [&](int64_t k0, int64_t k1) {
             for (int64_t k = k0; k < k1; ++k) {
                 tri_record(c, tri_order[k], &tri_geo[3 * k], &tri_shade[2 * k], &tri_info[k]);
-                tri_id[k] = tri_order[k];
+                tri_id[k] = c->tris[tri_order[k]].gid;
             }
         });
         if (ptimes) fprintf(stderr, "pm_commit: triangle records done at %.1f ms\n", tms(t_commit0, tnow()));
@@ -1153,9 +1341,13 @@ int pm_commit(void *ptr) {
         L.o_spheres = put(c->spheres.data(), c->spheres.size() * sizeof(float4));
         L.o_mats = put(c->materials.data(), c->materials.size() * sizeof(float4));
         L.o_lights = put(c->lights.data(), c->lights.size() * sizeof(LightDev));
+        /* instances: each object mesh's own tree and object-space triangles */
+        InstLayout IL;
+        if (ni > 0 && (rc = commit_objects(c, blob, put, IL))) return rc;
         /* scenes traversed from HBM also get the 4-wide BVH (half the dependent
-         * node fetches per ray; binary leaves of one primitive) */
-        if (blob.size() > LDS_SCENE_MAX) {
+         * node fetches per ray; binary leaves of one primitive);
+         * instanced scenes always (their objects' trees are 4-wide) */
+        if (blob.size() > LDS_SCENE_MAX || ni > 0) {
             {
                 Bvh4Out w;
                 const auto t_c0 = tnow();
@@ -1174,17 +1366,31 @@ int pm_commit(void *ptr) {
                 const auto t_q0 = tnow();
                 const bool coded = !quant || quantize_bvh4(w.nodes, bvh.refs, qn);
                 if (ptimes) fprintf(stderr, "pm_commit: quantize %.1f ms\n", tms(t_q0, tnow()));
+                if (ni > 0 && !(coded && quant && w.max_stack + IL.max_stack + 1 <= BVH_STACK))
+                    FAIL(c, PM_ERR_INVALID, "instanced scene: top-level tree not codable (stack %d + %d)", w.max_stack,
+                         IL.max_stack);
                 if (coded && w.max_stack <= BVH_STACK) {
+                    if (ni > 0) { /* the objects' nodes follow the top-level tree's */
+                        const uint32_t top = (uint32_t)(qn.size() / 16);
+                        relocate_bvh4(IL.qn, top);
+                        for (int64_t i = 0; i < ni; ++i) IL.insts[8 * i + 6].x = ibits(fbits_h(IL.insts[8 * i + 6].x) + (int)top);
+                        qn.insert(qn.end(), IL.qn.begin(), IL.qn.end());
+                        L.o_insts = put(IL.insts.data(), IL.insts.size() * sizeof(float4));
+                    }
                     L.o_wnodes = quant ? put(qn.data(), qn.size() * sizeof(uint32_t))
                                        : put(w.nodes.data(), w.nodes.size() * sizeof(float));
                     L.wide = quant ? 2 : 1;
-                    L.wide_stack = w.max_stack;
-                    c->bvh4_nodes = (int64_t)(w.nodes.size() / 32);
+                    L.wide_stack = w.max_stack + (ni > 0 ? IL.max_stack : 0);
+                    c->bvh4_nodes = (int64_t)(quant ? qn.size() / 16 : w.nodes.size() / 32);
                     c->bvh4_depth = w.depth;
                 }
             }
         }
         blob.resize(std::max<size_t>((blob.size() + 15) & ~(size_t)15, 16), 0);
+        /* instanced scenes never go LDS-resident (MODE_INST walks the 4-wide trees from HBM) */
+        if (ni > 0 && blob.size() <= LDS_SCENE_MAX) blob.resize(LDS_SCENE_MAX + 16, 0);
+        L.o_objv = IL.o_objv; L.o_objinfo = IL.o_objinfo; L.o_objn = IL.o_objn; L.o_objuv = IL.o_objuv;
+        L.o_objmesh = IL.o_objmesh;
         const auto t_u0 = tnow();
         if ((rc = upload(c, c->d_scene, blob))) return rc;
         if (id_order) {
@@ -1204,6 +1410,8 @@ int pm_commit(void *ptr) {
                             tms(t_commit0, tnow()));
         L.bytes = blob.size();
         L.n_nodes = (int64_t)nodes4.size() / 4;
+        /* the traversal loops' guard: with instances it must cover an object's tree too */
+        if (ni > 0) L.n_nodes = std::max<int64_t>(L.n_nodes, c->bvh4_nodes);
         L.n_refs = (int64_t)bvh.refs.size();
         L.n_tris = (int64_t)tri_info.size();
         L.id_order = id_order;
@@ -1225,6 +1433,13 @@ int pm_commit(void *ptr) {
     S.n_tris = (int)L.n_tris; S.n_disks = (int)nd; S.n_spheres = (int)ns;
     S.tri_geo_g = S.tri_geo; S.tri_id_g = S.tri_id;
     S.tri_pairs_g = L.id_order ? c->d_tripairs.as<float>() : nullptr;
+    S.n_inst = (int)ni;
+    S.insts = ni ? (const float4 *)(base + L.o_insts) : nullptr;
+    S.obj_v = ni ? (const float4 *)(base + L.o_objv) : nullptr;
+    S.obj_info = ni ? (const int4 *)(base + L.o_objinfo) : nullptr;
+    S.obj_n = ni ? (const float4 *)(base + L.o_objn) : nullptr;
+    S.obj_uv = ni ? (const float4 *)(base + L.o_objuv) : nullptr;
+    S.obj_mesh = ni ? (const int4 *)(base + L.o_objmesh) : nullptr;
     S.brute = (S.lds_bytes > 0 && L.id_order) ? 1 : 0;
     /* a push happens only when descending a level, so depth + 1 entries suffice;
      * sizing the LDS stack by the actual tree keeps occupancy VGPR-bound */
@@ -1472,7 +1687,7 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
         const int64_t waves = (int64_t)cus * (per_cu > 0 ? per_cu : 16);
         /* any pool size works (the wave's cursor hands out paths to dead lanes) */
         const int64_t per = std::max<int64_t>(1, (path_count + waves - 1) / waves);
-        T.pool_paths = per;
+        T.pool_paths = c->trace_pool ? per : 0;
         if (lstk < c->S.stack_depth) {
             const int64_t blocks = ((path_count + per - 1) / per + TRACE_BLOCK / 64 - 1) / (TRACE_BLOCK / 64);
             const int64_t threads = blocks * TRACE_BLOCK;
@@ -2328,12 +2543,13 @@ int pm_scene_info(void *ptr, int64_t out[7]) {
     GETCTX(ptr);
     if (!c->S.blob) FAIL(c, PM_ERR_INVALID, "no scene committed");
     const SceneDev &S = c->S;
-    out[0] = S.n_tris; out[1] = S.n_disks; out[2] = S.n_spheres;
+    out[0] = c->next_tri_id;   /* triangles rendered: meshes + every instance's */
+    out[1] = S.n_disks; out[2] = S.n_spheres;
     /* the tree the kernels traverse: the 4-wide BVH when the scene has one
      * (either builder), else the binary SAH tree */
     out[3] = S.wide ? c->bvh4_nodes : S.n_nodes;
     out[4] = S.wide ? c->bvh4_depth : c->bvh_depth;
-    out[5] = scene_mode(S) == MODE_BRUTE ? 2 : scene_mode(S) == MODE_LDS ? 1 : 0;
+    out[5] = scene_mode(S) == MODE_BRUTE ? 2 : scene_mode(S) == MODE_LDS ? 1 : scene_mode(S) == MODE_INST ? 3 : 0;
     out[6] = S.blob_bytes;
     return PM_OK;
 }
@@ -2352,6 +2568,8 @@ int pm_scene_section(void *ptr, int section, void *out, int64_t max_bytes, int64
     case PM_SCENE_TRI_ID: src = S.tri_id; n = 4 * (int64_t)S.n_tris; break;
     case PM_SCENE_TRI_INFO: src = S.tri_info; n = 16 * (int64_t)S.n_tris; break;
     case PM_SCENE_BVH4: src = S.wnodes; n = S.wide ? (S.wide == 2 ? 64 : 128) * c->bvh4_nodes : 0; break;
+    case PM_SCENE_INSTANCES: src = S.insts; n = 128 * (int64_t)S.n_inst; break;
+    case PM_SCENE_OBJ_TRIS: src = S.obj_v; n = S.n_inst ? 48 * c->obj_tris_stored : 0; break;
     default: FAIL(c, PM_ERR_INVALID, "unknown scene section %d", section);
     }
     if (bytes) *bytes = n;

@@ -57,7 +57,10 @@ constexpr float RT_DEFAULT_MAX = 1.e27f;
 
 /* ---------------------------------------------------------- scene layout */
 /* prim ref = (kind << 30) | index */
-enum : uint32_t { PRIM_TRI = 0u, PRIM_DISK = 1u, PRIM_SPHERE = 2u };
+/* PRIM_INST: an object instance (pm_add_mesh_instance) in the top-level
+ * tree; a hit on one of its triangles carries (PRIM_INST << 30) | the
+ * object triangle's storage slot, and the triangle's global id */
+enum : uint32_t { PRIM_TRI = 0u, PRIM_DISK = 1u, PRIM_SPHERE = 2u, PRIM_INST = 3u };
 
 struct LightDev {      /* CudaLightDevice (common.cu.h:47-59), 80 B */
     float4 o_type;     /* o.xyz, type (int bits) */
@@ -103,6 +106,25 @@ struct SceneDev {
      * for the LDS modes */
     const float4 *wnodes;
     int wide;        /* 4-wide BVH in wnodes: 1 = 128-B float nodes, 2 = 64-B quantized (pm_build.h) */
+    /* two-level instancing (pm_add_object_mesh / pm_add_mesh_instance): each
+     * object mesh is stored once, in object space, with its own quantized
+     * 4-wide tree in wnodes; the top-level tree's instance leaves (PRIM_INST
+     * refs) enter it. Per instance 8 float4 (inst_*): the object-to-world
+     * rows m[0..11], the world-to-object rows minv[0..11] (pbrt Transform's
+     * m and mInv), then (tree root, first object slot, first global id,
+     * triangles) and (tree stack bound, 0, 0, 0) as ints. Per object slot:
+     * obj_v 3 float4 (object-space p0, p1, p2; p0.w = the triangle's index
+     * in its mesh), obj_info (vertex ids into obj_n / obj_uv, mesh). A
+     * triangle is intersected and shaded in world space from its vertices
+     * transformed exactly as pbrt's Transform does (Transform::operator()),
+     * so every hit equals the hit of the instance flattened to world space. */
+    const float4 *insts;
+    const float4 *obj_v;
+    const int4 *obj_info;
+    const float4 *obj_n;  /* object vertex normals (xyz) */
+    const float4 *obj_uv; /* object vertex uvs (xy) */
+    const int4 *obj_mesh; /* per object mesh: material, light, has_n, has_uv */
+    int n_inst;
     /* all arrays above are 16-B aligned sections of one blob in HBM */
     const char *blob;
     uint32_t blob_bytes;
@@ -117,7 +139,9 @@ constexpr uint32_t LDS_SCENE_MAX = 16384;
 constexpr int BRUTE_MAX_PRIMS = 64;
 
 /* how the kernels see the scene (template argument of the traversal kernels) */
-enum SceneMode : int { MODE_GLOBAL = 0, MODE_LDS = 1, MODE_BRUTE = 2 };
+enum SceneMode : int { MODE_GLOBAL = 0, MODE_LDS = 1, MODE_BRUTE = 2, MODE_INST = 3 };
+/* MODE_INST: a MODE_GLOBAL scene with object instances (two-level 4-wide trees) */
+constexpr bool mode_lds(int mode) { return mode == MODE_LDS || mode == MODE_BRUTE; }
 
 struct Ray { v3 o, d; float tmin, tmax; };
 
@@ -321,14 +345,21 @@ PMD bool isect_sphere(const float4 *s, const Ray &ray, float *thit) {
  * ray). The slab test only culls: its error is about one ulp of the
  * coordinates, and every primitive box is padded by 1e-4 of its coordinate
  * magnitude at commit (thousands of ulps), so no box holding a hit is culled. */
+/* slab test; oinvH (default oinv) offsets the high planes: an instance tree
+ * widens every box by a pad with oinv = (o' + pad) * inv, oinvH = (o' - pad)
+ * * inv at no cost per box (blas_isect) */
 PMD float box_near(float lx, float ly, float lz, float hx, float hy, float hz, v3 oinv, v3 inv, float tmin,
-                   float tmax) {
-    float t0x = __builtin_fmaf(lx, inv.x, -oinv.x), t1x = __builtin_fmaf(hx, inv.x, -oinv.x);
-    float t0y = __builtin_fmaf(ly, inv.y, -oinv.y), t1y = __builtin_fmaf(hy, inv.y, -oinv.y);
-    float t0z = __builtin_fmaf(lz, inv.z, -oinv.z), t1z = __builtin_fmaf(hz, inv.z, -oinv.z);
+                   float tmax, v3 oinvH) {
+    float t0x = __builtin_fmaf(lx, inv.x, -oinv.x), t1x = __builtin_fmaf(hx, inv.x, -oinvH.x);
+    float t0y = __builtin_fmaf(ly, inv.y, -oinv.y), t1y = __builtin_fmaf(hy, inv.y, -oinvH.y);
+    float t0z = __builtin_fmaf(lz, inv.z, -oinv.z), t1z = __builtin_fmaf(hz, inv.z, -oinvH.z);
     float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
     float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), tmax));
     return tn <= tf ? tn : __int_as_float(0x7f800000);
+}
+PMD float box_near(float lx, float ly, float lz, float hx, float hy, float hz, v3 oinv, v3 inv, float tmin,
+                   float tmax) {
+    return box_near(lx, ly, lz, hx, hy, hz, oinv, inv, tmin, tmax, oinv);
 }
 
 PMD v3 safe_inv(v3 d) {
@@ -487,8 +518,14 @@ PMD bool brute_isect(const SceneDev &S, const Ray &ray, Hit &best, C &cen) {
  * TRIRUN: the leaf comes from a quantized 4-wide node, whose count may carry
  * pm_build.h's LEAF_TRIS flag (only quantize_bvh4 sets it; binary and float
  * 4-wide leaves are always decoded through their refs, whatever their size). */
-template <bool ANY, bool TRIRUN = false, class C>
-PMD bool leaf_isect(const SceneDev &S, uint32_t start, uint32_t count, const Ray &ray, Hit &best, C &cen) {
+template <bool ANY, class C>
+PMD bool blas_isect(const SceneDev &S, uint32_t inst, const Ray &ray, const v3 &oinv, const v3 &inv, Hit &best,
+                    int *stack, int stride, C &cen);
+/* INST: the leaf's refs may be instances (MODE_INST), whose trees are walked
+ * with the stack entries above the caller's (stack, stride) */
+template <bool ANY, bool TRIRUN = false, class C, bool INST = false>
+PMD bool leaf_isect(const SceneDev &S, uint32_t start, uint32_t count, const Ray &ray, Hit &best, C &cen,
+                    int *istack = nullptr, int istride = 0, const v3 *oinv = nullptr, const v3 *inv = nullptr) {
     if (TRIRUN && (count & 0x4000u)) { /* LEAF_TRIS: triangles at storage slots [start, start + n), no refs */
         for (uint32_t idx = start; idx < start + (count & 0x3fffu); ++idx) {
             cen.prim();
@@ -510,6 +547,10 @@ PMD bool leaf_isect(const SceneDev &S, uint32_t start, uint32_t count, const Ray
         float t, b = 0.f, g = 0.f;
         bool ok;
         uint32_t gid;
+        if (INST && kind == PRIM_INST) {
+            if (blas_isect<ANY>(S, idx, ray, *oinv, *inv, best, istack, istride, cen) && ANY) return true;
+            continue;
+        }
         if (kind == PRIM_TRI) {
             ok = isect_tri(S.tri_geo + 3 * idx, ray, &t, &b, &g);
             if (ANY) { if (ok) return true; continue; }
@@ -537,7 +578,7 @@ PMD bool leaf_isect(const SceneDev &S, uint32_t start, uint32_t count, const Ray
  * Closest hit (ANY=false) or occlusion (ANY=true). Node = 4 float4:
  * (l.lo, l.hi.x) (l.hi.yz, r.lo.xy) (r.lo.z, r.hi) (left, right, lcount, rcount);
  * child >= 0 internal node, child < 0 leaf with refs start ~child. */
-template <bool ANY, class C>
+template <bool ANY, class C, bool INST = false>
 PMD bool traverse4(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int stride, C &cen);
 
 template <bool ANY, int MODE, class C>
@@ -559,7 +600,9 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
         if (brute_isect<ANY>(S, ray, best, cen)) return true;
         return ANY ? false : best.ref != 0xffffffffu;
     }
-    if constexpr (MODE == MODE_GLOBAL) {
+    if constexpr (MODE == MODE_INST) {
+        return traverse4<ANY, C, true>(S, ray, best, stack, stride, cen);
+    } else if constexpr (MODE == MODE_GLOBAL) {
         if (S.wide) return traverse4<ANY>(S, ray, best, stack, stride, cen);
     }
     uint32_t l0s = 0, l0n = 0, l1s = 0, l1n = 0; /* pending leaves: first ref, count (0 = none) */
@@ -616,7 +659,7 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
 #define PM_BVH4_QUANT 1 /* build-time node format: 1 = quantized 64-B nodes, 0 = 128-B float nodes */
 #endif
 PMD void node4_test(const SceneDev &S, int cur, const v3 &oinv, const v3 &inv, float tmin, float tmax, float t[4],
-                    int c[4], int n[4]) {
+                    int c[4], int n[4], const v3 &oinvH) {
     if (PM_BVH4_QUANT) {
         const uint4 *nd = reinterpret_cast<const uint4 *>(S.wnodes) + 4 * cur;
         const uint4 w0 = nd[0], w1 = nd[1], w2 = nd[2], w3 = nd[3];
@@ -638,7 +681,7 @@ PMD void node4_test(const SceneDev &S, int cur, const v3 &oinv, const v3 &inv, f
             const float lx = QDEC(ox, (float)((w1.x >> sh) & 0xffu), sx), ly = QDEC(oy, (float)((w1.y >> sh) & 0xffu), sy);
             const float lz = QDEC(oz, (float)((w1.z >> sh) & 0xffu), sz), hx = QDEC(ox, (float)((w1.w >> sh) & 0xffu), sx);
             const float hy = QDEC(oy, (float)((w2.x >> sh) & 0xffu), sy), hz = QDEC(oz, (float)((w2.y >> sh) & 0xffu), sz);
-            t[k] = box_near(lx, ly, lz, hx, hy, hz, oinv, inv, tmin, tmax);
+            t[k] = box_near(lx, ly, lz, hx, hy, hz, oinv, inv, tmin, tmax, oinvH);
         }
         c[0] = (int)w3.x; c[1] = (int)w3.y; c[2] = (int)w3.z; c[3] = (int)w3.w;
         n[0] = (int)(int16_t)(w2.z & 0xffffu); n[1] = (int)(int16_t)(w2.z >> 16);
@@ -648,13 +691,17 @@ PMD void node4_test(const SceneDev &S, int cur, const v3 &oinv, const v3 &inv, f
         const float4 *nd = S.wnodes + 8 * cur;
         const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
         const int4 ch = *reinterpret_cast<const int4 *>(nd + 6), cn = *reinterpret_cast<const int4 *>(nd + 7);
-        t[0] = box_near(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, oinv, inv, tmin, tmax);
-        t[1] = box_near(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, oinv, inv, tmin, tmax);
-        t[2] = box_near(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, oinv, inv, tmin, tmax);
-        t[3] = box_near(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, oinv, inv, tmin, tmax);
+        t[0] = box_near(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, oinv, inv, tmin, tmax, oinvH);
+        t[1] = box_near(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, oinv, inv, tmin, tmax, oinvH);
+        t[2] = box_near(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, oinv, inv, tmin, tmax, oinvH);
+        t[3] = box_near(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, oinv, inv, tmin, tmax, oinvH);
         c[0] = ch.x; c[1] = ch.y; c[2] = ch.z; c[3] = ch.w;
         n[0] = cn.x; n[1] = cn.y; n[2] = cn.z; n[3] = cn.w;
     }
+}
+PMD void node4_test(const SceneDev &S, int cur, const v3 &oinv, const v3 &inv, float tmin, float tmax, float t[4],
+                    int c[4], int n[4]) {
+    node4_test(S, cur, oinv, inv, tmin, tmax, t, c, n, oinv);
 }
 
 /* 4-wide traversal (MODE_GLOBAL scenes with S.wide): one 128-B node per
@@ -662,7 +709,7 @@ PMD void node4_test(const SceneDev &S, int cur, const v3 &oinv, const v3 &inv, f
  * near to far with a sorting network, the nearest entered next and the rest
  * pushed (the stack is sized by the builder's max_stack); hit leaves are
  * postponed and tested together as in traverse() (at most four per node). */
-template <bool ANY, class C>
+template <bool ANY, class C, bool INST>
 PMD bool traverse4(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int stride, C &cen) {
     best.t = ray.tmax;
     best.gid = 0xffffffffu;
@@ -705,12 +752,119 @@ PMD bool traverse4(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int
             else cur = -1;
         }
         while (l0n != 0) {
-            if (leaf_isect<ANY, PM_BVH4_QUANT != 0>(S, l0s, l0n, ray, best, cen)) return true;
+            /* instance trees use the stack entries above the ones in use */
+            if (leaf_isect<ANY, PM_BVH4_QUANT != 0, C, INST>(S, l0s, l0n, ray, best, cen, stack + sp * stride, stride,
+                                                             &oinv, &inv))
+                return true;
             l0s = l1s; l0n = l1n; l1s = l2s; l1n = l2n; l2s = l3s; l2n = l3n; l3n = 0;
         }
         if (cur < 0 || guard > S.n_nodes) break;
     }
     return ANY ? false : best.ref != 0xffffffffu;
+}
+
+/* ------------------------------------------------------ instance trees */
+/* pbrt Transform::operator()(Point) for an affine transform (its w row is
+ * (0, 0, 0, 1), checked at pm_add_mesh_instance, so w == 1 and no divide):
+ * the host's flattening evaluates m[0] * x + m[1] * y + m[2] * z + m[3]
+ * left to right — the same IEEE operations, in the same order */
+PMD v3 inst_point(const float4 *m, float x, float y, float z) {
+    const float4 r0 = m[0], r1 = m[1], r2 = m[2];
+    return mk(((r0.x * x + r0.y * y) + r0.z * z) + r0.w, ((r1.x * x + r1.y * y) + r1.z * z) + r1.w,
+              ((r2.x * x + r2.y * y) + r2.z * z) + r2.w);
+}
+/* object slot k of instance record I as the world triangle pm_commit would
+ * have stored for the flattened mesh (tri_record: p0, e0 = p1 - p0,
+ * e1 = p0 - p2, n = e1 x e0) */
+PMD void inst_tri(const SceneDev &S, const float4 *I, uint32_t k, v3 &p0, v3 &p1, v3 &p2, float4 g[3]) {
+    const float4 a = S.obj_v[3 * k], b = S.obj_v[3 * k + 1], c = S.obj_v[3 * k + 2];
+    p0 = inst_point(I, a.x, a.y, a.z);
+    p1 = inst_point(I, b.x, b.y, b.z);
+    p2 = inst_point(I, c.x, c.y, c.z);
+    const v3 e0 = p1 - p0, e1 = p0 - p2;
+    const v3 n = mk(e1.y * e0.z - e1.z * e0.y, e1.z * e0.x - e1.x * e0.z, e1.x * e0.y - e1.y * e0.x);
+    g[0] = make_float4(p0.x, p0.y, p0.z, e0.x);
+    g[1] = make_float4(e0.y, e0.z, e1.x, e1.y);
+    g[2] = make_float4(e1.z, n.x, n.y, n.z);
+}
+/* the instance record holding global triangle id gid (records ascend by id) */
+PMD uint32_t inst_of_gid(const SceneDev &S, uint32_t gid) {
+    uint32_t lo = 0, hi = (uint32_t)S.n_inst - 1u;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1u) >> 1;
+        if ((uint32_t)__float_as_int(S.insts[8 * mid + 6].z) <= gid) lo = mid;
+        else hi = mid - 1u;
+    }
+    return lo;
+}
+/* Closest hit (or any hit) among an instance's triangles. The object tree
+ * is walked in object space: the ray taken through w2o (o' = w2o o, d' =
+ * w2o d; the same t parameterises both, the transform being affine) and
+ * every box widened by pad = 1e-5 (a (2 |o| + W) + k B), a = |w2o| (row
+ * sums), W the instance's world extent, k = |o2w| |w2o|, B the object's
+ * extent (both per instance, I[7]) — beyond the rounding of o', d' and of
+ * the world vertices mapped back (~3 ulps of those magnitudes), so culling
+ * is conservative: every triangle that can win is tested. Triangles are
+ * rebuilt in world space (inst_tri) and tested with the world ray like a
+ * flattened mesh's, so hits equal the flattened scene's bit for bit. The
+ * stack entries above the caller's hold the walk (collapse_bvh4's bound). */
+template <bool ANY, class C>
+PMD bool blas_isect(const SceneDev &S, uint32_t inst, const Ray &ray, const v3 &, const v3 &, Hit &best,
+                    int *stack, int stride, C &cen) {
+    const float4 *I = S.insts + 8 * inst;
+    const float4 hd = I[6], pk = I[7];
+    const uint32_t gid0 = (uint32_t)__float_as_int(hd.z);
+    const float4 w0 = I[3], w1 = I[4], w2 = I[5];
+    const v3 o = inst_point(I + 3, ray.o.x, ray.o.y, ray.o.z);
+    const v3 d = mk((w0.x * ray.d.x + w0.y * ray.d.y) + w0.z * ray.d.z, (w1.x * ray.d.x + w1.y * ray.d.y) + w1.z * ray.d.z,
+                    (w2.x * ray.d.x + w2.y * ray.d.y) + w2.z * ray.d.z);
+    const float on = fmaxf(fabsf(ray.o.x), fmaxf(fabsf(ray.o.y), fabsf(ray.o.z)));
+    const float pad = 1e-5f * (pk.y * (2.f * on) + pk.z);
+    const v3 inv = safe_inv(d);
+    const v3 oL = mk((o.x + pad) * inv.x, (o.y + pad) * inv.y, (o.z + pad) * inv.z);
+    const v3 oH = mk((o.x - pad) * inv.x, (o.y - pad) * inv.y, (o.z - pad) * inv.z);
+    const float INF = __int_as_float(0x7f800000);
+    int sp = 0, cur = __float_as_int(hd.x), guard = 0;
+    while (cur >= 0 && guard <= S.n_nodes) {
+        ++guard;
+        cen.node();
+        float t[4];
+        int c[4], n[4];
+        node4_test(S, cur, oL, inv, ray.tmin, best.t, t, c, n, oH);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (t[k] == INF || n[k] <= 0) continue;
+            /* a leaf: its triangles at object slots [~c, ~c + count) (LEAF_TRIS) */
+            const uint32_t s0 = (uint32_t)~c[k], cnt = (uint32_t)n[k] & 0x3fffu;
+            for (uint32_t q = s0; q < s0 + cnt; ++q) {
+                cen.prim();
+                v3 p0, p1, p2;
+                float4 g[3];
+                inst_tri(S, I, q, p0, p1, p2, g);
+                float tt, bb, gg;
+                const bool ok = isect_tri_v(g[0], g[1], g[2], ray, &tt, &bb, &gg);
+                if (ANY) { if (ok) return true; continue; }
+                if (!ok || tt > best.t) continue;
+                const uint32_t gid = gid0 + (uint32_t)__float_as_int(S.obj_v[3 * q].w);
+                if (tt < best.t || gid < best.gid) {
+                    best.t = tt; best.beta = bb; best.gamma = gg; best.ref = (PRIM_INST << 30) | q; best.gid = gid;
+                }
+            }
+            t[k] = INF;
+        }
+        /* internal children: nearest next, the others pushed */
+        auto cs = [&](int a, int b) {
+            if (t[b] < t[a]) { const float tt = t[a]; t[a] = t[b]; t[b] = tt; const int cc = c[a]; c[a] = c[b]; c[b] = cc; }
+        };
+        cs(0, 1); cs(2, 3); cs(0, 2); cs(1, 3); cs(1, 2);
+        if (t[3] != INF) { stack[sp * stride] = c[3]; ++sp; }
+        if (t[2] != INF) { stack[sp * stride] = c[2]; ++sp; }
+        if (t[1] != INF) { stack[sp * stride] = c[1]; ++sp; }
+        if (t[0] != INF) cur = c[0];
+        else if (sp > 0) { --sp; cur = stack[sp * stride]; }
+        else cur = -1;
+    }
+    return false;
 }
 
 /* Resumable closest-hit traversal of the 4-wide BVH for kernels that keep a
@@ -817,6 +971,48 @@ PMD Geo shade(const SceneDev &S, const Ray &ray, const Hit &h) {
     Geo g;
     uint32_t kind = h.ref >> 30, idx = h.ref & 0x3fffffffu;
     v3 nsw, dpduw;
+    if (kind == PRIM_INST) { /* an instance's triangle: the flattened triangle's frame, rebuilt */
+        const float4 *I = S.insts + 8 * inst_of_gid(S, h.gid);
+        v3 p0, p1, p2;
+        float4 gg[3];
+        inst_tri(S, I, idx, p0, p1, p2, gg);
+        const v3 n = mk(gg[2].y, gg[2].z, gg[2].w);
+        const int4 vi = S.obj_info[idx];
+        const int4 mi = S.obj_mesh[vi.w];
+        g.material = mi.x; g.light = mi.y;
+        /* tri_frame (pm_api.cpp): dp/du from the uvs (cudatrianglemesh.cu:49-58) */
+        float uv0x = 0.f, uv0y = 0.f, uv1x = 1.f, uv1y = 0.f, uv2x = 0.f, uv2y = 1.f;
+        if (mi.w) {
+            const float4 a = S.obj_uv[vi.x], b = S.obj_uv[vi.y], c = S.obj_uv[vi.z];
+            uv0x = a.x; uv0y = a.y; uv1x = b.x; uv1y = b.y; uv2x = c.x; uv2y = c.y;
+        }
+        const float du1 = uv0x - uv2x, du2 = uv1x - uv2x, dv1 = uv0y - uv2y, dv2 = uv1y - uv2y;
+        const float det = du1 * dv2 - dv1 * du2;
+        v3 d;
+        if (det == 0.0f) {
+            if (fabsf(n.x) > fabsf(n.y)) {
+                const float il = rcp_exact(sqrtf(n.x * n.x + n.z * n.z));
+                d = mk(-n.z * il, 0.f, n.x * il);
+            } else {
+                const float il = rcp_exact(sqrtf(n.y * n.y + n.z * n.z));
+                d = mk(0.f, n.z * il, n.y * il);
+            }
+        } else {
+            const float invdet = rcp_exact(det);
+            const v3 dp1 = p0 - p2, dp2 = p1 - p2;
+            d = mk((dv2 * dp1.x - dv1 * dp2.x) * invdet, (dv2 * dp1.y - dv1 * dp2.y) * invdet,
+                   (dv2 * dp1.z - dv1 * dp2.z) * invdet);
+        }
+        g.dpdu = normalize(d);
+        if (!mi.z) { g.ns = normalize(n); return g; }
+        /* vertex normals through pbrt's Transform::operator()(Normal) (transpose
+         * of mInv), then interpolated per hit as for a flattened mesh */
+        const float4 *W = I + 3;
+        const v3 n0 = xform_normal(W, xyz(S.obj_n[vi.x])), n1 = xform_normal(W, xyz(S.obj_n[vi.y])),
+                 n2 = xform_normal(W, xyz(S.obj_n[vi.z]));
+        g.ns = normalize(n1 * h.beta + n2 * h.gamma + n0 * (1.0f - h.beta - h.gamma));
+        return g;
+    }
     if (kind == PRIM_TRI) {
         /* per-triangle frame (cudatrianglemesh.cu:36-78 + normalize), see tri_shade */
         const float4 s0 = S.tri_shade[2 * idx], s1 = S.tri_shade[2 * idx + 1];

@@ -219,7 +219,9 @@ struct FinalParams {
 };
 
 /* traversal mode of a scene: LDS-resident blob (brute force when tiny) or HBM */
-inline int scene_mode(const SceneDev &S) { return S.lds_bytes ? (S.brute ? MODE_BRUTE : MODE_LDS) : MODE_GLOBAL; }
+inline int scene_mode(const SceneDev &S) {
+    return S.n_inst > 0 ? MODE_INST : S.lds_bytes ? (S.brute ? MODE_BRUTE : MODE_LDS) : MODE_GLOBAL;
+}
 
 hipError_t launch_eye(const EyeParams &p, hipStream_t s);
 /* simple renderer (simplerender.cu): direct light per eye sample into out

@@ -24,9 +24,9 @@ template <int MODE>
 __global__ __launch_bounds__(EYE_BLOCK) void k_eye(EyeParams P) {
     extern __shared__ __attribute__((aligned(16))) int stk[]; /* [stack_depth x EYE_BLOCK][scene blob (LDS)] */
     int *stack = stk + threadIdx.x;
-    const SceneDev S = scene_view<MODE != MODE_GLOBAL>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * EYE_BLOCK),
+    const SceneDev S = scene_view<mode_lds(MODE)>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * EYE_BLOCK),
                                                        threadIdx.x, EYE_BLOCK);
-    if (MODE != MODE_GLOBAL) __syncthreads();
+    if (mode_lds(MODE)) __syncthreads();
     const int64_t r = (int64_t)blockIdx.x * EYE_BLOCK + threadIdx.x;
     if (r >= P.R.count) return;
 
@@ -135,6 +135,7 @@ hipError_t launch_eye(const EyeParams &p, hipStream_t s) {
     switch (scene_mode(p.S)) {
     case MODE_BRUTE: pm_launch(k_eye<MODE_BRUTE>, dim3(grid), dim3(EYE_BLOCK), lds, s, p); break;
     case MODE_LDS: pm_launch(k_eye<MODE_LDS>, dim3(grid), dim3(EYE_BLOCK), lds, s, p); break;
+    case MODE_INST: pm_launch(k_eye<MODE_INST>, dim3(grid), dim3(EYE_BLOCK), lds, s, p); break;
     default: pm_launch(k_eye<MODE_GLOBAL>, dim3(grid), dim3(EYE_BLOCK), lds, s, p); break;
     }
     return hipGetLastError();
@@ -153,9 +154,9 @@ template <int MODE>
 __global__ __launch_bounds__(EYE_BLOCK) void k_simple(EyeParams P, float *out) {
     extern __shared__ __attribute__((aligned(16))) int stk[];
     int *stack = stk + threadIdx.x;
-    const SceneDev S = scene_view<MODE != MODE_GLOBAL>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * EYE_BLOCK),
+    const SceneDev S = scene_view<mode_lds(MODE)>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * EYE_BLOCK),
                                                        threadIdx.x, EYE_BLOCK);
-    if (MODE != MODE_GLOBAL) __syncthreads();
+    if (mode_lds(MODE)) __syncthreads();
     const int64_t r = (int64_t)blockIdx.x * EYE_BLOCK + threadIdx.x;
     if (r >= P.R.count) return;
 
@@ -225,6 +226,7 @@ hipError_t launch_simple(const EyeParams &p, float *out, hipStream_t s) {
     switch (scene_mode(p.S)) {
     case MODE_BRUTE: pm_launch(k_simple<MODE_BRUTE>, dim3(grid), dim3(EYE_BLOCK), lds, s, p, out); break;
     case MODE_LDS: pm_launch(k_simple<MODE_LDS>, dim3(grid), dim3(EYE_BLOCK), lds, s, p, out); break;
+    case MODE_INST: pm_launch(k_simple<MODE_INST>, dim3(grid), dim3(EYE_BLOCK), lds, s, p, out); break;
     default: pm_launch(k_simple<MODE_GLOBAL>, dim3(grid), dim3(EYE_BLOCK), lds, s, p, out); break;
     }
     return hipGetLastError();
@@ -488,7 +490,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
     __shared__ uint32_t perm[28];
     const int tid = threadIdx.x;
     if (tid < 28) perm[tid] = P.perm[tid];
-    const SceneDev S = scene_view<MODE != MODE_GLOBAL>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * TRACE_BLOCK),
+    const SceneDev S = scene_view<mode_lds(MODE)>(P.S, reinterpret_cast<uint4 *>(stk + P.S.stack_depth * TRACE_BLOCK),
                                                        tid, TRACE_BLOCK);
     __syncthreads();
     int *stack = stk + tid;
@@ -499,7 +501,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
     PathState st;
     Held held;
     if (HOLD) /* after the stacks and the (16-B padded) scene blob */
-        held.col = reinterpret_cast<uint32_t *>(stk + P.S.stack_depth * TRACE_BLOCK + (MODE != MODE_GLOBAL ? (int)((P.S.lds_bytes + 15u) / 4u & ~3u) : 0)) + tid;
+        held.col = reinterpret_cast<uint32_t *>(stk + P.S.stack_depth * TRACE_BLOCK + (mode_lds(MODE) ? (int)((P.S.lds_bytes + 15u) / 4u & ~3u) : 0)) + tid;
     prof.begin();
     if (path < P.path_count) {
         if (HOLD) held_clear(held);
@@ -673,6 +675,10 @@ static void launch_lane(const TraceParams &p, dim3 grid, size_t lds, int count, 
     case MODE_LDS:
         if (count) pm_launch((k_trace_lane<1, MODE_LDS, HOLD>), grid, dim3(TRACE_BLOCK), lds, s, p);
         else pm_launch((k_trace_lane<0, MODE_LDS, HOLD>), grid, dim3(TRACE_BLOCK), lds, s, p);
+        break;
+    case MODE_INST: /* instances: the per-lane kernel (the pooled one walks only one level) */
+        if (count) pm_launch((k_trace_lane<1, MODE_INST, HOLD>), grid, dim3(TRACE_BLOCK), lds, s, p);
+        else pm_launch((k_trace_lane<0, MODE_INST, HOLD>), grid, dim3(TRACE_BLOCK), lds, s, p);
         break;
     default:
         if (count) pm_launch((k_trace_lane<1, MODE_GLOBAL, HOLD>), grid, dim3(TRACE_BLOCK), lds, s, p);

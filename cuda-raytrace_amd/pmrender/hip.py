@@ -47,6 +47,8 @@ def load_library(path=None):
         "pm_version": (ctypes.c_char_p, []),
         "pm_add_material": (c_int, [vp, c_int, P_f, P_i]),
         "pm_add_trimesh": (c_int, [vp, P_f, c_int, P_i, c_int, P_f, P_f, c_int, c_int]),
+        "pm_add_object_mesh": (c_int, [vp, P_f, c_int, P_i, c_int, P_f, P_f, c_int, c_int, P_i]),
+        "pm_add_mesh_instance": (c_int, [vp, c_int, P_f, P_f]),
         "pm_add_sphere": (c_int, [vp, c_float, P_f, P_f, c_int, c_int]),
         "pm_add_disk": (c_int, [vp, P_f, P_f, P_f, P_f, c_float, c_float, c_int, c_int]),
         "pm_add_light_point": (c_int, [vp, P_f, P_f]),
@@ -176,6 +178,20 @@ class Context:
         N, uv = f32(N), f32(uv)
         self._chk(self.lib.pm_add_trimesh(self.h, fptr(P), P.size // 3, iptr(idx), idx.size // 3, fptr(N), fptr(uv),
                                           int(material), int(light)))
+
+    def add_object_mesh(self, P, idx, N=None, uv=None, material=0, light=-1):
+        """A mesh stored once in object space (pm_add_object_mesh); returns its object id."""
+        P = f32(P)
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        N, uv = f32(N), f32(uv)
+        out = ctypes.c_int()
+        self._chk(self.lib.pm_add_object_mesh(self.h, fptr(P), P.size // 3, iptr(idx), idx.size // 3, fptr(N),
+                                              fptr(uv), int(material), int(light), ctypes.byref(out)))
+        return out.value
+
+    def add_mesh_instance(self, obj, o2w, w2o):
+        """One instance of an object mesh (pm_add_mesh_instance): affine row-major 4x4 and its inverse."""
+        self._chk(self.lib.pm_add_mesh_instance(self.h, int(obj), fptr(f32(o2w, 16)), fptr(f32(w2o, 16))))
 
     def add_sphere(self, r, o2w, w2o, material, light=-1):
         self._chk(self.lib.pm_add_sphere(self.h, float(r), fptr(f32(o2w, 16)), fptr(f32(w2o, 16)), int(material),
@@ -376,10 +392,11 @@ class Context:
         self._chk(self.lib.pm_scene_info(self.h, out))
         v = [int(x) for x in out]
         return {"triangles": v[0], "disks": v[1], "spheres": v[2], "bvh_nodes": v[3], "bvh_depth": v[4],
-                "mode": ("bvh-hbm", "bvh-lds", "brute")[v[5]], "bytes": v[6]}
+                "mode": ("bvh-hbm", "bvh-lds", "brute", "bvh-instanced")[v[5]], "bytes": v[6]}
 
     SCENE_SECTIONS = {"refs": (0, np.uint32), "tri_geo": (1, np.float32), "tri_shade": (2, np.float32),
-                      "tri_id": (3, np.uint32), "tri_info": (4, np.int32), "bvh4": (5, np.uint32)}
+                      "tri_id": (3, np.uint32), "tri_info": (4, np.int32), "bvh4": (5, np.uint32),
+                      "instances": (6, np.float32), "obj_tris": (7, np.float32)}
 
     def scene_section(self, name):
         """One section of the committed scene blob as the kernels read it (pm_scene_section)."""

@@ -34,6 +34,8 @@ class Scene:
     spheres: list = field(default_factory=list)     # (r, o2w, w2o, material, light)
     disks: list = field(default_factory=list)       # (o, x, y, z, inner, phimax, material, light)
     lights: list = field(default_factory=list)      # ("point", pos, I) | ("disk", o, p1, p2, n, Le, area, ns)
+    objects: list = field(default_factory=list)     # object meshes (as meshes), placed by `instances` only
+    instances: list = field(default_factory=list)   # (object index, o2w 4x4, w2o 4x4), affine
     camera: tuple = None                            # ("pinhole", eye, fwd, right, up, W, H) | ("rays", rays, rand2d, n2d)
 
     def material(self, mtype, rgb):
@@ -52,13 +54,46 @@ class Scene:
 
     @property
     def num_triangles(self):
-        return sum(len(m["idx"]) for m in self.meshes)
+        """triangles rendered (an object mesh once per instance)"""
+        return sum(len(m["idx"]) for m in self.meshes) + sum(len(self.objects[o]["idx"]) for o, _, _ in self.instances)
 
-    def load_into(self, api):
+    def flattened(self, k):
+        """Instance k as the world-space mesh pbrt's Transform gives (the
+        adapter's flattening, pm_cudarender.cpp): points m[0]*x + m[1]*y +
+        m[2]*z + m[3] per row, left to right, in float32; normals through the
+        transpose of w2o."""
+        o, m, mi = self.objects[self.instances[k][0]], *self.instances[k][1:]
+        m = np.asarray(m, np.float32).reshape(4, 4)
+        mi = np.asarray(mi, np.float32).reshape(4, 4)
+        P = np.asarray(o["P"], np.float32).reshape(-1, 3)
+        W = np.stack([((m[a, 0] * P[:, 0] + m[a, 1] * P[:, 1]) + m[a, 2] * P[:, 2]) + m[a, 3] for a in range(3)], 1)
+        N = o.get("N")
+        if N is not None:
+            N = np.asarray(N, np.float32).reshape(-1, 3)
+            N = np.stack([(mi[0, a] * N[:, 0] + mi[1, a] * N[:, 1]) + mi[2, a] * N[:, 2] for a in range(3)], 1)
+        return dict(o, P=W.astype(np.float32), N=N)
+
+    def load_into(self, api, instancing=True):
+        """The scene through the C-ABI calls of `api`. Object instances go in
+        as pm_add_object_mesh / pm_add_mesh_instance (two-level) when the api
+        has them and `instancing`, else flattened (the CPU oracle; the A/B
+        of the two-level trees) — after the meshes either way, so the global
+        ids are the same."""
         for mtype, rgb in self.materials:
             api.add_material(mtype, rgb)
         for m in self.meshes:
             api.add_trimesh(m["P"], m["idx"], m.get("N"), m.get("uv"), m["material"], m["light"])
+        if self.instances and instancing and hasattr(api, "add_mesh_instance"):
+            ids = {}
+            for k, (oi, o2w, w2o) in enumerate(self.instances):
+                if oi not in ids:
+                    o = self.objects[oi]
+                    ids[oi] = api.add_object_mesh(o["P"], o["idx"], o.get("N"), o.get("uv"), o["material"], o["light"])
+                api.add_mesh_instance(ids[oi], o2w, w2o)
+        else:
+            for k in range(len(self.instances)):
+                m = self.flattened(k)
+                api.add_trimesh(m["P"], m["idx"], m.get("N"), m.get("uv"), m["material"], m["light"])
         for r, o2w, w2o, mat, light in self.spheres:
             api.add_sphere(r, o2w, w2o, mat, light)
         for o, x, y, z, inner, phimax, mat, light in self.disks:
@@ -181,6 +216,41 @@ def translate(tx, ty, tz):
     return m.reshape(-1), inv.reshape(-1)
 
 
+def affine(yaw_deg=0.0, pitch_deg=0.0, scale=(1.0, 1.0, 1.0), t=(0.0, 0.0, 0.0)):
+    """o2w = T * Ry(yaw) * Rx(pitch) * S and its inverse (float64 math, float32 out)."""
+    a, b = math.radians(yaw_deg), math.radians(pitch_deg)
+    ry = np.array([[math.cos(a), 0, math.sin(a)], [0, 1, 0], [-math.sin(a), 0, math.cos(a)]])
+    rx = np.array([[1, 0, 0], [0, math.cos(b), -math.sin(b)], [0, math.sin(b), math.cos(b)]])
+    m = np.eye(4)
+    m[:3, :3] = ry @ rx @ np.diag(scale)
+    m[:3, 3] = t
+    return m.astype(np.float32).reshape(-1), np.linalg.inv(m).astype(np.float32).reshape(-1)
+
+
+def instanced_scene(W=80, H=64, subdiv=2):
+    """Two-level test scene: the figure mesh three times under rotations and
+    non-uniform scales (one mirror object among them), plus a shading-normal
+    + uv quad object (one degenerate-uv triangle) placed twice. Built for the
+    two-level vs flattened A/B (tests/test_gpu_parity.py)."""
+    s = cornell_box(W, H, blocks=False)
+    blue = s.material(PM_MATTE, (0.5, 0.5, 0.8))
+    mir = s.material(PM_MIRROR, (0.9, 0.9, 0.9))
+    tan = s.material(PM_MATTE, (0.8, 0.6, 0.3))
+    P, idx = figure_mesh(subdiv)
+    s.objects.append(dict(P=P, idx=idx, N=None, uv=None, material=blue, light=-1))
+    s.objects.append(dict(P=P, idx=idx, N=None, uv=None, material=mir, light=-1))
+    Pq = np.float32([[-60, 0, 0], [60, 10, 20], [0, 120, -20], [70, 140, 30]])
+    Nq = np.float32([[0, 0, -1], [0.2, 0, -1], [-0.2, 0.1, -1], [0, 0.3, -1]])
+    uvq = np.float32([[0, 0], [1, 0], [0, 1], [0, 1]])
+    s.objects.append(dict(P=Pq, idx=np.int32([[0, 1, 2], [0, 2, 3]]), N=Nq, uv=uvq, material=tan, light=-1))
+    s.instances.append((0, *affine(30.0, 0.0, (1.2, 0.8, 1.0), (170.0, 0.0, 220.0))))
+    s.instances.append((0, *affine(-75.0, 10.0, (0.7, 0.7, 0.9), (400.0, 40.0, 380.0))))
+    s.instances.append((1, *affine(140.0, 0.0, (0.6, 0.9, 0.6), (300.0, 200.0, 150.0))))
+    s.instances.append((2, *affine(20.0, -15.0, (1.0, 1.0, 1.0), (120.0, 300.0, 420.0))))
+    s.instances.append((2, *affine(-160.0, 0.0, (0.8, 1.3, 0.8), (430.0, 250.0, 120.0))))
+    return s
+
+
 def caustic_scene(W=256, H=256, mirror=True):
     s = cornell_box(W, H, blocks=False)
     glass = s.material(PM_GLASS, (1.0, 1.0, 1.0))
@@ -243,9 +313,10 @@ def figure_scene(W=256, H=256, subdiv=4):
     s = cornell_box(W, H, blocks=False)
     blue = s.material(PM_MATTE, (0.5, 0.5, 0.8))
     P, idx = figure_mesh(subdiv)
+    s.objects.append(dict(P=P, idx=idx, N=None, uv=None, material=blue, light=-1))
     for t in FIGURE_INSTANCES:
-        s.meshes.append(dict(P=(P + np.float32(t)).astype(np.float32), idx=idx, N=None, uv=None,
-                             material=blue, light=-1))
+        o2w, w2o = translate(*t)
+        s.instances.append((0, o2w, w2o))
     return s
 
 

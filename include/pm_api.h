@@ -169,6 +169,21 @@ int pm_add_material(void *ctx, int type, const float rgb[3], int *out_id);
  * the area light this shape emits for, -1 otherwise. */
 int pm_add_trimesh(void *ctx, const float *P, int nverts, const int *indices, int ntris,
                    const float *N, const float *uv, int material, int light_index);
+/* Object instancing (the reference's CudaObjectInstance, cudaapi.h:17 /
+ * cudarender.cpp:88-103: an OptiX Transform over the instance's group).
+ * pm_add_object_mesh stores a mesh once, in object space (arguments as
+ * pm_add_trimesh), without rendering it; *out_object = its id.
+ * pm_add_mesh_instance places it with a row-major affine object-to-world
+ * matrix (last row 0 0 0 1, else PM_ERR_INVALID) and its inverse: the scene
+ * gets a two-level tree (the object's own 4-wide tree, entered from the
+ * top-level one), and every hit, shading frame and photon equals the hit of
+ * the mesh flattened to world space with pbrt's Transform (points:
+ * m[0]*x + m[1]*y + m[2]*z + m[3] per row, left to right; normals: the
+ * transpose of w2o) and added with pm_add_trimesh at this call (global ids
+ * in call order). */
+int pm_add_object_mesh(void *ctx, const float *P, int nverts, const int *indices, int ntris,
+                       const float *N, const float *uv, int material, int light_index, int *out_object);
+int pm_add_mesh_instance(void *ctx, int object, const float o2w[16], const float w2o[16]);
 /* Object-space sphere (cudasphere.cpp:15-40): row-major 4x4 matrices. */
 int pm_add_sphere(void *ctx, float radius, const float o2w[16], const float w2o[16],
                   int material, int light_index);
@@ -297,9 +312,11 @@ int pm_gather_counters(void *ctx, int64_t out[4]);
  * [1] BVH nodes entered, [2] primitive intersection tests, [3] photons
  * deposited (the traffic census behind the trace roofline) */
 int pm_trace_counters(void *ctx, int64_t out[4]);
-/* the loaded scene as the traversal kernels see it: [0] triangles, [1] disks,
- * [2] spheres, [3] BVH nodes, [4] BVH depth, [5] traversal mode (0 BVH in
- * HBM, 1 BVH in LDS, 2 brute force over an LDS-sized scene), [6] scene bytes.
+/* the loaded scene as the traversal kernels see it: [0] triangles rendered
+ * (an instanced mesh counted once per instance), [1] disks, [2] spheres,
+ * [3] BVH nodes, [4] BVH depth, [5] traversal mode (0 BVH in HBM, 1 BVH in
+ * LDS, 2 brute force over an LDS-sized scene, 3 two-level: top tree over
+ * instance boxes + one tree per object mesh), [6] scene bytes.
  * [3] / [4] describe the tree the kernels traverse: with mode 0 that is the
  * 4-wide quantized BVH (its node count and its depth in 4-wide levels),
  * whichever builder made it (device PLOC for >= 65,536 primitives, else the
@@ -316,6 +333,8 @@ int pm_scene_info(void *ctx, int64_t out[7]);
 #define PM_SCENE_TRI_ID 3
 #define PM_SCENE_TRI_INFO 4
 #define PM_SCENE_BVH4 5
+#define PM_SCENE_INSTANCES 6 /* 128 B per instance (pm_device.h SceneDev::insts) */
+#define PM_SCENE_OBJ_TRIS 7  /* 48 B per stored object triangle (object-space p0, p1, p2) */
 int pm_scene_section(void *ctx, int section, void *out, int64_t max_bytes, int64_t *bytes);
 /* the current photon map (pm_build_photon_map; the reference's
  * CreatePhotonMap, photonmappingrenderer.cpp:150-180): [0] structure

@@ -110,7 +110,7 @@ def test_killeroo_proxy_pbrt_is_the_figure_scene():
     np.testing.assert_array_equal(f32(proto[0]["P"]), P.reshape(-1))
     np.testing.assert_array_equal(np.int32(proto[0]["indices"]), idx.reshape(-1))
     np.testing.assert_array_equal(f32(proto[0]["k"]), f32([0.5, 0.5, 0.8]))
-    figs = sc.meshes[-2:]
+    figs = [sc.flattened(k) for k in range(len(sc.instances))]
     for inst, want in zip(insts, figs):
         m = f32(inst["o2w"]).reshape(4, 4)
         assert np.array_equal(m[:3, :3], np.eye(3, dtype=np.float32))

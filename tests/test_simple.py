@@ -98,7 +98,7 @@ def test_simple_specular_hit_is_black(oracle_mod):
 
 # ---------------------------------------------------------------- GPU parity
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["cornell", "feature", "caustic", "soup", "cornell_rays", "feature_rays"])
+@pytest.mark.parametrize("name", ["cornell", "feature", "caustic", "soup", "instanced", "cornell_rays", "feature_rays"])
 def test_simple_gpu_bitexact(name, oracle_mod, hip_mod):
     if name.startswith("cornell"):
         s = scenes.cornell_box(64, 48)
@@ -106,6 +106,8 @@ def test_simple_gpu_bitexact(name, oracle_mod, hip_mod):
         s = scenes.feature_scene()
     elif name == "caustic":
         s = scenes.caustic_scene(48, 40)
+    elif name == "instanced":   # two-level trees (MODE_INST) on the GPU, flattened in the oracle
+        s = scenes.instanced_scene(64, 48)
     else:
         s = scenes.triangle_soup(20000, 64, 40)
     if name.endswith("_rays"):
