@@ -439,9 +439,13 @@ PMD void isect_tri_pair(const TriPair &q, const RaySplat &ray, f2 &t, f2 &beta, 
     const f2 e1x = q.e1x, e1y = q.e1y, e1z = q.e1z, nx = q.nx, ny = q.ny, nz = q.nz;
     const f2 dx = ray.dx, dy = ray.dy, dz = ray.dz;
     const f2 den = (nx * dx + ny * dy) + nz * dz; /* dot(n, d) */
-    f2 inv;
-    inv.x = rcp_exact(den.x);
-    inv.y = rcp_exact(den.y);
+    /* rcp_exact of both, one range check for the pair (either outside
+     * [2^-125, 2^125): both divide; a NaN passes the check and gives NaN
+     * either way) and the Newton step as two packed FMAs */
+    const f2 r0 = f2{__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+    f2 inv = __builtin_elementwise_fma(__builtin_elementwise_fma(-den, r0, bc2(1.0f)), r0, r0);
+    const float alo = fminf(fabsf(den.x), fabsf(den.y)), ahi = fmaxf(fabsf(den.x), fabsf(den.y));
+    if (__builtin_expect(!(alo >= 0x1p-125f) | !(ahi < 0x1p125f), 0)) { inv.x = 1.0f / den.x; inv.y = 1.0f / den.y; }
     const f2 e2x = inv * (p0x - ray.ox), e2y = inv * (p0y - ray.oy), e2z = inv * (p0z - ray.oz);
     const f2 ix = dy * e2z - dz * e2y, iy = dz * e2x - dx * e2z, iz = dx * e2y - dy * e2x; /* cross(d, e2) */
     beta = (ix * e1x + iy * e1y) + iz * e1z;
@@ -474,6 +478,10 @@ PMD bool brute_isect(const SceneDev &S, const Ray &ray, Hit &best, C &cen) {
     /* (software-pipelining the next pair's scalar loads measured slower:
      * C2 trace 91 vs 86 us — more live SGPRs, no unroll; so did pipelined
      * vector loads of the pairs into VGPRs: 73.5 -> 99 us, 111 VGPRs) */
+    /* the running best in locals (one register per field: with the Hit
+     * reference the compiler kept best.t twice, one more move per hit) */
+    float bt = best.t, bb = best.beta, bg = best.gamma;
+    uint32_t bref = best.ref;
 #pragma unroll 2
     for (; k + 1 < S.n_tris; k += 2) {
         cen.prim(); cen.prim();
@@ -484,9 +492,10 @@ PMD bool brute_isect(const SceneDev &S, const Ray &ray, Hit &best, C &cen) {
         const bool ok0 = (!ANY || t.x < ray.tmax) & (t.x > ray.tmin) & (b.x >= 0.0f) & (g.x >= 0.0f) & (b.x + g.x <= 1);
         const bool ok1 = (!ANY || t.y < ray.tmax) & (t.y > ray.tmin) & (b.y >= 0.0f) & (g.y >= 0.0f) & (b.y + g.y <= 1);
         if (ANY) { if (ok0 | ok1) return true; continue; }
-        if (ok0 && t.x < best.t) take(best, t.x, b.x, g.x, (PRIM_TRI << 30) | (uint32_t)k);
-        if (ok1 && t.y < best.t) take(best, t.y, b.y, g.y, (PRIM_TRI << 30) | (uint32_t)(k + 1));
+        if (ok0 && t.x < bt) { bt = t.x; bb = b.x; bg = g.x; bref = (PRIM_TRI << 30) | (uint32_t)k; }
+        if (ok1 && t.y < bt) { bt = t.y; bb = b.y; bg = g.y; bref = (PRIM_TRI << 30) | (uint32_t)(k + 1); }
     }
+    if (!ANY) { best.t = bt; best.beta = bb; best.gamma = bg; best.ref = bref; }
     if (k < S.n_tris) {
         cen.prim();
         float t, b, g;
