@@ -505,7 +505,9 @@ def main():
             "flops_per_launch": int(41 * prims), "formula": "41 * prim_tests",
             "units": {"rays": rays, "prim_tests": prims, "deposits": deposits},
             "avg_launch_ms": stages["trace"],
-            "note": "bounded by its slowest waves (avg wave lifetime ~0.7 of the kernel), not by VALU throughput"}
+            "note": "one occupancy round of 4,096 waves, each as long as its longest path (~5 rays against 3.46 on "
+                    "average); ~64 % VALU busy, ~60 % of the VALU work in the packed triangle-pair test "
+                    "(profiles/r05/trace_c2)"}
     elif tcensus is not None and "trace" in stages:
         rays, nodes, prims, deposits = tcensus
         # SURVEY.md §8d (reported, not graded): 40 B per deposit + 32 B per BVH
@@ -514,8 +516,9 @@ def main():
         tach = tbytes / (stages["trace"] * 1e-3) / 1e9
         trace_roofline = {
             "bound": "hbm",
-            "kernel": ("k_trace_pool (4-wide BVH in HBM / MALL, pooled paths)" if ctx.scene_info()["mode"] == "bvh-hbm"
-                       else "k_trace_lane<0,MODE_LDS>"),
+            "kernel": {"bvh-hbm": "k_trace_pool (4-wide BVH in HBM / MALL, pooled paths)",
+                       "bvh-instanced": "k_trace_lane<0,MODE_INST> (top tree + one tree per object mesh)"}.get(
+                           ctx.scene_info()["mode"], "k_trace_lane<0,MODE_LDS>"),
             "achieved": round(tach, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(tach / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": int(tbytes),
             "formula": "40*deposits + 32*bvh_nodes + 36*prim_tests (SURVEY.md §8d B_trace)",
