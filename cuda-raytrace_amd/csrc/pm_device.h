@@ -528,13 +528,12 @@ PMD bool brute_isect(const SceneDev &S, const Ray &ray, Hit &best, C &cen) {
  * pm_build.h's LEAF_TRIS flag (only quantize_bvh4 sets it; binary and float
  * 4-wide leaves are always decoded through their refs, whatever their size). */
 template <bool ANY, class C>
-PMD bool blas_isect(const SceneDev &S, uint32_t inst, const Ray &ray, const v3 &oinv, const v3 &inv, Hit &best,
-                    int *stack, int stride, C &cen);
+PMD bool blas_isect(const SceneDev &S, uint32_t inst, const Ray &ray, Hit &best, int *stack, int stride, C &cen);
 /* INST: the leaf's refs may be instances (MODE_INST), whose trees are walked
  * with the stack entries above the caller's (stack, stride) */
 template <bool ANY, bool TRIRUN = false, class C, bool INST = false>
 PMD bool leaf_isect(const SceneDev &S, uint32_t start, uint32_t count, const Ray &ray, Hit &best, C &cen,
-                    int *istack = nullptr, int istride = 0, const v3 *oinv = nullptr, const v3 *inv = nullptr) {
+                    int *istack = nullptr, int istride = 0) {
     if (TRIRUN && (count & 0x4000u)) { /* LEAF_TRIS: triangles at storage slots [start, start + n), no refs */
         for (uint32_t idx = start; idx < start + (count & 0x3fffu); ++idx) {
             cen.prim();
@@ -557,7 +556,7 @@ PMD bool leaf_isect(const SceneDev &S, uint32_t start, uint32_t count, const Ray
         bool ok;
         uint32_t gid;
         if (INST && kind == PRIM_INST) {
-            if (blas_isect<ANY>(S, idx, ray, *oinv, *inv, best, istack, istride, cen) && ANY) return true;
+            if (blas_isect<ANY>(S, idx, ray, best, istack, istride, cen) && ANY) return true;
             continue;
         }
         if (kind == PRIM_TRI) {
@@ -667,11 +666,30 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
 #ifndef PM_BVH4_QUANT
 #define PM_BVH4_QUANT 1 /* build-time node format: 1 = quantized 64-B nodes, 0 = 128-B float nodes */
 #endif
+/* a quantized node's four child boxes against the ray (the node's 64 B
+ * already loaded: trav_step requests them ahead) */
+PMD void node4_decode(const uint4 w0, const uint4 w1, const uint4 w2, const uint4 w3, const v3 &oinv, const v3 &inv,
+                      float tmin, float tmax, float t[4], int c[4], int n[4], const v3 &oinvH);
 PMD void node4_test(const SceneDev &S, int cur, const v3 &oinv, const v3 &inv, float tmin, float tmax, float t[4],
                     int c[4], int n[4], const v3 &oinvH) {
     if (PM_BVH4_QUANT) {
         const uint4 *nd = reinterpret_cast<const uint4 *>(S.wnodes) + 4 * cur;
-        const uint4 w0 = nd[0], w1 = nd[1], w2 = nd[2], w3 = nd[3];
+        node4_decode(nd[0], nd[1], nd[2], nd[3], oinv, inv, tmin, tmax, t, c, n, oinvH);
+    } else {
+        const float4 *nd = S.wnodes + 8 * cur;
+        const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
+        const int4 ch = *reinterpret_cast<const int4 *>(nd + 6), cn = *reinterpret_cast<const int4 *>(nd + 7);
+        t[0] = box_near(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, oinv, inv, tmin, tmax, oinvH);
+        t[1] = box_near(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, oinv, inv, tmin, tmax, oinvH);
+        t[2] = box_near(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, oinv, inv, tmin, tmax, oinvH);
+        t[3] = box_near(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, oinv, inv, tmin, tmax, oinvH);
+        c[0] = ch.x; c[1] = ch.y; c[2] = ch.z; c[3] = ch.w;
+        n[0] = cn.x; n[1] = cn.y; n[2] = cn.z; n[3] = cn.w;
+    }
+}
+PMD void node4_decode(const uint4 w0, const uint4 w1, const uint4 w2, const uint4 w3, const v3 &oinv, const v3 &inv,
+                      float tmin, float tmax, float t[4], int c[4], int n[4], const v3 &oinvH) {
+    {
         const float ox = __uint_as_float(w0.x), oy = __uint_as_float(w0.y), oz = __uint_as_float(w0.z);
         /* step 2^e: exponent field e + 127 = stored byte - 1 */
         const float sx = __uint_as_float(((w0.w & 0xffu) - 1u) << 23);
@@ -696,16 +714,6 @@ PMD void node4_test(const SceneDev &S, int cur, const v3 &oinv, const v3 &inv, f
         n[0] = (int)(int16_t)(w2.z & 0xffffu); n[1] = (int)(int16_t)(w2.z >> 16);
         n[2] = (int)(int16_t)(w2.w & 0xffffu); n[3] = (int)(int16_t)(w2.w >> 16);
 #undef QDEC
-    } else {
-        const float4 *nd = S.wnodes + 8 * cur;
-        const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
-        const int4 ch = *reinterpret_cast<const int4 *>(nd + 6), cn = *reinterpret_cast<const int4 *>(nd + 7);
-        t[0] = box_near(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, oinv, inv, tmin, tmax, oinvH);
-        t[1] = box_near(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, oinv, inv, tmin, tmax, oinvH);
-        t[2] = box_near(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, oinv, inv, tmin, tmax, oinvH);
-        t[3] = box_near(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, oinv, inv, tmin, tmax, oinvH);
-        c[0] = ch.x; c[1] = ch.y; c[2] = ch.z; c[3] = ch.w;
-        n[0] = cn.x; n[1] = cn.y; n[2] = cn.z; n[3] = cn.w;
     }
 }
 PMD void node4_test(const SceneDev &S, int cur, const v3 &oinv, const v3 &inv, float tmin, float tmax, float t[4],
@@ -762,8 +770,7 @@ PMD bool traverse4(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int
         }
         while (l0n != 0) {
             /* instance trees use the stack entries above the ones in use */
-            if (leaf_isect<ANY, PM_BVH4_QUANT != 0, C, INST>(S, l0s, l0n, ray, best, cen, stack + sp * stride, stride,
-                                                             &oinv, &inv))
+            if (leaf_isect<ANY, PM_BVH4_QUANT != 0, C, INST>(S, l0s, l0n, ray, best, cen, stack + sp * stride, stride))
                 return true;
             l0s = l1s; l0n = l1n; l1s = l2s; l1n = l2n; l2s = l3s; l2n = l3n; l3n = 0;
         }
@@ -818,8 +825,7 @@ PMD uint32_t inst_of_gid(const SceneDev &S, uint32_t gid) {
  * flattened mesh's, so hits equal the flattened scene's bit for bit. The
  * stack entries above the caller's hold the walk (collapse_bvh4's bound). */
 template <bool ANY, class C>
-PMD bool blas_isect(const SceneDev &S, uint32_t inst, const Ray &ray, const v3 &, const v3 &, Hit &best,
-                    int *stack, int stride, C &cen) {
+PMD bool blas_isect(const SceneDev &S, uint32_t inst, const Ray &ray, Hit &best, int *stack, int stride, C &cen) {
     const float4 *I = S.insts + 8 * inst;
     const float4 hd = I[6], pk = I[7];
     const uint32_t gid0 = (uint32_t)__float_as_int(hd.z);
@@ -918,6 +924,9 @@ struct SpillStack {
 /* false once the ray is done (best holds its closest hit, if any) */
 template <class C>
 PMD bool trav_step(const SceneDev &S, const Ray &ray, TravState &T, const SpillStack &stk, C &cen) {
+    /* (requesting the node before the pending leaf's test, so a wave's leaf
+     * and node loads overlap, measured slower: C3 trace 4.14 -> 4.22-4.27 ms,
+     * 88 B of scratch at 5 waves/SIMD or 4.23-4.26 ms at 4; profiles/r05/trace_c3) */
     if (T.l0n != 0) {
         leaf_isect<false, PM_BVH4_QUANT != 0>(S, T.l0s, T.l0n, ray, T.best, cen);
         T.l0s = T.l1s; T.l0n = T.l1n; T.l1s = T.l2s; T.l1n = T.l2n; T.l2s = T.l3s; T.l2n = T.l3n; T.l3n = 0;
@@ -976,11 +985,14 @@ struct Geo { v3 ns, dpdu; int material, light; };
 /* hit attributes (cudatrianglemesh.cu:20-78, cudadisk.cu:36-47,
  * cudasphere.cu:35-48), transformed and normalized as the closest-hit
  * programs do (raytracing.cu:110-117, cudamaterial.cu.h:84-85). */
+/* INST: the scene may hold instances (MODE_INST kernels); the others compile
+ * without that branch (its registers cost the pooled trace kernel scratch) */
+template <bool INST = true>
 PMD Geo shade(const SceneDev &S, const Ray &ray, const Hit &h) {
     Geo g;
     uint32_t kind = h.ref >> 30, idx = h.ref & 0x3fffffffu;
     v3 nsw, dpduw;
-    if (kind == PRIM_INST) { /* an instance's triangle: the flattened triangle's frame, rebuilt */
+    if (INST && kind == PRIM_INST) { /* an instance's triangle: the flattened triangle's frame, rebuilt */
         const float4 *I = S.insts + 8 * inst_of_gid(S, h.gid);
         v3 p0, p1, p2;
         float4 gg[3];

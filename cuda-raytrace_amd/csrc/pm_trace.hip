@@ -62,7 +62,7 @@ __global__ __launch_bounds__(EYE_BLOCK) void k_eye(EyeParams P) {
     uint32_t flags = 0;
     while (true) {
         if (!traverse<false, MODE>(S, ray, h, stack, EYE_BLOCK)) { flags = PM_REC_MISS; break; }
-        g = shade(S, ray, h);
+        g = shade<MODE == MODE_INST>(S, ray, h);
         const v3 point = ray.o + ray.d * h.t;
         int mtype = fbits(S.materials[g.material].w);
         if (is_specular(mtype)) {
@@ -184,7 +184,7 @@ __global__ __launch_bounds__(EYE_BLOCK) void k_simple(EyeParams P, float *out) {
     v3 L = mk(0.f, 0.f, 0.f);
     Hit h;
     if (traverse<false, MODE>(S, ray, h, stack, EYE_BLOCK)) {
-        const Geo g = shade(S, ray, h);
+        const Geo g = shade<MODE == MODE_INST>(S, ray, h);
         const v3 point = ray.o + ray.d * h.t;
         const float4 m = S.materials[g.material];
         const v3 fv = fbits(m.w) == PM_MATTE ? xyz(m) * INV_PI : mk(0.f, 0.f, 0.f); /* f(wo, wi) */
@@ -386,7 +386,7 @@ PMD bool emit_path(const TraceParams &P, const SceneDev &S, const uint32_t *perm
 
 /* one ray of a path: trace, then specular continuation or diffuse deposit +
  * Lambert bounce (photontracing.cu:119-183); false when the path ends */
-template <int HOLD>
+template <int HOLD, bool INST = false>
 PMD bool path_shade(const TraceParams &P, const SceneDev &S, PathState &st, const Hit &h, TProf &prof, Held &held);
 
 template <int MODE, int HOLD, class C>
@@ -396,16 +396,16 @@ PMD bool path_step(const TraceParams &P, const SceneDev &S, int *stack, PathStat
     const bool hit = traverse<false, MODE>(S, st.ray, h, stack, TRACE_BLOCK, cen);
     prof.mark(1);
     if (!hit) return false;
-    return path_shade<HOLD>(P, S, st, h, prof, held);
+    return path_shade<HOLD, MODE == MODE_INST>(P, S, st, h, prof, held);
 }
 
 /* the hit of a path's ray: specular continuation, or diffuse deposit +
  * Lambert bounce (photontracing.cu:119-183); false when the path ends.
  * HOLD: the deposit goes to `held` (written at path end, held_write) */
-template <int HOLD>
+template <int HOLD, bool INST>
 PMD bool path_shade(const TraceParams &P, const SceneDev &S, PathState &st, const Hit &h, TProf &prof, Held &held) {
     const uint32_t mpc = (uint32_t)P.mpc;
-    Geo g = shade(S, st.ray, h);
+    Geo g = shade<INST>(S, st.ray, h);
     v3 hit_point = st.ray.o + h.t * st.ray.d;
     float4 m = S.materials[g.material];
     int mtype = fbits(m.w);
