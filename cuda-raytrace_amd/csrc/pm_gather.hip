@@ -636,7 +636,10 @@ PMD void coop_batch(const GatherParams &P, TileLds &T, int lane, const GatherRec
     wave_lds_sync(); /* the sums are read before anything else writes the array */
 }
 
-template <int PARTIAL, int NN, int KR>
+/* COST: record each wave's lifetime into P.tile_cost (the launch that
+ * measures the tile list for k_tile_sort); a separate instance, since the
+ * clock kept live across the kernel cost the timed instance 12 B of scratch */
+template <int PARTIAL, int NN, int KR, bool COST>
 __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParams P) {
     static_assert(KR >= 2 && KR <= 5 && 2 * tile_group_r<KR>() + KR <= 8, "lane box / group radius");
     constexpr uint32_t GR = tile_group_r<KR>();
@@ -644,7 +647,7 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
     TileLds &T = tiles[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     int64_t r, w = 0;
-    const unsigned long long tc0 = P.tile_cost ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const unsigned long long tc0 = COST ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (P.tiles) { /* only tiles with an active record (no block-level barrier below: a wave may leave) */
         w = (int64_t)blockIdx.x * (TILE_BLOCK / 64) + (threadIdx.x >> 6);
         const int64_t nt = P.n_tiles_dev ? (int64_t)*P.n_tiles_dev : P.n_tiles;
@@ -995,7 +998,7 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
     gp.mark(5);
     R.store<PARTIAL>(P, r, M, Lf);
     if (!PARTIAL && P.r2hist) r2_histogram(P, R.live, R.st.w);
-    if (P.tile_cost && lane == 0)
+    if (COST && lane == 0)
         P.tile_cost[w] = (uint16_t)min(__builtin_amdgcn_s_memrealtime() - tc0, 65535ull);
     gp.mark(6);
     gp.flush(P.counters);
@@ -2434,19 +2437,21 @@ __global__ __launch_bounds__(GATHER_BLOCK) void k_gather_kd(GatherParams P) {
     if (COUNT) count4(P.counters, vis, hits, rows, act);
 }
 
-template <int PARTIAL, int NN>
+template <int PARTIAL, int NN, bool COST>
 static void launch_tile_nn(const GatherParams &p, unsigned g, hipStream_t s) {
     switch (p.span) { /* cells per axis of a lane box at the grid's design radius */
-    case 2: pm_launch((k_gather_tile<PARTIAL, NN, 2>), dim3(g), dim3(TILE_BLOCK), 0, s, p); break;
-    case 3: pm_launch((k_gather_tile<PARTIAL, NN, 3>), dim3(g), dim3(TILE_BLOCK), 0, s, p); break;
-    case 4: pm_launch((k_gather_tile<PARTIAL, NN, 4>), dim3(g), dim3(TILE_BLOCK), 0, s, p); break;
-    default: pm_launch((k_gather_tile<PARTIAL, NN, 5>), dim3(g), dim3(TILE_BLOCK), 0, s, p); break;
+    case 2: pm_launch((k_gather_tile<PARTIAL, NN, 2, COST>), dim3(g), dim3(TILE_BLOCK), 0, s, p); break;
+    case 3: pm_launch((k_gather_tile<PARTIAL, NN, 3, COST>), dim3(g), dim3(TILE_BLOCK), 0, s, p); break;
+    case 4: pm_launch((k_gather_tile<PARTIAL, NN, 4, COST>), dim3(g), dim3(TILE_BLOCK), 0, s, p); break;
+    default: pm_launch((k_gather_tile<PARTIAL, NN, 5, COST>), dim3(g), dim3(TILE_BLOCK), 0, s, p); break;
     }
 }
 template <int PARTIAL>
 static void launch_tile(const GatherParams &p, unsigned g, hipStream_t s) {
-    if (p.fx_nonneg) launch_tile_nn<PARTIAL, 1>(p, g, s);
-    else launch_tile_nn<PARTIAL, 0>(p, g, s);
+    /* only a list launch measures tile costs (they index the list) */
+    const bool cost = p.tile_cost != nullptr && p.tiles != nullptr;
+    if (p.fx_nonneg) cost ? launch_tile_nn<PARTIAL, 1, true>(p, g, s) : launch_tile_nn<PARTIAL, 1, false>(p, g, s);
+    else cost ? launch_tile_nn<PARTIAL, 0, true>(p, g, s) : launch_tile_nn<PARTIAL, 0, false>(p, g, s);
 }
 
 template <int STRUCT, int PARTIAL, int COUNT>
