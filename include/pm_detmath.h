@@ -41,35 +41,29 @@
 #define PMDM_PI 3.14159265358979311600e+00
 #define PMDM_PI_2 1.57079632679489655800e+00
 
-/* sin on |r| <= pi/4 + tiny, Taylor to r^19 (truncation < 1e-19). */
+/* sin and cos on |r| <= pi/4 + tiny: minimax polynomials for a float
+ * result evaluated in double (|sin(r)/r - poly| < 2^-37.5, |cos(r) - poly| <
+ * 2^-34.6 — the published coefficients of FreeBSD/musl __sindf / __cosdf),
+ * so the one rounding to float is correct but for values within ~1e-11 of a
+ * rounding midpoint: within 1 ulp everywhere. Round 5: these replace Taylor
+ * series to r^19 / r^20 (~48 double operations per sincos -> ~26). */
 PMDM_FN double pmdm_sin_kern(double r) {
+    const double S1 = -0x15555554cbac77.0p-55, S2 = 0x111110896efbb2.0p-59;
+    const double S3 = -0x1a00f9e2cae774.0p-65, S4 = 0x16cd878c3b46a7.0p-71;
     double z = r * r;
-    double p = -1.0 / 121645100408832000.0;          /* -1/19! */
-    p = p * z + 1.0 / 355687428096000.0;             /*  1/17! */
-    p = p * z - 1.0 / 1307674368000.0;               /* -1/15! */
-    p = p * z + 1.0 / 6227020800.0;                  /*  1/13! */
-    p = p * z - 1.0 / 39916800.0;                    /* -1/11! */
-    p = p * z + 1.0 / 362880.0;                      /*  1/9!  */
-    p = p * z - 1.0 / 5040.0;                        /* -1/7!  */
-    p = p * z + 1.0 / 120.0;                         /*  1/5!  */
-    p = p * z - 1.0 / 6.0;                           /* -1/3!  */
-    return r + (r * z) * p;
+    double w = z * z;
+    double q = S3 + z * S4;
+    double s = z * r;
+    return (r + s * (S1 + z * S2)) + (s * w) * q;
 }
 
-/* cos on |r| <= pi/4 + tiny, Taylor to r^20. */
 PMDM_FN double pmdm_cos_kern(double r) {
+    const double C0 = -0x1ffffffd0c5e81.0p-54, C1 = 0x155553e1053a42.0p-57;
+    const double C2 = -0x16c087e80f1e27.0p-62, C3 = 0x199342e0ee5069.0p-68;
     double z = r * r;
-    double p = 1.0 / 2432902008176640000.0;          /*  1/20! */
-    p = p * z - 1.0 / 6402373705728000.0;            /* -1/18! */
-    p = p * z + 1.0 / 20922789888000.0;              /*  1/16! */
-    p = p * z - 1.0 / 87178291200.0;                 /* -1/14! */
-    p = p * z + 1.0 / 479001600.0;                   /*  1/12! */
-    p = p * z - 1.0 / 3628800.0;                     /* -1/10! */
-    p = p * z + 1.0 / 40320.0;                       /*  1/8!  */
-    p = p * z - 1.0 / 720.0;                         /* -1/6!  */
-    p = p * z + 1.0 / 24.0;                          /*  1/4!  */
-    p = p * z - 0.5;                                 /* -1/2!  */
-    return 1.0 + z * p;
+    double w = z * z;
+    double q = C2 + z * C3;
+    return ((1.0 + z * C0) + w * C1) + (w * z) * q;
 }
 
 /* Shared range reduction: x = k*pi/2 + r. Valid for |x| < 2^19 (all our
