@@ -1903,11 +1903,12 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
     if (p->estimator == PM_ESTIMATOR_KNN) {
         G.knn_k = p->knn_lookup;
         G.knn_r2 = p->initial_radius2; /* pbrt's maxDistSquared: the buckets cover it */
-        /* every term (kernel <= 3/pi < 1) is <= alpha_max / r_k^2: 2^47 of the
-         * per-record scale per term, and <= PM_KNN_MAX = 2^6 terms sum below
-         * 2^53 — exact in double */
+        /* every term (kernel <= 3/pi < 1) is <= alpha_max / r_k^2: <= 2^22 of
+         * the per-record scale per term (x4 headroom in amax), exact as a float
+         * and as an int32, and <= PM_KNN_MAX = 2^6 terms sum below 2^28 —
+         * exact in int32 */
         const double amax = c->emit_max * std::pow(c->kd_max, (double)p->max_photon_count) * 4.0;
-        G.knn_fx = (float)(std::ldexp(1.0, 47) / std::max(amax, 1e-30));
+        G.knn_fx = (float)(std::ldexp(1.0, 24) / std::max(amax, 1e-30));
         G.slots = c->d_slots.as<pm_photon>();
         if (c->knn_ss && !c->counting && c->gather_kernel == PM_GK_TILE) {
             const int64_t nph = (int64_t)(c->d_pha.bytes / 16), pairs = (nph + 1) / 2 + 16;

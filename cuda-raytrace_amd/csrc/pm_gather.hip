@@ -1035,16 +1035,18 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
  * slots (slot ids ride in ph_b; a third scan runs only when more ties than
  * places exist). The sum is exact and order-free: integer-valued terms
  * in the record's fixed point (scale: the power of two below knn_fx * r_k^2,
- * every term <= 2^47) added in double (Dx3). Fused record update: flux += S, radius2 = r_k^2,
+ * every term <= 2^22) added in int32 (Kx3). Fused record update: flux += S, radius2 = r_k^2,
  * photon_count = found; the final pass applies 1/paths and rho/pi = Kd/pi
  * (k_final). Both passes visit rows in rings around the query's row,
  * nearest first, and skip rows / cells beyond the current bound. */
 PMD float sq(float x) { return x * x; }
-/* kNN sums: each term rint(c * sc) is an integer-valued float <= 2^47
- * (knn_fx), at most PM_KNN_MAX = 2^6 of them per record, so their double sum
- * is exact (< 2^53): order-free like the PPM gather's int64 fixed point, at
- * one conversion and one add per channel */
-struct Dx3 { double x, y, z; };
+/* kNN sums: each term rint(c * sc) is an integer-valued float <= 2^22
+ * (knn_fx), at most PM_KNN_MAX = 2^6 of them per record, so their int32 sum
+ * is exact (< 2^28): order-free like the PPM gather's int64 fixed point, at
+ * one rounding, one conversion and one integer add per channel (round 4
+ * summed terms <= 2^47 in double: two double-rate operations per term; the
+ * scalar-stream SUM pass is 41 % of the kNN gather) */
+struct Kx3 { int x, y, z; };
 /* Dot(Faceforward(ns, wo), wi) > 0 for the photon's wi = (wx, b.w, wz) */
 PMD bool knn_facing(v3 ns, bool back, const float4 &b, float wx, float wz) {
     float dn = dot(ns, mk(wx, b.w, wz));
@@ -1053,11 +1055,11 @@ PMD bool knn_facing(v3 ns, bool back, const float4 &b, float wx, float wz) {
 }
 /* pbrt kernel() 3/pi (1 - d^2/r_k^2)^2 / r_k^2 times alpha, inv = 1/r_k^2,
  * in the record's fixed point sc */
-PMD void knn_add(Dx3 &a, float d2, float inv, float sc, const float4 &b) {
+PMD void knn_add(Kx3 &a, float d2, float inv, float sc, const float4 &b) {
     const float s = 1.f - d2 * inv;
     const float kk = 3.f * INV_PI * s * s;
     const v3 c = (kk * inv) * xyz(b);
-    a.x += (double)rintf(c.x * sc); a.y += (double)rintf(c.y * sc); a.z += (double)rintf(c.z * sc);
+    a.x += (int)rintf(c.x * sc); a.y += (int)rintf(c.y * sc); a.z += (int)rintf(c.z * sc);
 }
 /* distance, in cell units, from coordinate u (cell units) to cell c of an
  * axis with dim cells — the border cells extend to infinity (cell_axis
@@ -1160,7 +1162,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn(GatherParams P) {
             const v3 p = xyz(pos), ns = xyz(nrm);
             int cnt = 0;
             float md2 = maxd2;
-            Dx3 acc{0, 0, 0};
+            Kx3 acc{0, 0, 0};
             float sc = 1.f;
             bool nan = false;
             if (__float_as_int(m.w) == PM_MATTE) { /* non-specular BSDF components only */
@@ -1187,7 +1189,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn(GatherParams P) {
                 const float *phb = reinterpret_cast<const float *>(P.ph_b);
                 /* contribution of photon j (LPhoton term) into a */
                 const float inv = 1.f / md2;
-                auto add = [&](Dx3 &a, uint32_t j, const float4 &pa, float d2) {
+                auto add = [&](Kx3 &a, uint32_t j, const float4 &pa, float d2) {
                     const float4 b0 = P.ph_b[2 * (size_t)j];
                     if (!knn_facing(ns, back, b0, pa.w, phb[8 * (size_t)j + 4])) return;
                     if (md2 == 0.f) { nan = true; return; } /* K photons at distance 0: kernel() is 0/0 */
@@ -1196,7 +1198,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn(GatherParams P) {
                 /* pass 2: every photon below r_k^2 (all below maxD2 when not full);
                  * ties at r_k^2 aside */
                 int less = 0, ties = 0;
-                Dx3 acc_eq{0, 0, 0};
+                Kx3 acc_eq{0, 0, 0};
                 G.scan(P.cell_start, P.ph_a, p, [&]() { return md2; },
                        [&](uint32_t j, const float4 &pa, float d2) {
                            if (d2 < md2) { less++; add(acc, j, pa, d2); }
@@ -1227,7 +1229,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn(GatherParams P) {
             }
             if (COUNT) { hits += (unsigned long long)cnt; act++; }
             const double isc = 1.0 / (double)sc;
-            v3 L = mk((float)(acc.x * isc), (float)(acc.y * isc), (float)(acc.z * isc));
+            v3 L = mk((float)((double)acc.x * isc), (float)((double)acc.y * isc), (float)((double)acc.z * isc));
             if (nan) L = mk(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
             const v3 flux = xyz(st) + L;
             P.R.state[r] = make_float4(flux.x, flux.y, flux.z, md2);
@@ -1324,7 +1326,7 @@ struct KnnSel {
     int less = 0, ties = 0, cnt = 0;
     bool full = true, tiefix = false, nan = false, nan_eq = false;
     float inv = 0.f; /* 1 / r_k^2 */
-    Dx3 acc{0, 0, 0};
+    Kx3 acc{0, 0, 0};
     PMD int bin(float d2) const { return (int)fminf((d2 - lo) * s, (float)(KT_BINS - 1)); }
 };
 
@@ -1372,7 +1374,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
 
     /* contribution of a found photon (pbrt kernel(), LPhoton diffuse term) into
      * a; returns true when it is pbrt's 0/0 (K photons at distance 0) */
-    auto contrib = [&](Dx3 &a, float d2, const float4 &b, float wx, float wz) PM_INLINE {
+    auto contrib = [&](Kx3 &a, float d2, const float4 &b, float wx, float wz) PM_INLINE {
         if (!knn_facing(ns, back, b, wx, wz)) return false;
         if (S.md2 == 0.f) return true;
         knn_add(a, d2, S.inv, S.sc, b);
@@ -1415,7 +1417,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
     auto begin_sum = [&]() PM_INLINE {
         S.sc = knn_scale(P.knn_fx, S.md2);
         S.inv = 1.f / S.md2;
-        S.acc = Dx3{0, 0, 0};
+        S.acc = Kx3{0, 0, 0};
         S.less = S.ties = 0;
         S.nan = S.nan_eq = false;
         S.blo = 0.f; S.bhi = S.full ? next_up(S.md2) : S.md2; /* not full: every d^2 < maxD^2 */
@@ -1801,7 +1803,7 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
         if (!live) S.md2 = maxd2; /* specular: nothing found, cnt 0 */
         const float4 st = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : P.R.state[r];
         const double isc = 1.0 / (double)S.sc;
-        v3 Lr = mk((float)(S.acc.x * isc), (float)(S.acc.y * isc), (float)(S.acc.z * isc));
+        v3 Lr = mk((float)((double)S.acc.x * isc), (float)((double)S.acc.y * isc), (float)((double)S.acc.z * isc));
         if (S.nan) Lr = mk(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
         const v3 flux = xyz(st) + Lr;
         P.R.state[r] = make_float4(flux.x, flux.y, flux.z, S.md2);
@@ -1847,7 +1849,10 @@ __global__ __launch_bounds__(KNN_BLOCK) void k_gather_knn_tile(GatherParams P) {
 #define KS_OCC __attribute__((amdgpu_waves_per_eu(PM_KS_WAVES, PM_KS_WAVES)))
 constexpr int KS_NB = 32;   /* bins per histogram level (+1 sink), 16-bit counters: two lanes per word */
 constexpr int KS_HW = KS_NB / 2 + 1; /* LDS words per lane: (KS_NB + 1) 16-bit counters, or KS_LIST + 1 list rows + a sink row */
-constexpr int KS_LIST = 12; /* values a COLLECT keeps per lane (rows 0..KS_LIST of the histogram, +1 scratch) */
+#ifndef PM_KS_LIST
+#define PM_KS_LIST 12
+#endif
+constexpr int KS_LIST = PM_KS_LIST; /* values a COLLECT keeps per lane (rows 0..KS_LIST of the histogram, +1 scratch) */
 /* (y, z) rows of a group's union box: two per lane. With 64, a tile across a
  * corner of the room (lanes on two walls, the union deeper than 8 x 8 rows)
  * split into leader groups, each running its own passes over nearly the same
@@ -1964,7 +1969,7 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
     uint32_t klo = 0u, kw = 0u, cc = 0u;
     int need = 0, less = 0, cnt = 0;
     float md2 = maxd2, inv = 0.f, sc = 1.f;
-    Dx3 acc{0, 0, 0};
+    Kx3 acc{0, 0, 0};
 
     const const_f32_ptr pkp = (const_f32_ptr)P.knn_pk_p;
     const const_f32_ptr pkq = (const_f32_ptr)P.knn_pk_q;
@@ -2172,9 +2177,9 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
                                     if (!(h0 && dn.x > 0.f)) ki.x = 0.f;
                                     if (!(h1 && dn.y > 0.f)) ki.y = 0.f;
                                     const f2 cr = (ki * R) * sc2, cg = (ki * G) * sc2, cb = (ki * Bl) * sc2;
-                                    acc.x += (double)rintf(cr.x) + (double)rintf(cr.y);
-                                    acc.y += (double)rintf(cg.x) + (double)rintf(cg.y);
-                                    acc.z += (double)rintf(cb.x) + (double)rintf(cb.y);
+                                    acc.x += (int)rintf(cr.x) + (int)rintf(cr.y);
+                                    acc.y += (int)rintf(cg.x) + (int)rintf(cg.y);
+                                    acc.z += (int)rintf(cb.x) + (int)rintf(cb.y);
                                 }
                             }
                         }
@@ -2269,7 +2274,7 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
             if (phase == KS_SUM && pt != KS_SUM) { /* begin_sum */
                 sc = knn_scale(P.knn_fx, md2);
                 inv = 1.f / md2;
-                acc = Dx3{0, 0, 0};
+                acc = Kx3{0, 0, 0};
                 less = 0;
             } else if (pt == KS_SUM) {
                 cnt = full ? K : less;
@@ -2291,7 +2296,7 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
         if (!live) md2 = maxd2; /* specular: nothing found, cnt 0 */
         const float4 st = P.fresh ? make_float4(0.f, 0.f, 0.f, P.r2init) : P.R.state[r];
         const double isc = 1.0 / (double)sc;
-        const v3 Lr = mk((float)(acc.x * isc), (float)(acc.y * isc), (float)(acc.z * isc));
+        const v3 Lr = mk((float)((double)acc.x * isc), (float)((double)acc.y * isc), (float)((double)acc.z * isc));
         const v3 flux = xyz(st) + Lr;
         P.R.state[r] = make_float4(flux.x, flux.y, flux.z, md2);
         P.R.n[r] = (float)cnt;
