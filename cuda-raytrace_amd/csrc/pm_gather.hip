@@ -1058,8 +1058,9 @@ PMD bool knn_facing(v3 ns, bool back, const float4 &b, float wx, float wz) {
 PMD void knn_add(Kx3 &a, float d2, float inv, float sc, const float4 &b) {
     const float s = 1.f - d2 * inv;
     const float kk = 3.f * INV_PI * s * s;
-    const v3 c = (kk * inv) * xyz(b);
-    a.x += (int)rintf(c.x * sc); a.y += (int)rintf(c.y * sc); a.z += (int)rintf(c.z * sc);
+    /* sc is a power of two: (k * sc) * alpha rounds like (k * alpha) * sc */
+    const float ks = (kk * inv) * sc;
+    a.x += (int)rintf(ks * b.x); a.y += (int)rintf(ks * b.y); a.z += (int)rintf(ks * b.z);
 }
 /* distance, in cell units, from coordinate u (cell units) to cell c of an
  * axis with dim cells — the border cells extend to infinity (cell_axis
@@ -2173,10 +2174,10 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
                                     /* knn_add: s = 1 - d^2 / r_k^2, kernel 3/pi s^2, times 1/r_k^2 and alpha;
                                      * a photon that does not count gets ki = 0, so every term of it is rint(0) = 0 */
                                     const f2 sv = one2 - d2 * inv2;
-                                    f2 ki = ((c3 * sv) * sv) * inv2;
+                                    f2 ki = (((c3 * sv) * sv) * inv2) * sc2;
                                     if (!(h0 && dn.x > 0.f)) ki.x = 0.f;
                                     if (!(h1 && dn.y > 0.f)) ki.y = 0.f;
-                                    const f2 cr = (ki * R) * sc2, cg = (ki * G) * sc2, cb = (ki * Bl) * sc2;
+                                    const f2 cr = ki * R, cg = ki * G, cb = ki * Bl;
                                     acc.x += (int)rintf(cr.x) + (int)rintf(cr.y);
                                     acc.y += (int)rintf(cg.x) + (int)rintf(cg.y);
                                     acc.z += (int)rintf(cb.x) + (int)rintf(cb.y);
