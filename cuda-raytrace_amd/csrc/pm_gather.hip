@@ -2079,7 +2079,7 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
             const unsigned long long rows0 = rows | rows_hi;
 #endif
             /* per-lane constants of the pass (lanes outside it never hit) */
-            const uint32_t hA = act ? A : 0u, hsh = act ? sh : 0u, hlo = act ? 0u : (uint32_t)KS_NB;
+            const uint32_t hA = act ? A : 0u, hsh = act ? sh : 0u;
             const uint32_t clo = act ? klo : 0u, cw = act ? kw : 0u;
             const float smd = act ? md2 : -1.f, sinv = inv, ssc = sc;
             const f2 inv2 = {sinv, sinv}, sc2 = {ssc, ssc}, one2 = {1.f, 1.f}, c3 = {3.f * INV_PI, 3.f * INV_PI};
@@ -2089,7 +2089,8 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
              * h * 32 + l / 2 (lanes l, l ^ 1 share a word column), so a count
              * is one address op and a per-lane constant increment */
             uint32_t *hpair = H + (lane >> 1);
-            const uint32_t hinc = 1u << ((lane & 1) * 16);
+            /* lanes outside the pass add 0 (their half of each word stays 0) */
+            const uint32_t hinc = act ? 1u << ((lane & 1) * 16) : 0u;
             /* COLLECT: the lane's list rows (lanes outside the pass write the sink row) */
             uint32_t *lcol = hcol + (act ? 0 : (KS_HW - 1) * 64);
             uint32_t ccl = 0u;
@@ -2154,8 +2155,8 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
                             const f2 d2 = (dx * dx + dy * dy) + dz * dz; /* in_radius / KnnGrid::scan's order */
                             const uint32_t u0 = __float_as_uint(d2.x), u1 = __float_as_uint(d2.y);
                             if constexpr (PT == KS_HIST) {
-                                const uint32_t h0 = min(max(__builtin_elementwise_sub_sat(u0, hA) >> hsh, hlo), (uint32_t)KS_NB);
-                                const uint32_t h1 = min(max(__builtin_elementwise_sub_sat(u1, hA) >> hsh, hlo), (uint32_t)KS_NB);
+                                const uint32_t h0 = min(__builtin_elementwise_sub_sat(u0, hA) >> hsh, (uint32_t)KS_NB);
+                                const uint32_t h1 = min(__builtin_elementwise_sub_sat(u1, hA) >> hsh, (uint32_t)KS_NB);
                                 atomicAdd(hpair + h0 * 32u, hinc);
                                 atomicAdd(hpair + h1 * 32u, hinc);
                             } else if constexpr (PT == KS_COLLECT) {
