@@ -1040,7 +1040,7 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
  * (k_final). Both passes visit rows in rings around the query's row,
  * nearest first, and skip rows / cells beyond the current bound. */
 PMD float sq(float x) { return x * x; }
-/* kNN sums: each term rint(c * sc) is an integer-valued float <= 2^22
+/* kNN sums: each term trunc(c * sc) is an integer <= 2^22
  * (knn_fx), at most PM_KNN_MAX = 2^6 of them per record, so their int32 sum
  * is exact (< 2^28): order-free like the PPM gather's int64 fixed point, at
  * one rounding, one conversion and one integer add per channel (round 4
@@ -1058,9 +1058,10 @@ PMD bool knn_facing(v3 ns, bool back, const float4 &b, float wx, float wz) {
 PMD void knn_add(Kx3 &a, float d2, float inv, float sc, const float4 &b) {
     const float s = 1.f - d2 * inv;
     const float kk = 3.f * INV_PI * s * s;
-    /* sc is a power of two: (k * sc) * alpha rounds like (k * alpha) * sc */
-    const float ks = (kk * inv) * sc;
-    a.x += (int)rintf(ks * b.x); a.y += (int)rintf(ks * b.y); a.z += (int)rintf(ks * b.z);
+    /* sc is a power of two: k * (inv * sc) * alpha rounds like (k * inv * alpha) * sc;
+     * terms are truncated to integers (one conversion; a bias below 2^-20 of a term) */
+    const float ks = kk * (inv * sc);
+    a.x += (int)(ks * b.x); a.y += (int)(ks * b.y); a.z += (int)(ks * b.z);
 }
 /* distance, in cell units, from coordinate u (cell units) to cell c of an
  * axis with dim cells — the border cells extend to infinity (cell_axis
@@ -2082,7 +2083,9 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
             const uint32_t hA = act ? A : 0u, hsh = act ? sh : 0u;
             const uint32_t clo = act ? klo : 0u, cw = act ? kw : 0u;
             const float smd = act ? md2 : -1.f, sinv = inv, ssc = sc;
-            const f2 inv2 = {sinv, sinv}, sc2 = {ssc, ssc}, one2 = {1.f, 1.f}, c3 = {3.f * INV_PI, 3.f * INV_PI};
+            /* 1/r_k^2 times the power-of-two scale: exact, one multiply per term */
+            const float sis = sinv * ssc;
+            const f2 inv2 = {sinv, sinv}, is2 = {sis, sis}, one2 = {1.f, 1.f}, c3 = {3.f * INV_PI, 3.f * INV_PI};
             const f2 nx2 = {nsx, nsx}, ny2 = {nsy, nsy}, nz2 = {nsz, nsz};
             uint32_t *hcol = H + lane;
             /* HIST counters: bin h of lane l is the (l & 1) half of word
@@ -2175,13 +2178,13 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
                                     /* knn_add: s = 1 - d^2 / r_k^2, kernel 3/pi s^2, times 1/r_k^2 and alpha;
                                      * a photon that does not count gets ki = 0, so every term of it is rint(0) = 0 */
                                     const f2 sv = one2 - d2 * inv2;
-                                    f2 ki = (((c3 * sv) * sv) * inv2) * sc2;
+                                    f2 ki = ((c3 * sv) * sv) * is2;
                                     if (!(h0 && dn.x > 0.f)) ki.x = 0.f;
                                     if (!(h1 && dn.y > 0.f)) ki.y = 0.f;
                                     const f2 cr = ki * R, cg = ki * G, cb = ki * Bl;
-                                    acc.x += (int)rintf(cr.x) + (int)rintf(cr.y);
-                                    acc.y += (int)rintf(cg.x) + (int)rintf(cg.y);
-                                    acc.z += (int)rintf(cb.x) + (int)rintf(cb.y);
+                                    acc.x += (int)cr.x + (int)cr.y; /* knn_add's truncation */
+                                    acc.y += (int)cg.x + (int)cg.y;
+                                    acc.z += (int)cb.x + (int)cb.y;
                                 }
                             }
                         }
