@@ -106,11 +106,12 @@ struct Ctx {
     /* lazy zero fill (TraceParams::lazy_zero): slots [0, slots_dirty) may hold
      * stale data where their fused-count key (d_scratch, dirty_key_np /
      * dirty_mpc) is invalid; materialize_slots zeroes them before any reader
-     * but the bucket fill (env PM_LAZY_ZERO=0: the trace zeroes them itself) */
+     * but the bucket fill (env PM_LAZY_ZERO=1; by default the trace zeroes them
+     * itself: same-box A/B in profiles/r05/trace_writes) */
     int64_t slots_dirty = 0, dirty_key_np = 0;
     int dirty_mpc = 0;
     hipEvent_t dirty_event = nullptr;
-    bool lazy_zero = true, slots_exposed = false;
+    bool lazy_zero = false, slots_exposed = false;
     /* photon buckets */
     DevBuf d_count, d_cell_start, d_scratch, d_pha, d_phb;
     DevBuf d_knnpk, d_knnovf; /* kNN scalar stream: photon pairs, handed-back tiles (+ count) */

@@ -469,9 +469,11 @@ PMD void finish_path(const TraceParams &P, PathState &st, const Held *held = nul
     const float2 z = make_float2(0.f, 0.f);
     for (uint32_t k = st.stored; k < mpc; ++k) {
         float2 *q = reinterpret_cast<float2 *>(slots + k);
-        /* lazy_zero (fused counting): the invalid key alone marks the slot;
-         * the bucket fill never reads it, and pm_api zeroes it before any
-         * other reader (C2 trace 75-79 -> 73-74 us: 20 MB of stores fewer) */
+        /* lazy_zero (fused counting, env PM_LAZY_ZERO=1; off by default):
+         * the invalid key alone marks the slot; the bucket fill never reads
+         * it, and pm_api zeroes it before any other reader. 20-50 MB fewer
+         * trace stores per pass, but no faster C2 trace on a same-box A/B and
+         * a slower C4 bucket fill (46.5 -> 69 us; profiles/r05/trace_writes) */
         if (!P.lazy_zero) { q[0] = z; q[1] = z; q[2] = z; q[3] = z; q[4] = z; }
         if (P.bucket) P.key[key_index(P, st.pid, k)] = 0xffffffffu;
     }
