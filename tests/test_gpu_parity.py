@@ -756,6 +756,27 @@ def test_two_level_instances(oracle_mod, hip_mod):
     assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
 
 
+def test_instance_arguments(hip_mod):
+    """pm_add_mesh_instance refuses an unknown object and a projective
+    transform (the two-level path handles affine ones only); pm_add_object_mesh
+    refuses out-of-range indices."""
+    ctx = hip_mod.Context(0)
+    mat = ctx.add_material(0, (0.5, 0.5, 0.5))
+    P = np.float32([[0, 0, 0], [1, 0, 0], [0, 1, 0]])
+    with pytest.raises(hip_mod.PMError):
+        ctx.add_object_mesh(P, np.int32([[0, 1, 3]]), None, None, mat, -1)
+    obj = ctx.add_object_mesh(P, np.int32([[0, 1, 2]]), None, None, mat, -1)
+    o2w, w2o = scenes.translate(1.0, 2.0, 3.0)
+    with pytest.raises(hip_mod.PMError):
+        ctx.add_mesh_instance(obj + 1, o2w, w2o)
+    proj = np.array(o2w, np.float32).copy()
+    proj[14] = 0.5  # last row (0, 0, 0.5, 1): not affine
+    with pytest.raises(hip_mod.PMError):
+        ctx.add_mesh_instance(obj, proj, w2o)
+    ctx.add_mesh_instance(obj, o2w, w2o)
+    ctx.close()
+
+
 def test_eye_rays_mode(oracle_mod, hip_mod):
     sc = scenes.cornell_box(40, 24, nsamples=3)
     sc.camera = scenes.rays_from_pinhole(sc)

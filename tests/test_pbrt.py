@@ -278,3 +278,19 @@ def test_pbrt_render_matches_stage_driver(scene, renderer, tmp_path, hip_mod, or
     else:
         err = float(np.sqrt(np.mean((img.astype(np.float64) - want) ** 2)))
         assert err < 1e-3, f"{scene}: .pbrt image vs oracle RMSE {err}"
+
+
+@pytest.mark.gpu
+def test_pbrt_instancing_two_level_equals_flattened(tmp_path):
+    """killeroo-proxy.pbrt's ObjectInstance through the adapter: the two-level
+    path (pm_add_object_mesh + pm_add_mesh_instance, the default) and the
+    flattened one (PM_INSTANCING=0) render the same image bit for bit."""
+    imgs = {}
+    for inst in ("1", "0"):
+        out = tmp_path / ("img%s.pfm" % inst)
+        env = dict(os.environ, PM_INSTANCING=inst)
+        r = subprocess.run([CLI, "--pbrt", os.path.join(SCENES, "killeroo-proxy.pbrt"), "--paths", "16384",
+                            "--passes", "2", "--out", str(out)], capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stderr
+        imgs[inst] = read_pfm(out)
+    assert np.array_equal(imgs["1"].view(np.uint32), imgs["0"].view(np.uint32))
