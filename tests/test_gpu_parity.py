@@ -756,6 +756,37 @@ def test_two_level_instances(oracle_mod, hip_mod):
     assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
 
 
+def test_many_instances(hip_mod):
+    """48 instances of a 320-triangle object under random rotations, scales
+    and translations (a top tree of many instance boxes, overlapping object
+    trees): slots and grid renders of the two-level scene equal the flattened
+    scene's bit for bit."""
+    rng = np.random.RandomState(7)
+    sc = scenes.cornell_box(48, 40, blocks=False)
+    mat = sc.material(scenes.PM_MATTE, (0.6, 0.5, 0.4))
+    P, idx = scenes.figure_mesh(2)
+    sc.objects.append(dict(P=P, idx=idx, N=None, uv=None, material=mat, light=-1))
+    for _ in range(48):
+        s = rng.uniform(0.2, 0.45, 3)
+        t = rng.uniform([60, 0, 60], [480, 350, 480])
+        sc.instances.append((0, *scenes.affine(rng.uniform(-180, 180), rng.uniform(-40, 40), s, t)))
+    two = sc.load_into(hip_mod.Context(0))
+    flat = sc.load_into(hip_mod.Context(0), instancing=False)
+    try:
+        assert two.scene_info()["mode"] == "bvh-instanced"
+        p = RenderParams.defaults(paths_per_pass=32768)
+        for ctx in (two, flat):
+            ctx.trace_photons(p, 2, 0, 32768)
+        assert_bitexact(two.download_slots(32768 * 4), flat.download_slots(32768 * 4), "many-instance slots")
+        p.gather_structure = PM_GATHER_GRID
+        a, _ = two.render(p)
+        b, _ = flat.render(p)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    finally:
+        two.close()
+        flat.close()
+
+
 def test_instance_arguments(hip_mod):
     """pm_add_mesh_instance refuses an unknown object and a projective
     transform (the two-level path handles affine ones only); pm_add_object_mesh
