@@ -2063,6 +2063,37 @@ int pm_ppm_update_split(void *ptr, const pm_render_params *p, const void *d_coun
     return PM_OK;
 }
 
+int pm_ppm_update_split_radius(void *ptr, const pm_render_params *p, const void *d_count, void *d_ratio, void *stream) {
+    GETCTX(ptr);
+    int rc;
+    if ((rc = check_params(c, p))) return rc;
+    const int64_t n = view_size(c);
+    if (!d_count || !d_ratio) FAIL(c, PM_ERR_INVALID, "null count / ratio buffer");
+    hipStream_t s = pick(c, stream);
+    GatherParams G = gather_params(c, p);
+    const int fresh = c->rec_fresh ? 1 : 0;
+    G.r2init = c->rec_fresh_r2;
+    timer_begin(c, "update", s);
+    HIPCHK(c, launch_ppm_update_radius(G, (const int *)d_count, (float *)d_ratio, n, fresh, s));
+    timer_end(c, "update", s);
+    c->rec_fresh = false; /* every view record written (records outside the view are inactive) */
+    return PM_OK;
+}
+
+int pm_ppm_update_split_flux(void *ptr, const pm_render_params *p, const void *d_ratio, const void *d_flux_chunk,
+                             int64_t v_begin, int64_t v_count, void *stream) {
+    GETCTX(ptr);
+    int rc;
+    if ((rc = check_params(c, p))) return rc;
+    const int64_t n = view_size(c);
+    if (!d_ratio || (v_count > 0 && !d_flux_chunk) || v_begin < 0 || v_count < 0 || v_begin + v_count > n)
+        FAIL(c, PM_ERR_INVALID, "bad view chunk");
+    hipStream_t s = pick(c, stream);
+    GatherParams G = gather_params(c, p);
+    HIPCHK(c, launch_ppm_update_flux(G, (const float *)d_ratio, (const long long *)d_flux_chunk, v_begin, v_count, s));
+    return PM_OK;
+}
+
 int pm_ppm_update(void *ptr, const pm_render_params *p, const void *d_partial, int64_t rec_begin, int64_t rec_count,
                   void *stream) {
     GETCTX(ptr);

@@ -2579,6 +2579,63 @@ __global__ __launch_bounds__(256) void k_ppm_update_split(RecordsDev R, const in
     R.n[r] = N;
 }
 
+/* pm_ppm_update_split in two halves (ppm_apply's operations, split at the
+ * ratio): radius2 and N of every view record now, the ratio kept for the
+ * owner's flux update after the flux reduce-scatter has landed */
+__global__ __launch_bounds__(256) void k_ppm_update_radius(RecordsDev R, const int *count, float *ratio_out,
+                                                           int64_t n_view, float alpha, const uint32_t *view,
+                                                           int fresh, float r2init) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_view) return;
+    const int64_t r = view ? (int64_t)view[i] : i;
+    ratio_out[i] = -1.f;
+    const uint32_t flags = (uint32_t)__float_as_int(R.pos[r].w);
+    if (flags & (PM_REC_MISS | PM_REC_EXCEPTION | PM_REC_INVALID)) return;
+    const int M = count[i];
+    if (M <= 0 && !fresh) return;
+    float4 st = fresh ? make_float4(0.f, 0.f, 0.f, r2init) : R.state[r];
+    float N = fresh ? 0.f : R.n[r];
+    if (M > 0) { /* ppm_apply without the flux */
+        int totalPhotons = N + alpha * M;
+        float ratio = totalPhotons / (N + M);
+        st.w = st.w * ratio;
+        N = totalPhotons;
+        ratio_out[i] = ratio;
+    }
+    R.state[r] = st;
+    R.n[r] = N;
+}
+__global__ __launch_bounds__(256) void k_ppm_update_flux(RecordsDev R, const float *ratio, const long long *flux,
+                                                         int64_t v_begin, int64_t v_count, double inv,
+                                                         const uint32_t *view) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= v_count) return;
+    const int64_t i = v_begin + k;
+    const float q = ratio[i];
+    if (!(q >= 0.f)) return;
+    const int64_t r = view ? (int64_t)view[i] : i;
+    const long long *f = flux + 3 * k;
+    const v3 L = mk((float)((double)f[0] * inv), (float)((double)f[1] * inv), (float)((double)f[2] * inv));
+    float4 st = R.state[r];
+    const v3 fl = (xyz(st) + L) * q;
+    st.x = fl.x; st.y = fl.y; st.z = fl.z;
+    R.state[r] = st;
+}
+hipError_t launch_ppm_update_radius(const GatherParams &p, const int *count, float *ratio, int64_t n_view, int fresh,
+                                    hipStream_t s) {
+    if (n_view <= 0) return hipSuccess;
+    pm_launch(k_ppm_update_radius, dim3((unsigned)((n_view + 255) / 256)), dim3(256), 0, s, p.R, count, ratio, n_view,
+              p.ppm_alpha, p.view_list, fresh, p.r2init);
+    return hipGetLastError();
+}
+hipError_t launch_ppm_update_flux(const GatherParams &p, const float *ratio, const long long *flux, int64_t v_begin,
+                                  int64_t v_count, hipStream_t s) {
+    if (v_count <= 0) return hipSuccess;
+    pm_launch(k_ppm_update_flux, dim3((unsigned)((v_count + 255) / 256)), dim3(256), 0, s, p.R, ratio, flux, v_begin,
+              v_count, p.fx_inv, p.view_list);
+    return hipGetLastError();
+}
+
 hipError_t launch_ppm_update_split(const GatherParams &p, const int *count, const long long *flux, int64_t n_view,
                                    int64_t v_begin, int64_t v_count, int fresh, hipStream_t s) {
     if (n_view <= 0) return hipSuccess;

@@ -253,6 +253,10 @@ hipError_t launch_ppm_update(const GatherParams &p, const long long *partial, in
                              hipStream_t s);
 hipError_t launch_ppm_update_split(const GatherParams &p, const int *count, const long long *flux, int64_t n_view,
                                    int64_t v_begin, int64_t v_count, int fresh, hipStream_t s);
+hipError_t launch_ppm_update_radius(const GatherParams &p, const int *count, float *ratio, int64_t n_view, int fresh,
+                                    hipStream_t s);
+hipError_t launch_ppm_update_flux(const GatherParams &p, const float *ratio, const long long *flux, int64_t v_begin,
+                                  int64_t v_count, hipStream_t s);
 hipError_t launch_final(const FinalParams &p, hipStream_t s);
 /* list[0 .. *count) = the tiles (records [64 t, 64 t + 64)) holding an
  * active record, ascending, built on the device (flags: one byte per tile) */

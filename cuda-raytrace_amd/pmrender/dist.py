@@ -73,7 +73,8 @@ class _AsyncExchange:
     start() issues the count all-reduce and the flux reduce-scatter
     asynchronously, wait() joins them — afterwards `count` holds the global
     photon counts of every view record and `flux_chunk` this rank's slice of
-    the summed flux. The backend enters in one place: RCCL runs
+    the summed flux; wait_count() joins the count all-reduce alone (the radii
+    need it before the next gather, the flux only after it). The backend enters in one place: RCCL runs
     reduce_scatter_tensor on the device tensors; gloo (the CPU tests, and
     several ranks sharing one GPU) has no reduce-scatter, so it all-reduces
     the flux (on host copies for device tensors) and slices at wait()."""
@@ -97,14 +98,22 @@ class _AsyncExchange:
         self.works = [dist.all_reduce(count, async_op=True), dist.all_reduce(flux, async_op=True)]
         return self
 
+    def wait_count(self):
+        """the count all-reduce only (the flux reduce-scatter may continue)"""
+        if self.works[0] is not None:
+            self.works[0].wait()               # RCCL: the compute stream waits for the collective
+            self.works[0] = None
+            if self.gloo and self.host is not None:
+                self.count.copy_(self.host[0])
+
     def wait(self):
-        for w in self.works:
-            w.wait()                           # RCCL: the compute stream waits for the collectives
-        if self.gloo:
-            count, flux = self.host if self.host is not None else (self.count, self.flux)
-            if self.host is not None:
-                self.count.copy_(count)
-            self.flux_chunk.copy_(flux[self.rank * self.v_per:(self.rank + 1) * self.v_per])
+        self.wait_count()
+        if self.works[1] is not None:
+            self.works[1].wait()
+            self.works[1] = None
+            if self.gloo:
+                flux = self.host[1] if self.host is not None else self.flux
+                self.flux_chunk.copy_(flux[self.rank * self.v_per:(self.rank + 1) * self.v_per])
 
 
 class HipEngine:
@@ -160,6 +169,12 @@ class HipEngine:
 
     def ppm_update_split(self, p, count, flux_chunk, v_begin, v_count):
         self.ctx.ppm_update_split(p, count.data_ptr(), flux_chunk.data_ptr(), v_begin, v_count, self._s())
+
+    def ppm_update_radius(self, p, count, ratio):
+        self.ctx.ppm_update_split_radius(p, count.data_ptr(), ratio.data_ptr(), self._s())
+
+    def ppm_update_flux(self, p, ratio, flux_chunk, v_begin, v_count):
+        self.ctx.ppm_update_split_flux(p, ratio.data_ptr(), flux_chunk.data_ptr(), v_begin, v_count, self._s())
 
     def ppm_update(self, p, partial, rec_begin, rec_count):
         self.ctx.ppm_update(p, partial.data_ptr(), rec_begin, rec_count, self._s())
@@ -217,6 +232,7 @@ class PassRunner:
         self.padded = self.rec_per * world
         self.slot_buf = None
         self._pending = None
+        self._radius_done = False
         if self.multi and exchange == "reduce":
             # exchange over the active records only, owned in contiguous chunks of the view
             self.n_view = engine.set_record_view(True)
@@ -227,6 +243,14 @@ class PassRunner:
             self.count = engine.alloc((self.v_per * world,), torch.int32)
             self.flux = engine.alloc((self.v_per * world, 3), torch.int64)
             self.flux_chunk = engine.alloc((self.v_per, 3), torch.int64)
+            # engines with the two-phase update (HipEngine): the radii are
+            # updated as soon as the counts have landed, the flux only after the
+            # next pass's gather, so the flux reduce-scatter overlaps trace,
+            # build AND gather; the gather writes the other of two flux buffers
+            self.late_flux = callable(getattr(engine, "ppm_update_radius", None))
+            if self.late_flux:
+                self.flux_bufs = [self.flux, engine.alloc((self.v_per * world, 3), torch.int64)]
+                self.ratio = engine.alloc((self.v_per * world,), torch.float32)
         if self.multi and exchange == "allgather":
             self.slot_buf = engine.alloc((world * self.slots_per_rank * PHOTON_DTYPE.itemsize,), torch.uint8)
             engine.use_slot_buffer(self.slot_buf)
@@ -268,10 +292,25 @@ class PassRunner:
 
     def _start_exchange(self):
         self._pending = _AsyncExchange(self.count, self.flux, self.flux_chunk, self.rank, self.v_per).start()
+        self._radius_done = False
+
+    def _finish_radius(self):
+        """Two-phase update, first half: global counts -> every radius (before the next gather)."""
+        if self._pending is None or self._radius_done:
+            return
+        self._pending.wait_count()
+        self.e.ppm_update_radius(self.p, self.count, self.ratio)
+        self._radius_done = True
 
     def _finish_exchange(self):
         """Complete the previous pass: global counts -> every radius; summed flux -> owner's chunk."""
         if self._pending is None:
+            return
+        if self.late_flux:
+            self._finish_radius()
+            self._pending.wait()
+            self._pending = None
+            self.e.ppm_update_flux(self.p, self.ratio, self.flux_chunk, self.v_begin, self.v_count)
             return
         self._pending.wait()
         self._pending = None
@@ -296,9 +335,18 @@ class PassRunner:
             if self.paths:
                 e.trace_photons(p, pass_index, self.path_begin, self.paths, self.path_begin)
                 e.build_photon_map(p, self.slots_mine)
-            self._finish_exchange()
-            if reset:
-                e.reset_records(p)                  # deferred: the split update below consumes it
+            if self.late_flux:
+                # the previous pass's radii before this gather (before a reset,
+                # which the next radius update consumes), its flux after it
+                self._finish_radius()
+                if reset:
+                    e.reset_records(p)
+                if self._pending is not None and self.flux is self._pending.flux:
+                    self.flux = self.flux_bufs[1] if self.flux is self.flux_bufs[0] else self.flux_bufs[0]
+            else:
+                self._finish_exchange()
+                if reset:
+                    e.reset_records(p)              # deferred: the split update below consumes it
             if self.paths:
                 e.gather_split(p, self.count, self.flux)
             else:
@@ -307,6 +355,8 @@ class PassRunner:
                 # would otherwise come from stale slots of an earlier pass)
                 self.count.zero_()
                 self.flux.zero_()
+            if self.late_flux:
+                self._finish_exchange()             # the previous pass's flux (its reduce-scatter ran meanwhile)
             self._start_exchange()
             if self.time_exchange:
                 self._timed(self._finish_exchange)

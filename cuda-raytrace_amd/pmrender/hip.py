@@ -66,6 +66,8 @@ def load_library(path=None):
         "pm_gather_partial": (c_int, [vp, ctypes.POINTER(RenderParams), vp, vp]),
         "pm_gather_split": (c_int, [vp, ctypes.POINTER(RenderParams), vp, vp, vp]),
         "pm_ppm_update_split": (c_int, [vp, ctypes.POINTER(RenderParams), vp, vp, i64, i64, vp]),
+        "pm_ppm_update_split_radius": (c_int, [vp, ctypes.POINTER(RenderParams), vp, vp, vp]),
+        "pm_ppm_update_split_flux": (c_int, [vp, ctypes.POINTER(RenderParams), vp, vp, i64, i64, vp]),
         "pm_ppm_update": (c_int, [vp, ctypes.POINTER(RenderParams), vp, i64, i64, vp]),
         "pm_final": (c_int, [vp, c_double, i64, i64, vp, vp]),
         "pm_num_records": (i64, [vp]),
@@ -278,6 +280,13 @@ class Context:
     def ppm_update_split(self, params, d_count, d_flux_chunk, v_begin, v_count, stream=None):
         self._chk(self.lib.pm_ppm_update_split(self.h, ctypes.byref(params), d_count, d_flux_chunk, int(v_begin),
                                                int(v_count), stream))
+
+    def ppm_update_split_radius(self, params, d_count, d_ratio, stream=None):
+        self._chk(self.lib.pm_ppm_update_split_radius(self.h, ctypes.byref(params), d_count, d_ratio, stream))
+
+    def ppm_update_split_flux(self, params, d_ratio, d_flux_chunk, v_begin, v_count, stream=None):
+        self._chk(self.lib.pm_ppm_update_split_flux(self.h, ctypes.byref(params), d_ratio, d_flux_chunk,
+                                                    int(v_begin), int(v_count), stream))
 
     def ppm_update(self, params, d_partial, rec_begin, rec_count, stream=None):
         self._chk(self.lib.pm_ppm_update(self.h, ctypes.byref(params), ctypes.c_void_p(d_partial), int(rec_begin),

@@ -263,6 +263,19 @@ int pm_gather_split(void *ctx, const pm_render_params *params, void *d_count, vo
  * reduce-scattered to the owner). Consumes a pending pm_reset_records. */
 int pm_ppm_update_split(void *ctx, const pm_render_params *params, const void *d_count, const void *d_flux_chunk,
                         int64_t v_begin, int64_t v_count, void *stream);
+/* The same update in two halves, so that the flux reduce-scatter of pass k
+ * can still be in flight while pass k + 1 gathers (pmrender/dist.py):
+ * pm_ppm_update_split_radius applies the global counts (d_count) to radius2
+ * and photon count of every view record and writes each record's ratio
+ * N'/(N + M) to d_ratio (n_view floats; < 0: nothing to apply), consuming a
+ * pending pm_reset_records (a fresh record's flux is set to 0);
+ * pm_ppm_update_split_flux later applies flux = (flux + L) * ratio to view
+ * records [v_begin, v_begin + v_count) from d_flux_chunk. Together they are
+ * pm_ppm_update_split bit for bit (gathering.cu:115-125 order of operations). */
+int pm_ppm_update_split_radius(void *ctx, const pm_render_params *params, const void *d_count, void *d_ratio,
+                               void *stream);
+int pm_ppm_update_split_flux(void *ctx, const pm_render_params *params, const void *d_ratio,
+                             const void *d_flux_chunk, int64_t v_begin, int64_t v_count, void *stream);
 /* Record view of pm_gather_partial, pm_ppm_update, pm_get_radius2 and
  * pm_set_radius2 (their rec_begin / rec_count and buffers index the view):
  * active_only = 0 -> all records (default); 1 -> only active records (not

@@ -25,7 +25,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, exchange, outdir, backend="gloo"):
+def _worker(rank, world, port, exchange, outdir, backend="gloo", reset_at=-1, fused=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -43,11 +43,13 @@ def _worker(rank, world, port, exchange, outdir, backend="gloo"):
     p = RenderParams.defaults(paths_per_pass=PATHS, initial_radius2=25.0)
     with torch.cuda.stream(torch.cuda.Stream()):
         eng = HipEngine(ctx)
+        if fused:   # the one-kernel update after both collectives (pm_ppm_update_split)
+            eng.ppm_update_radius = None
         ctx.eye_pass(p, eng._s())
         runner = PassRunner(eng, p, rank, world, exchange, force_exchange=True)
         assert runner.multi
         for k in range(PASSES):
-            runner.step(k)
+            runner.step(k, reset=k == reset_at)
         out = torch.zeros((runner.n_records, 3), dtype=torch.float32, device="cuda")
         runner.final_gather(float(runner.emitted_per_pass * PASSES), out)
         torch.cuda.synchronize()
@@ -57,13 +59,15 @@ def _worker(rank, world, port, exchange, outdir, backend="gloo"):
     dist.destroy_process_group()
 
 
-def _single_context_image(world, hip_mod):
+def _single_context_image(world, hip_mod, reset_at=-1):
     from pmrender import scenes
     from pmrender.abi import RenderParams
     ref = scenes.cornell_box(W, H).load_into(hip_mod.Context(0))
     p = RenderParams.defaults(paths_per_pass=world * PATHS, initial_radius2=25.0)
     ref.eye_pass(p)
     for k in range(PASSES):
+        if k == reset_at:
+            ref.reset_records(p)
         ref.trace_photons(p, k, 0, world * PATHS)
         ref.build_photon_map(p)
         ref.gather(p)
@@ -102,3 +106,19 @@ def test_rccl_world1_exchange_matches_single_context(exchange, tmp_path, hip_mod
     got = np.load(tmp_path / "img0.npy")
     assert (want > 0).any()
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"RCCL world-1 {exchange} image differs"
+
+
+@pytest.mark.parametrize("mode", ["late", "fused"])
+def test_two_ranks_reduce_with_reset(mode, tmp_path, hip_mod):
+    """The reduce exchange's two update schedules — radii from the counts
+    before the next gather and flux after it (the default, so the flux
+    reduce-scatter overlaps the next pass's gather), or one fused update after
+    both collectives — with a PPM reset between passes (bench.py's per-step
+    pattern): images bit for bit equal to one context."""
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), "reduce", str(tmp_path), "gloo", 1, mode == "fused"),
+                       nprocs=world, join=True, start_method="spawn")
+    want = _single_context_image(world, hip_mod, reset_at=1)
+    for r in range(world):
+        got = np.load(tmp_path / f"img{r}.npy")
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"rank {r} image differs ({mode})"
