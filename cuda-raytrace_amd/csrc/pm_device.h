@@ -663,6 +663,9 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
  * == 2) or, in builds with PM_BVH4_QUANT=0, 128-B float nodes (S.wide == 1).
  * C3 trace 5.16 -> 4.75 ms per 1M paths (same box): half the bytes per visit,
  * 24 byte conversions + 24 multiply-adds more per node. */
+#ifndef PM_QSLAB
+#define PM_QSLAB 1 /* quantized planes folded into the slab test (node4_decode) */
+#endif
 #ifndef PM_BVH4_QUANT
 #define PM_BVH4_QUANT 1 /* build-time node format: 1 = quantized 64-B nodes, 0 = 128-B float nodes */
 #endif
@@ -695,13 +698,35 @@ PMD void node4_decode(const uint4 w0, const uint4 w1, const uint4 w2, const uint
         const float sx = __uint_as_float(((w0.w & 0xffu) - 1u) << 23);
         const float sy = __uint_as_float((((w0.w >> 8) & 0xffu) - 1u) << 23);
         const float sz = __uint_as_float((((w0.w >> 16) & 0xffu) - 1u) << 23);
+#if PM_QSLAB
+        /* the plane o + q 2^e and the slab (plane - O) / d folded: t = q a + b
+         * with a = 2^e / d, b = o / d - O / d per node, one FMA per plane
+         * instead of a decode FMA and a slab FMA. Not the decoded plane's t
+         * bit for bit, but within a few ulps of the coordinates, far inside
+         * the 1e-4 relative pad of every primitive box (culling stays
+         * conservative; closest hits do not depend on it) */
+        const float ax = sx * inv.x, ay = sy * inv.y, az = sz * inv.z;
+        const float bx = __builtin_fmaf(ox, inv.x, -oinv.x), by = __builtin_fmaf(oy, inv.y, -oinv.y),
+                    bz = __builtin_fmaf(oz, inv.z, -oinv.z);
+        const float bxH = __builtin_fmaf(ox, inv.x, -oinvH.x), byH = __builtin_fmaf(oy, inv.y, -oinvH.y),
+                    bzH = __builtin_fmaf(oz, inv.z, -oinvH.z);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t sh = 8u * (uint32_t)k;
+            const float t0x = __builtin_fmaf((float)((w1.x >> sh) & 0xffu), ax, bx);
+            const float t0y = __builtin_fmaf((float)((w1.y >> sh) & 0xffu), ay, by);
+            const float t0z = __builtin_fmaf((float)((w1.z >> sh) & 0xffu), az, bz);
+            const float t1x = __builtin_fmaf((float)((w1.w >> sh) & 0xffu), ax, bxH);
+            const float t1y = __builtin_fmaf((float)((w2.x >> sh) & 0xffu), ay, byH);
+            const float t1z = __builtin_fmaf((float)((w2.y >> sh) & 0xffu), az, bzH);
+            const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
+            const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), tmax));
+            t[k] = tn <= tf ? tn : __int_as_float(0x7f800000);
+        }
+#else
         /* o + q * 2^e as one FMA: the product is exact, so the single
          * rounding is the add's — the encoder's decode, bit for bit */
-#ifdef PM_QDECODE_MULADD
-#define QDEC(o, q, s) ((o) + (q) * (s))
-#else
 #define QDEC(o, q, s) __builtin_fmaf((q), (s), (o))
-#endif
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t sh = 8u * (uint32_t)k;
@@ -710,10 +735,11 @@ PMD void node4_decode(const uint4 w0, const uint4 w1, const uint4 w2, const uint
             const float hy = QDEC(oy, (float)((w2.x >> sh) & 0xffu), sy), hz = QDEC(oz, (float)((w2.y >> sh) & 0xffu), sz);
             t[k] = box_near(lx, ly, lz, hx, hy, hz, oinv, inv, tmin, tmax, oinvH);
         }
+#undef QDEC
+#endif
         c[0] = (int)w3.x; c[1] = (int)w3.y; c[2] = (int)w3.z; c[3] = (int)w3.w;
         n[0] = (int)(int16_t)(w2.z & 0xffffu); n[1] = (int)(int16_t)(w2.z >> 16);
         n[2] = (int)(int16_t)(w2.w & 0xffffu); n[3] = (int)(int16_t)(w2.w >> 16);
-#undef QDEC
     }
 }
 PMD void node4_test(const SceneDev &S, int cur, const v3 &oinv, const v3 &inv, float tmin, float tmax, float t[4],
