@@ -80,6 +80,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="oracle threads (default: this process's CPU share: OMP_NUM_THREADS, else its affinity set)")
     ap.add_argument("--no-census", action="store_true")
+    ap.add_argument("--pipeline", type=int, default=int(os.environ.get("PM_BENCH_PIPELINE", "0")),
+                    help="1: each timed pass's gather overlaps the next pass's trace (second stream; one GPU)")
     return ap.parse_args()
 
 
@@ -261,15 +263,19 @@ def main():
         # next pass of one render (Halton permutation of pass k, radii shrink)
         pass_no = [0]
 
-        def step():
+        def step(ahead=False):
+            # ahead: with --pipeline, issue the next step's trace during this one's gather
             if progressive:
-                runner.step(pass_no[0], reset=pass_no[0] == 0)
+                runner.step(pass_no[0], reset=pass_no[0] == 0, next_pass=pass_no[0] + 1 if ahead else None)
                 pass_no[0] += 1
             else:
-                runner.step(0, reset=True)
+                runner.step(0, reset=True, next_pass=0 if ahead else None)
 
-        for _ in range(args.warmup):
-            step()
+        runner.pipeline = bool(args.pipeline) and world == 1
+        # the pipeline never reaches across the timed region's edges: the first
+        # timed step traces its own pass, the last issues no trace ahead
+        for i in range(args.warmup):
+            step(ahead=i < args.warmup - 1)
         runner.flush()
         torch.cuda.synchronize()
         setup_s = time.perf_counter() - t_setup
@@ -281,8 +287,8 @@ def main():
         # every timed stage boundary costs a few us of idle GPU
         ctx.set_stage_timing("gather")
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
+        for i in range(args.steps):
+            step(ahead=i < args.steps - 1)
         runner.flush()                 # the last pass's exchange is part of the timed work
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
@@ -299,6 +305,7 @@ def main():
         # N > 1: each pass's exchange also timed here, run to completion at
         # once (in the timed steps it overlaps the next pass's trace + build)
         runner.time_exchange = world > 1
+        runner.pipeline = False            # stage times of passes run one after another
         split_passes = min(args.steps, 10)
         for _ in range(split_passes):
             step()
@@ -553,6 +560,7 @@ def main():
             "radius2": radius2,
             "exchange": args.exchange if world > 1 else "none",
             "parallelism": f"photon-shard x{world}" if world > 1 else "single",
+            "pass_pipeline": bool(args.pipeline) and world == 1,
         },
         "mgather_samples_per_s": round(g_points * args.steps / elapsed / 1e6, 3),
         "kernel_rates": {

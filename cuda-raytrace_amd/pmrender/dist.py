@@ -233,6 +233,11 @@ class PassRunner:
         self.slot_buf = None
         self._pending = None
         self._radius_done = False
+        # pass pipelining (one GPU, HipEngine): the next pass's trace runs on a
+        # second stream while this pass gathers (set by the caller, step(next_pass=))
+        self.pipeline = False
+        self._ahead = None             # (pass, event) of a trace issued ahead
+        self._tstream = None
         if self.multi and exchange == "reduce":
             # exchange over the active records only, owned in contiguous chunks of the view
             self.n_view = engine.set_record_view(True)
@@ -317,13 +322,23 @@ class PassRunner:
         self.e.ppm_update_split(self.p, self.count, self.flux_chunk, self.v_begin, self.v_count)
 
     def flush(self):
-        """Finish the exchange still in flight (call before reading records or timing)."""
+        """Finish the exchange still in flight (call before reading records or
+        timing); a trace issued ahead for a pass that will not run is joined."""
         self._finish_exchange()
+        if self._ahead is not None:
+            torch.cuda.current_stream().wait_event(self._ahead[1])
+            self._ahead = None
 
-    def step(self, pass_index, reset=False):
-        """One PPM pass: trace this rank's paths, build, gather (+ exchange)."""
+    def step(self, pass_index, reset=False, next_pass=None):
+        """One PPM pass: trace this rank's paths, build, gather (+ exchange).
+        With self.pipeline (one GPU), next_pass = the pass the caller runs next:
+        its trace is issued here, on a second stream, between this pass's build
+        and gather."""
         e, p = self.e, self.p
         if not self.multi:
+            if self.pipeline:
+                self._step_pipelined(pass_index, reset, next_pass)
+                return
             if reset:
                 e.reset_records(p)
             e.trace_photons(p, pass_index, 0, self.paths, 0)
@@ -371,6 +386,40 @@ class PassRunner:
             e.build_photon_map(p, self.world * self.slots_per_rank)
             for b, c in self.bands[self.rank]:                  # replicated map, owned bands
                 e.gather_range(p, b, c)
+
+    def _step_pipelined(self, k, reset, next_pass):
+        """Pass k with the trace of pass next_pass overlapping its gather.
+        The trace writes the slots, the bucket keys / ranks and the cell
+        counts; the build reads them (and leaves the counts cleared) and the
+        gather reads only the built buckets and the records. So trace(k + 1)
+        may start once build(k) is done — on its own stream, concurrent with
+        gather(k) — and build(k + 1) follows gather(k) on the main stream. The
+        next pass's grid is chosen when its trace is issued, from the radii
+        binned by pass k - 1's gather (the grid sets only the cost)."""
+        e, p = self.e, self.p
+        main = torch.cuda.current_stream()
+        if self._ahead is not None and self._ahead[0] == k:
+            main.wait_event(self._ahead[1])
+        else:
+            if self._ahead is not None:          # a trace issued for another pass: let it land first
+                main.wait_event(self._ahead[1])
+            e.trace_photons(p, k, 0, self.paths, 0)
+        self._ahead = None
+        if reset:
+            e.reset_records(p)
+        e.build_photon_map(p, self.slots_mine)
+        if next_pass is not None:
+            if self._tstream is None:
+                self._tstream = torch.cuda.Stream()
+            built = torch.cuda.Event()
+            built.record(main)
+            self._tstream.wait_event(built)
+            with torch.cuda.stream(self._tstream):
+                e.trace_photons(p, next_pass, 0, self.paths, 0)
+                traced = torch.cuda.Event()
+                traced.record(self._tstream)
+            self._ahead = (next_pass, traced)
+        e.gather(p)
 
     def final_gather(self, emitted, out_full):
         """Final radiance of all records (record order) on every rank."""
