@@ -947,6 +947,9 @@ struct SpillStack {
 #ifndef PM_TRAV_FUSE
 #define PM_TRAV_FUSE 1
 #endif
+#ifndef PM_LEAFQ_SHIFT
+#define PM_LEAFQ_SHIFT 1 /* trav_step: hit leaves enter the (empty) queue by selects; C3 trace 3.86-3.88 -> 3.81-3.85 ms */
+#endif
 /* false once the ray is done (best holds its closest hit, if any) */
 template <class C>
 PMD bool trav_step(const SceneDev &S, const Ray &ray, TravState &T, const SpillStack &stk, C &cen) {
@@ -975,6 +978,25 @@ PMD bool trav_step(const SceneDev &S, const Ray &ray, TravState &T, const SpillS
     float t[4];
     int c[4], n[4];
     node4_test(S, T.cur, T.oinv, T.inv, ray.tmin, T.best.t, t, c, n);
+#if PM_LEAFQ_SHIFT
+    /* the pending-leaf queue is empty here (a visit follows the last pending
+     * leaf's test): the hit leaves, in child order, enter it by shifting from
+     * the back — selects only, no branch per child */
+    {
+        uint32_t a0s = 0, a0n = 0, a1s = 0, a1n = 0, a2s = 0, a2n = 0, a3s = 0, a3n = 0;
+#pragma unroll
+        for (int k = 3; k >= 0; --k) {
+            if (t[k] != INF && n[k] > 0) {
+                a3s = a2s; a3n = a2n; a2s = a1s; a2n = a1n; a1s = a0s; a1n = a0n;
+                a0s = (uint32_t)~c[k]; a0n = (uint32_t)n[k];
+            }
+        }
+        T.l0s = a0s; T.l0n = a0n; T.l1s = a1s; T.l1n = a1n; T.l2s = a2s; T.l2n = a2n; T.l3s = a3s; T.l3n = a3n;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (n[k] != 0) t[k] = INF;
+#else
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         if (t[k] != INF && n[k] > 0) {
@@ -986,6 +1008,7 @@ PMD bool trav_step(const SceneDev &S, const Ray &ray, TravState &T, const SpillS
         }
         if (n[k] != 0) t[k] = INF;
     }
+#endif
     auto cs = [&](int a, int b) {
         if (t[b] < t[a]) { const float tt = t[a]; t[a] = t[b]; t[b] = tt; const int cc = c[a]; c[a] = c[b]; c[b] = cc; }
     };
