@@ -190,6 +190,9 @@ PMD float box_reach(float r2) { return __builtin_amdgcn_sqrtf(r2) * 1.0001f + 1e
 #ifndef PM_REC_EARLY
 #define PM_REC_EARLY 1
 #endif
+#ifndef PM_TILE_SIDX
+#define PM_TILE_SIDX 1
+#endif
 /* record prologue shared by the bucket kernels: flags, PPM state, BSDF, cell
  * box of [p - r', p + r'] (small: at most 2 x 2 rows, the grid's design case) */
 struct GatherRec {
@@ -669,7 +672,13 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
         const int64_t nt = P.n_tiles_dev ? (int64_t)*P.n_tiles_dev : P.n_tiles;
         if (w >= nt) return;
         if (TILE_BLOCK == 64) w = xcd_tile(w, nt);
+#if PM_TILE_SIDX
+        /* wave-uniform entry through the scalar cache (a vector load of it cost an L2 round trip) */
+        w = (int64_t)__builtin_amdgcn_readfirstlane((int)w);
+        r = P.rec_begin + (int64_t)((const_u32_ptr)P.tiles)[w] * 64 + lane;
+#else
         r = P.rec_begin + (int64_t)P.tiles[w] * 64 + lane;
+#endif
     } else {
         r = P.rec_begin + (int64_t)blockIdx.x * TILE_BLOCK + threadIdx.x;
     }
