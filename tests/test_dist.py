@@ -152,6 +152,61 @@ class OracleEngine:
         out.copy_(torch.from_numpy(self.view.astype(np.int32)))
 
 
+class OracleEngineLate(OracleEngine):
+    """The two-phase update of HipEngine (pm_ppm_update_split_radius /
+    _flux): radii and photon counts from the global counts before the next
+    gather, the owner's flux after it. Each flux update replays the oracle's
+    ppm_update from the record's state before its radius update, so the
+    arithmetic is the oracle's own."""
+
+    def __init__(self, scene, params):
+        super().__init__(scene, params)
+        self.pending = {}   # view index -> (radius2, photon_count, M) before the radius update
+
+    def reset_records(self, p):
+        super().reset_records(p)
+        self.pending = {}   # the reset discards the pass whose flux is still in flight
+
+    def ppm_update_radius(self, p, count, ratio):
+        import ctypes
+        lib = self.oracle.load()
+        fp = ctypes.POINTER(ctypes.c_float)
+        C, Q = count.numpy(), ratio.numpy()
+        n_view = len(self.view) if self.view is not None else len(self.recs)
+        self.pending = {}
+        for i in range(n_view):
+            r = self.recs[self._rec(i)]
+            Q[i] = -1.0
+            if r["flags"] & 7 or C[i] <= 0:
+                continue
+            r2 = np.float32([r["radius2"]])
+            N = np.float32([r["photon_count"]])
+            self.pending[i] = (r2[0], N[0], int(C[i]))
+            fl = np.zeros(3, np.float32)
+            lib.orc_ppm_update(r2.ctypes.data_as(fp), N.ctypes.data_as(fp), fl.ctypes.data_as(fp), int(C[i]),
+                               np.zeros(3, np.float32).ctypes.data_as(fp), float(p.ppm_alpha))
+            r["radius2"], r["photon_count"] = r2[0], N[0]
+            Q[i] = 1.0
+
+    def ppm_update_flux(self, p, ratio, flux_chunk, v_begin, v_count):
+        import ctypes
+        lib = self.oracle.load()
+        fp = ctypes.POINTER(ctypes.c_float)
+        F = flux_chunk.numpy()
+        for i in range(v_begin, v_begin + v_count):
+            if i not in self.pending:
+                continue
+            r2o, No, M = self.pending[i]
+            ri = self._rec(i)
+            r2 = np.float32([r2o])
+            N = np.float32([No])
+            fl = np.ascontiguousarray(self.recs[ri]["flux"], np.float32)
+            L = (F[i - v_begin].astype(np.float64) / self.FX).astype(np.float32)
+            lib.orc_ppm_update(r2.ctypes.data_as(fp), N.ctypes.data_as(fp), fl.ctypes.data_as(fp), M,
+                               L.ctypes.data_as(fp), float(p.ppm_alpha))
+            self.recs[ri]["flux"] = fl
+
+
 def _scene():
     from pmrender import scenes
     sc = scenes.cornell_box(40, 24)
@@ -159,7 +214,7 @@ def _scene():
     return sc
 
 
-def _worker(rank, world, port, exchange, outdir, total=None):
+def _worker(rank, world, port, exchange, outdir, total=None, late=False, reset_at=-1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -167,10 +222,11 @@ def _worker(rank, world, port, exchange, outdir, total=None):
     from pmrender.dist import PassRunner
     dist.init_process_group("gloo", rank=rank, world_size=world)
     p = RenderParams.defaults(paths_per_pass=PATHS, initial_radius2=25.0)
-    eng = OracleEngine(_scene(), p)
+    eng = (OracleEngineLate if late else OracleEngine)(_scene(), p)
     runner = PassRunner(eng, p, rank, world, exchange, force_exchange=world == 1, total_paths=total)
+    assert runner.multi and (exchange != "reduce" or runner.late_flux == late)
     for pass_index in range(2):
-        runner.step(pass_index)
+        runner.step(pass_index, reset=pass_index == reset_at)
     runner.flush()
     out = torch.zeros((runner.n_records, 3), dtype=torch.float32)
     runner.final_gather(float(runner.emitted_per_pass * 2), out)
@@ -192,14 +248,17 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _single_process_reference(world, total=None):
+def _single_process_reference(world, total=None, reset_at=-1):
     """1 process, the union of all ranks' global paths, kd gather."""
     import oracle
     n = total if total is not None else PATHS * world
     p = RenderParams.defaults(paths_per_pass=n, initial_radius2=25.0)
     orc = _scene().load_into(oracle.Oracle(nthreads=2))
     recs = orc.eye_pass(p)
+    init = recs.copy()
     for pass_index in range(2):
+        if pass_index == reset_at:
+            recs = init.copy()
         slots = orc.trace_photons(p, pass_index, 0, n)
         orc.gather(oracle.Oracle.build_kdtree(slots), recs, p)
     return recs, orc.final(recs, float(n * 2))
@@ -257,3 +316,24 @@ def test_allgather_bands_cover_every_record_once(n, unit, world):
         # interleaved: consecutive runs belong to consecutive ranks
         order = sorted((b, q) for q, r in enumerate(owned) for b, _ in r)
         assert [q for _, q in order[:world]] == list(range(world))
+
+
+@pytest.mark.parametrize("world,total,reset_at", [(2, None, -1), (3, 3 * PATHS + 1001, -1), (2, None, 1), (4, 5, -1)])
+def test_reduce_two_phase_update_matches_single_process(world, total, reset_at, tmp_path):
+    """The reduce exchange with HipEngine's update schedule (radii from the
+    all-reduced counts before the next gather, the owner's flux after it,
+    so the flux reduce-scatter overlaps a whole pass), over gloo: the same
+    records as one process — also across a reset between passes (the reset
+    discards the pass whose flux is still in flight) and with ranks that hold
+    no paths."""
+    mp.start_processes(_worker, args=(world, _free_port(), "reduce", str(tmp_path), total, True, reset_at),
+                       nprocs=world, join=True, start_method="spawn")
+    ref_recs, ref_img = _single_process_reference(world, total, reset_at)
+    idx = np.concatenate([np.load(tmp_path / f"idx{r}.npy") for r in range(world)])
+    recs = np.concatenate([np.load(tmp_path / f"recs{r}.npy") for r in range(world)]).view(RECORD_DTYPE)
+    assert np.array_equal(np.sort(idx), np.nonzero((ref_recs["flags"] & 7) == 0)[0])
+    ref_recs = ref_recs[idx]
+    assert np.array_equal(recs["photon_count"], ref_recs["photon_count"])
+    assert np.array_equal(recs["radius2"].view(np.uint32), ref_recs["radius2"].view(np.uint32))
+    np.testing.assert_allclose(recs["flux"], ref_recs["flux"], rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(np.load(tmp_path / "img0.npy"), ref_img, rtol=1e-5, atol=1e-6)
