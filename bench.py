@@ -13,9 +13,13 @@ records) already resident in HBM:
 `value` = emitted photon paths over all ranks / step time (whole job,
 Mphotons/s); `mgather_samples_per_s` = gather points / step time.
 
-Single GPU: `python bench.py`. N GPUs (one process per GPU):
+Single GPU: `python bench.py`. N GPUs (one process per GPU): either
 `python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N`
-(weak scaling: the config's paths per GPU). Strong scaling: `--total-paths T`
+or plain `python bench.py --gpus N`, which starts that launcher itself as a
+child process (before torch is imported) and relays rank 0's JSON line
+(weak scaling: the config's paths per GPU). At N > 1 the line also carries the
+other exchange (`alt_exchange`: the slot all-gather when the headline ran the
+reduce exchange), timed the same way after the headline steps. Strong scaling: `--total-paths T`
 splits T paths per pass over the N ranks (`--config c4 --total-paths 4194304`
 is BASELINE C4's 16,777,216 photon slots at any N) and reports "scaling":
 "strong". At N > 1 `stages_ms.exchange` is the per-pass exchange (RCCL
@@ -80,6 +84,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="oracle threads (default: this process's CPU share: OMP_NUM_THREADS, else its affinity set)")
     ap.add_argument("--no-census", action="store_true")
+    ap.add_argument("--no-alt-exchange", action="store_true",
+                    help="N > 1: skip timing the other exchange (reduce <-> allgather) after the headline steps")
     ap.add_argument("--pipeline", type=int, default=int(os.environ.get("PM_BENCH_PIPELINE", "0")),
                     help="1: each timed pass's gather overlaps the next pass's trace (second stream; one GPU)")
     return ap.parse_args()
@@ -116,7 +122,7 @@ def load_pmc_traffic(kernel_prefix, config, field="hbm_bytes_per_launch"):
     and this config; else (None, reason)."""
     sha = kernel_src_sha()
     path, d = None, None
-    for rnd in ("r05", "r04", "r03", "r02"):      # the newest committed profile of these sources
+    for rnd in ("r06", "r05", "r04", "r03", "r02"):      # the newest committed profile of these sources
         cand = os.path.join(ROOT, "profiles", rnd, "pmc_traffic_%s.json" % config)
         if os.path.exists(cand):
             with open(cand) as f:
@@ -203,6 +209,34 @@ def cpu_baseline(scene, params, threads, cfg):
     }
 
 
+def self_launch(n):
+    """`bench.py --gpus N` (N > 1) started as a plain process: start
+    torch.distributed.run with N ranks on this node as a CHILD process (this
+    process has not imported torch or touched the GPU), relay rank 0's JSON
+    line on stdout (everything else the ranks print goes to stderr) and exit
+    with the launcher's code."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env["PM_BENCH_LAUNCHED"] = "1"
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    for line in proc.stdout:
+        s = line.strip()
+        if s.startswith("{"):
+            try:
+                json.loads(s)
+                print(s, flush=True)
+                continue
+            except ValueError:
+                pass
+        sys.stderr.write(line)
+    return proc.wait()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -210,7 +244,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world:
         if world == 1 and args.gpus > 1:
-            sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+            if os.environ.get("PM_BENCH_LAUNCHED") == "1":
+                sys.exit("bench.py: the self-launched ranks have no WORLD_SIZE")
+            sys.exit(self_launch(args.gpus))
         args.gpus = world
 
     import torch  # first: the renderer then shares torch's HIP runtime (one runtime per process)
@@ -346,6 +382,56 @@ def main():
                 torch.cuda.synchronize()
                 canonical = ctx.gather_counters(full=True)
                 ctx.set_counting(False)
+
+        # N > 1: the other exchange timed the same way (K steps between barriers,
+        # max over ranks), so the line carries both designs: reduce (default)
+        # and the all-gather of photon slots that north_star names
+        alt = None
+        if world > 1 and not args.no_alt_exchange and not knn:
+            alt_x = "allgather" if args.exchange == "reduce" else "reduce"
+            if args.exchange == "reduce":
+                ctx.set_record_view(False)             # band gathers address records, not the active view
+            runner2 = PassRunner(eng, p, rank, world, alt_x, total_paths=args.total_paths)
+            pass2 = [0]
+
+            def step2():
+                if progressive:
+                    runner2.step(pass2[0], reset=pass2[0] == 0)
+                    pass2[0] += 1
+                else:
+                    runner2.step(0, reset=True)
+
+            for _ in range(max(1, args.warmup)):
+                step2()
+            runner2.flush()
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+            ctx.set_stage_timing("")
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                step2()
+            runner2.flush()
+            torch.cuda.synchronize()
+            el2 = time.perf_counter() - t1
+            dist.barrier()
+            t = torch.tensor([el2], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el2 = float(t.item())
+            xb2 = (40 * runner2.slots_per_rank * world if alt_x == "allgather"
+                   else 28 * runner2.v_per * world)
+            alt = {"exchange": alt_x,
+                   "value": round(runner2.total * args.steps / el2 / 1e6, 3),
+                   "unit": "Mphotons/s",
+                   "ms_per_step": round(el2 / args.steps * 1e3, 5),
+                   "mgather_samples_per_s": round(scene.width * scene.height * args.steps / el2 / 1e6, 3),
+                   "exchange_bytes_per_pass_per_rank": int(xb2),
+                   "note": ("40-B photon slots all-gathered into a replicated map, each rank gathers its 8-row "
+                            "bands (north_star's design)" if alt_x == "allgather" else
+                            "photon-count all-reduce + flux reduce-scatter, every rank gathers every active record "
+                            "against its own photon shard") + "; timed like the headline steps, after them"}
+            if args.exchange == "reduce":
+                ctx.set_record_view(True)              # the census / record reads below use the full set
 
     n_rec = ctx.num_records()
     recs = ctx.download_records()
@@ -563,6 +649,8 @@ def main():
             "pass_pipeline": bool(args.pipeline) and world == 1,
         },
         "mgather_samples_per_s": round(g_points * args.steps / elapsed / 1e6, 3),
+        # the reference's "Total photons" convention (4 slots per path): value x 4
+        "mphoton_slots_per_s": round(paths_total * int(p.max_photon_count) * args.steps / elapsed / 1e6, 3),
         "kernel_rates": {
             "trace_mphotons_per_s": round(runner.paths / (stages["trace"] * 1e-3) / 1e6, 2) if "trace" in stages else None,
             # records this rank gathered per pass over its per-pass gather time
@@ -575,7 +663,9 @@ def main():
     }
     if exchange is not None:
         out["exchange"] = exchange
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if alt is not None:
+        out["alt_exchange"] = alt
+    if rank == 0 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(scene, RenderParams.defaults(paths_per_pass=args.paths, **est),
                                                args.cpu_threads or default_cpu_threads(), args.config)

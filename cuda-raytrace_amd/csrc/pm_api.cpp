@@ -73,7 +73,7 @@ struct Ctx {
     std::vector<float> P, N, UV;
     std::vector<HMesh> meshes;
     std::vector<HTri> tris;
-    uint32_t next_tri_id = 0;    /* global ids handed out to triangles (meshes and instances) */
+    int64_t next_tri_id = 0;     /* global ids handed out to triangles (meshes and instances); < 2^31 */
     std::vector<HObj> objs;
     std::vector<HInst> insts;
     int64_t obj_tris_stored = 0; /* object triangles in the committed scene (each mesh once) */
@@ -175,6 +175,7 @@ struct Ctx {
     DevBuf d_r2hist;
     uint32_t *h_r2hist = nullptr, *h_r2hist_dev = nullptr; /* host-mapped R2_BINS words, its device address */
     hipEvent_t r2_event = nullptr;
+    hipStream_t r2_stream = nullptr; /* the stream the last histogram reduce ran on (r2_event) */
     bool r2_wanted = false;    /* a progressive pass asked for the radii (no histogram otherwise) */
     bool r2_accum = false;     /* d_r2hist holds bins of this pass's gathers (every band), not yet reduced */
     bool r2_dirty = false;     /* d_r2hist holds bins of invalidated radii: zero before binning again */
@@ -895,6 +896,7 @@ int pm_add_trimesh(void *ptr, const float *P, int nverts, const int *idx, int nt
     if (material < 0 || material >= (int)c->materials.size()) FAIL(c, PM_ERR_INVALID, "bad material id %d", material);
     for (int64_t i = 0; i < 3 * (int64_t)ntris; ++i)
         if (idx[i] < 0 || idx[i] >= nverts) FAIL(c, PM_ERR_INVALID, "vertex index %d out of range", idx[i]);
+    if (c->next_tri_id + ntris >= ((int64_t)1 << 31)) FAIL(c, PM_ERR_INVALID, "too many triangles (global ids reach 2^31)");
     int64_t base = (int64_t)c->P.size() / 3;
     c->P.insert(c->P.end(), P, P + 3 * (size_t)nverts);
     if (N) c->N.insert(c->N.end(), N, N + 3 * (size_t)nverts);
@@ -905,7 +907,7 @@ int pm_add_trimesh(void *ptr, const float *P, int nverts, const int *idx, int nt
     c->meshes.push_back(HMesh{material, light, N != nullptr, uv != nullptr});
     for (int t = 0; t < ntris; ++t)
         c->tris.push_back(HTri{{(int)(base + idx[3 * t]), (int)(base + idx[3 * t + 1]), (int)(base + idx[3 * t + 2])}, mid,
-                               c->next_tri_id++});
+                               (uint32_t)c->next_tri_id++});
     c->committed = false;
     return PM_OK;
 }
@@ -937,12 +939,17 @@ int pm_add_mesh_instance(void *ptr, int object, const float o2w[16], const float
     if (!o2w || !w2o) FAIL(c, PM_ERR_INVALID, "null instance transform");
     if (o2w[12] != 0.f || o2w[13] != 0.f || o2w[14] != 0.f || o2w[15] != 1.f)
         FAIL(c, PM_ERR_INVALID, "instance transform is not affine (flatten it with pm_add_trimesh)");
+    /* every instance takes global ids for all of its triangles (as the
+     * flattened scene would): heavy instancing must not wrap them */
+    const int64_t n_obj_tris = (int64_t)(c->objs[object].idx.size() / 3);
+    if (c->next_tri_id + n_obj_tris >= ((int64_t)1 << 31))
+        FAIL(c, PM_ERR_INVALID, "too many instanced triangles (global ids reach 2^31)");
     HInst in;
     in.obj = object;
     std::memcpy(in.m, o2w, sizeof in.m);
     std::memcpy(in.minv, w2o, sizeof in.minv);
-    in.gid_base = c->next_tri_id;
-    c->next_tri_id += (uint32_t)(c->objs[object].idx.size() / 3);
+    in.gid_base = (uint32_t)c->next_tri_id;
+    c->next_tri_id += n_obj_tris;
     c->insts.push_back(in);
     c->committed = false;
     return PM_OK;
@@ -1585,6 +1592,7 @@ static float grid_radius2(Ctx *c, const pm_render_params *p, bool refresh, hipSt
             launch_r2hist_reduce(c->d_r2hist.as<uint32_t>(), c->h_r2hist_dev, s) == hipSuccess &&
             hipEventRecord(c->r2_event, s) == hipSuccess) {
             c->r2_pending = true;
+            c->r2_stream = s;
             c->r2_accum = false;
             c->r2_valid = true;
             c->r2_hist_init = c->r2_accum_init;
@@ -1883,6 +1891,11 @@ static int gather_common(Ctx *c, const pm_render_params *p, long long *partial, 
                       !split && c->gather_kernel == PM_GK_TILE &&
                       !c->counting && c->grid_quantile > 0.0 && c->r2_wanted;
     if (hist) {
+        /* the reduce that read and re-zeroed the bins may have run on another
+         * stream (a trace issued ahead on a second stream chose its grid:
+         * dist.py's pipelined passes): this gather bins (and may clear) only
+         * after it — otherwise the two race on d_r2hist */
+        if (c->r2_pending && c->r2_stream != s) HIPCHK(c, hipStreamWaitEvent(s, c->r2_event, 0));
         if (c->r2_accum && c->r2_accum_init != p->initial_radius2) { c->r2_accum = false; c->r2_dirty = true; }
         if (!c->d_r2hist.p) {
             HIPCHK(c, c->d_r2hist.ensure(R2_COPIES * R2_BINS * 4));

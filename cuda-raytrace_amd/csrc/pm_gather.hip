@@ -1065,13 +1065,21 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
  * (k_final). Both passes visit rows in rings around the query's row,
  * nearest first, and skip rows / cells beyond the current bound. */
 PMD float sq(float x) { return x * x; }
-/* kNN sums: each term trunc(c * sc) is an integer <= 2^22
+/* kNN sums: each term round(c * sc) is an integer <= 2^22
  * (knn_fx), at most PM_KNN_MAX = 2^6 of them per record, so their int32 sum
  * is exact (< 2^28): order-free like the PPM gather's int64 fixed point, at
  * one rounding, one conversion and one integer add per channel (round 4
  * summed terms <= 2^47 in double: two double-rate operations per term; the
  * scalar-stream SUM pass is 41 % of the kNN gather) */
 struct Kx3 { int x, y, z; };
+/* a kNN term to the nearest integer, floor(x + 0.5) in one instruction
+ * (v_cvt_rpi_i32_f32): an error of at most half a unit of the record's fixed
+ * point per term, without the one-sided bias of truncation (round 6) */
+PMD int knn_rnd(float x) {
+    int r;
+    asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
 /* Dot(Faceforward(ns, wo), wi) > 0 for the photon's wi = (wx, b.w, wz) */
 PMD bool knn_facing(v3 ns, bool back, const float4 &b, float wx, float wz) {
     float dn = dot(ns, mk(wx, b.w, wz));
@@ -1084,9 +1092,9 @@ PMD void knn_add(Kx3 &a, float d2, float inv, float sc, const float4 &b) {
     const float s = 1.f - d2 * inv;
     const float kk = 3.f * INV_PI * s * s;
     /* sc is a power of two: k * (inv * sc) * alpha rounds like (k * inv * alpha) * sc;
-     * terms are truncated to integers (one conversion; a bias below 2^-20 of a term) */
+     * terms are rounded to the nearest integer (knn_rnd: <= 1/2 unit each) */
     const float ks = kk * (inv * sc);
-    a.x += (int)(ks * b.x); a.y += (int)(ks * b.y); a.z += (int)(ks * b.z);
+    a.x += knn_rnd(ks * b.x); a.y += knn_rnd(ks * b.y); a.z += knn_rnd(ks * b.z);
 }
 /* distance, in cell units, from coordinate u (cell units) to cell c of an
  * axis with dim cells — the border cells extend to infinity (cell_axis
@@ -2207,9 +2215,9 @@ __global__ __launch_bounds__(64) KS_OCC void k_gather_knn_ss(GatherParams P) {
                                     if (!(h0 && dn.x > 0.f)) ki.x = 0.f;
                                     if (!(h1 && dn.y > 0.f)) ki.y = 0.f;
                                     const f2 cr = ki * R, cg = ki * G, cb = ki * Bl;
-                                    acc.x += (int)cr.x + (int)cr.y; /* knn_add's truncation */
-                                    acc.y += (int)cg.x + (int)cg.y;
-                                    acc.z += (int)cb.x + (int)cb.y;
+                                    acc.x += knn_rnd(cr.x) + knn_rnd(cr.y); /* knn_add's rounding */
+                                    acc.y += knn_rnd(cg.x) + knn_rnd(cg.y);
+                                    acc.z += knn_rnd(cb.x) + knn_rnd(cb.y);
                                 }
                             }
                         }

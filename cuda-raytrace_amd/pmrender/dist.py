@@ -323,7 +323,11 @@ class PassRunner:
 
     def flush(self):
         """Finish the exchange still in flight (call before reading records or
-        timing); a trace issued ahead for a pass that will not run is joined."""
+        timing); a trace issued ahead for a pass that will not run is joined.
+        The records are those of the passes that ran; the photon slot buffer
+        (pm_download_slots) and the fused bucket counts, however, then hold
+        the abandoned pass's photons — the next step traces its own pass
+        again, but a caller that reads the slots after flush() reads those."""
         self._finish_exchange()
         if self._ahead is not None:
             torch.cuda.current_stream().wait_event(self._ahead[1])

@@ -126,6 +126,39 @@ def test_c2_full_records(oracle_mod, hip_mod):
         ctx.close()
 
 
+def test_c2_bench_step_twice(oracle_mod, hip_mod):
+    """C2 at full size, bench.py's step run twice in one context: reset ->
+    trace -> build -> gather. The first full-range gather of a context runs
+    the cost-recording tile instance over the unsorted tile list; the second
+    is the timed instance (k_gather_tile over the cost-sorted list, counts
+    fused into the trace) — compared here with the oracle: M -> N', r^2
+    exact, flux <= 2e-5 (gathering.cu:104-126); and equal to the first
+    gather bit for bit (exact fixed-point sums)."""
+    sc = scenes.cornell_box(1920, 1080)
+    ctx, orc = make_pair(sc, oracle_mod, hip_mod)
+    try:
+        p = RenderParams.defaults()
+        n = p.paths_per_pass
+        ctx.eye_pass(p)
+        recs = orc.eye_pass(p)
+        first = None
+        for step in range(2):
+            ctx.reset_records(p)
+            ctx.trace_photons(p, 0, 0, n)
+            ctx.build_photon_map(p, n * 4)
+            ctx.gather(p)
+            if step == 0:
+                first = ctx.download_records()
+        got = ctx.download_records()
+    finally:
+        ctx.close()
+    slots = orc.trace_photons(p, 0, 0, n)
+    orc.gather(orc.build_kdtree(slots), recs, p)
+    assert (recs["photon_count"] > 0).sum() > 500_000
+    compare_gathered_records(got, recs)
+    assert_bitexact(got, first, "C2 second (sorted-list) gather vs the first (unsorted, cost-recording)")
+
+
 def shard_records(ctx, orc, p, path_begin):
     """One rank's photon shard at its global path ids (slots of paths
     [path_begin, path_begin + paths_per_pass)), gathered over all records:
@@ -180,11 +213,29 @@ def test_c4_allgather_map(oracle_mod, hip_mod):
         2,097,152-slot maps gathered one by one into per-record partial sums
         (int32 M, int64 fixed-point flux), summed, then one split update —
         are the full map's records bit for bit (exact fixed-point sums)."""
+    _allgather_map(scenes.cornell_box(3840, 2160), 3840, 2160, 524_288, 8_000_000, 500_000,
+                   oracle_mod, hip_mod)
+
+
+def test_c5_allgather_map(oracle_mod, hip_mod):
+    """C5's photon budget in its 8-GPU all-gather form: the caustic scene at
+    1080p, 8 ranks x 1,048,576 paths = 8,388,608 paths = 33,554,432 slots
+    all-gathered into one map (twice C4's), the bands of ranks 0 and 7
+    gathered against it vs the oracle's kd-tree gather (M -> N', r^2 exact,
+    flux <= 2e-5), slots bit-exact, and the 8 reduce-mode shares summed equal
+    to the full map bit for bit — as test_c4_allgather_map."""
+    _allgather_map(scenes.caustic_scene(1920, 1080), 1920, 1080, 1_048_576, 5_000_000, 100_000,
+                   oracle_mod, hip_mod)
+
+
+def _allgather_map(sc, W, H, per, min_valid, min_lit, oracle_mod, hip_mod):
+    """one context holds what every rank of 8 holds after the slot all-gather
+    (the 8 shards traced at their global path ids are one trace of all the
+    paths, slot for slot) and gathers the bands of ranks 0 and 7"""
     import torch
     from pmrender.dist import _bands
-    W, H, world, per = 3840, 2160, 8, 524_288
+    world = 8
     total = world * per
-    sc = scenes.cornell_box(W, H)
     p = RenderParams.defaults(paths_per_pass=total)
     ctx, orc = make_pair(sc, oracle_mod, hip_mod)
     try:
@@ -203,17 +254,17 @@ def test_c4_allgather_map(oracle_mod, hip_mod):
     finally:
         ctx.close()
     ref_slots = orc.trace_photons(p, 0, 0, total)
-    assert_bitexact(slots, ref_slots, "C4 all-gathered slots (16,777,216)")
+    assert_bitexact(slots, ref_slots, f"all-gathered slots ({total * 4:,})")
     del slots
     nvalid = int((ref_slots["bits"] & 1).sum())
-    assert info["valid"] == nvalid > 8_000_000, (info, nvalid)
+    assert info["valid"] == nvalid > min_valid, (info, nvalid)
     recs = orc.eye_pass(p)
     idx = np.concatenate([np.arange(b, b + c) for runs in mine for b, c in runs])
-    assert len(idx) > 1_900_000  # 2 x 3,840 x 2,160 / 8 less the bands short of a whole run
+    assert len(idx) > 0.9 * 2 * W * H / world  # two ranks' bands, less the bands short of a whole run
     sub = recs[idx].copy()
     orc.gather(orc.build_kdtree(ref_slots), sub, p)
     del ref_slots
-    assert (sub["photon_count"] > 0).sum() > 500_000
+    assert (sub["photon_count"] > 0).sum() > min_lit
     compare_gathered_records(got[idx], sub)
     rest = np.ones(n, bool)
     rest[idx] = False
@@ -275,14 +326,16 @@ def test_c3_full_workload(oracle_mod, hip_mod):
 
 
 def test_c5_progressive(oracle_mod, hip_mod):
-    """C5 substitute: caustic scene (glass + mirror spheres), 1080p, 4
-    progressive passes of 1,048,576 paths (shrinking radii, PPM state carried):
-    per-record N', r^2 exact after the passes, flux within tolerance, image
-    RMSE < 1e-3."""
+    """C5 substitute at its full photon budget: caustic scene (glass + mirror
+    spheres), 1080p, 8 progressive passes of 1,048,576 paths = 8,388,608
+    paths = 33,554,432 slots (shrinking radii, PPM state
+    carried, later passes on the cost-sorted tile list and the radius
+    histogram's grid): per-record N', r^2 exact after the passes, flux within
+    tolerance, image RMSE < 1e-3."""
     sc = scenes.caustic_scene(1920, 1080)
     ctx, orc = make_pair(sc, oracle_mod, hip_mod)
     try:
-        paths, passes = 1_048_576, 4
+        paths, passes = 1_048_576, 8
         p = RenderParams.defaults(paths_per_pass=paths)
         got, ref = stage_records(ctx, orc, p, passes=passes)
         compare_gathered_records(got, ref, flux_rtol=5e-5)
@@ -300,7 +353,7 @@ def test_c2_full_knn(oracle_mod, hip_mod, monkeypatch):
     the bench's kNN line): the tile kernel equals the per-lane heap kernel
     bit for bit, and both match the oracle's pbrt kd-tree lookup (found
     count and r_k^2 exact, flux to fp32 summation order)."""
-    from parity_util import compare_knn_records
+    from parity_util import compare_knn_records, knn_term_floor
     from pmrender.abi import PM_ESTIMATOR_KNN
     sc = scenes.cornell_box(1920, 1080)
     orc = sc.load_into(oracle_mod.Oracle())
@@ -327,4 +380,5 @@ def test_c2_full_knn(oracle_mod, hip_mod, monkeypatch):
     orc.gather(orc.build_kdtree(slots), ref, p)
     act = (ref["flags"] & 7) == 0
     assert act.sum() > 1_000_000 and (ref["photon_count"][act] == 50).mean() > 0.2
-    compare_knn_records(outs["tile"], ref["photon_count"].astype(np.int64), ref["radius2"], ref["flux"])
+    compare_knn_records(outs["tile"], ref["photon_count"].astype(np.int64), ref["radius2"], ref["flux"],
+                        floor=knn_term_floor(sc, ref["photon_count"], ref["radius2"]))

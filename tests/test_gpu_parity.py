@@ -857,7 +857,7 @@ def test_knn_gather_parity(cornell, K, radius2):
     """k_gather_knn over the photon buckets vs the oracle's pbrt kd-tree
     lookup (shrinking radius, PhotonProcess heap): photons found and r_k^2
     bit-exact, flux to fp32 summation order; two passes accumulate."""
-    from parity_util import compare_knn_records
+    from parity_util import compare_knn_records, knn_term_floor
     from pmrender.abi import PM_ESTIMATOR_KNN
     ctx, orc = cornell
     p = RenderParams.defaults(paths_per_pass=16384, initial_radius2=radius2, estimator=PM_ESTIMATOR_KNN,
@@ -865,16 +865,18 @@ def test_knn_gather_parity(cornell, K, radius2):
     recs = orc.eye_pass(p)
     ref = recs.copy()
     ctx.upload_records(recs)
+    floor = np.zeros(len(recs))
     for pass_index in range(2):
         slots = orc.trace_photons(p, pass_index, 0, 16384)
         ctx.upload_slots(slots)
         ctx.build_photon_map(p, len(slots))
         ctx.gather(p)
         orc.gather(orc.build_kdtree(slots), ref, p)
+        floor += knn_term_floor(scenes.cornell_box(), ref["photon_count"], ref["radius2"])
     got = ctx.download_records()
     act = (ref["flags"] & 7) == 0
     assert (ref["photon_count"][act] == K).mean() > 0.2 and (ref["photon_count"][act] < K).any()
-    compare_knn_records(got, ref["photon_count"].astype(np.int64), ref["radius2"], ref["flux"])
+    compare_knn_records(got, ref["photon_count"].astype(np.int64), ref["radius2"], ref["flux"], floor=floor)
 
 
 def test_knn_render_parity(cornell):

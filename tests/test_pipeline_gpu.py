@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "cuda-raytrace_amd")]
 
 
-def _run(scene_fn, paths, passes, pipeline, reset_every, r2, drop_last=False):
+def _run(scene_fn, paths, passes, pipeline, reset_every, r2, drop_last=False, hint=None):
     from pmrender import hip
     from pmrender.abi import RenderParams
     from pmrender.dist import HipEngine, PassRunner
@@ -33,6 +33,8 @@ def _run(scene_fn, paths, passes, pipeline, reset_every, r2, drop_last=False):
         for k in range(passes):
             k_pass = 0 if reset_every else k
             nxt = None if k == passes - 1 and not drop_last else (0 if reset_every else k + 1)
+            if hint is not None:
+                nxt = hint(k)
             runner.step(k_pass, reset=reset_every or k == 0, next_pass=nxt)
         runner.flush()
         torch.cuda.synchronize()
@@ -70,4 +72,16 @@ def test_pipelined_unused_trace_ahead_is_joined():
     fn = lambda: scenes.cornell_box(96, 64)  # noqa: E731
     seq = _run(fn, 16384, 3, False, False, 16.0)
     pip = _run(fn, 16384, 3, True, False, 16.0, drop_last=True)
+    _same(seq, pip)
+
+
+def test_pipelined_mismatched_trace_ahead_is_redone():
+    """traces issued ahead for passes that do not come next (the caller's
+    next_pass hint is wrong on every other pass): the mismatched trace lands
+    first, the pass traces its own photons again (and re-zeroes the fused
+    cell counts), so the records equal the sequential passes bit for bit"""
+    from pmrender import scenes
+    fn = lambda: scenes.cornell_box(96, 64)  # noqa: E731
+    seq = _run(fn, 16384, 4, False, False, 16.0)
+    pip = _run(fn, 16384, 4, True, False, 16.0, hint=lambda k: k + 1 if k % 2 else k + 3)
     _same(seq, pip)
