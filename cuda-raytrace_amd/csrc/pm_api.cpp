@@ -1262,7 +1262,11 @@ int pm_commit(void *ptr) {
     SceneLayout L;
     int rc;
     bool built = false;
-    if (ni == 0 && gpu_bvh_wanted((int64_t)prims.size())) {
+    /* env PM_BVH8=1 (round 6): scenes traversed from HBM get an 8-wide
+     * quantized tree (host build; pm_build.h quantize_bvh8) instead of the
+     * 4-wide one; instanced scenes keep 4-wide trees */
+    const bool bvh8 = ni == 0 && getenv("PM_BVH8") && atoi(getenv("PM_BVH8")) != 0;
+    if (ni == 0 && !bvh8 && gpu_bvh_wanted((int64_t)prims.size())) {
         if ((rc = commit_gpu_bvh(c, prims, nt, L, built, ptimes))) return rc;
         if (ptimes && built) fprintf(stderr, "pm_commit: device build, total %.1f ms\n", tms(t_commit0, tnow()));
     }
@@ -1355,7 +1359,21 @@ int pm_commit(void *ptr) {
         /* scenes traversed from HBM also get the 4-wide BVH (half the dependent
          * node fetches per ray; binary leaves of one primitive);
          * instanced scenes always (their objects' trees are 4-wide) */
-        if (blob.size() > LDS_SCENE_MAX || ni > 0) {
+        bool wide8 = false;
+        if (bvh8 && blob.size() > LDS_SCENE_MAX) {
+            Bvh4Out w;
+            collapse_bvh8(bvh, 1, w);
+            std::vector<uint32_t> qn;
+            if (quantize_bvh8(w.nodes, bvh.refs, qn) && w.max_stack <= BVH8_STACK) {
+                L.o_wnodes = put(qn.data(), qn.size() * sizeof(uint32_t));
+                L.wide = 3;
+                L.wide_stack = w.max_stack;
+                c->bvh4_nodes = (int64_t)(qn.size() / 32);
+                c->bvh4_depth = w.depth;
+                wide8 = true;
+            }
+        }
+        if (!wide8 && (blob.size() > LDS_SCENE_MAX || ni > 0)) {
             {
                 Bvh4Out w;
                 const auto t_c0 = tnow();
@@ -1458,7 +1476,7 @@ int pm_commit(void *ptr) {
      * MODE_GLOBAL query to traverse4): its exact stack bound sizes the LDS
      * stacks, not the binary tree's depth — k_trace_pool's 256-thread blocks
      * then fit four per CU (its VGPR occupancy) instead of three */
-    if (L.wide) S.stack_depth = std::min(BVH_STACK, std::max(2, L.wide_stack + 1));
+    if (L.wide) S.stack_depth = std::min(L.wide == 3 ? BVH8_STACK : BVH_STACK, std::max(2, L.wide_stack + 1));
     for (int a = 0; a < 3; ++a) { c->bbox_lo[a] = blo[a]; c->bbox_hi[a] = bhi[a]; }
     double em = 0.0, kd = 1.0;
     for (const LightDev &L : c->lights) {
@@ -1687,16 +1705,17 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0) cus = 256;
         const size_t lds = (size_t)lstk * TRACE_BLOCK * 4 + c->S.lds_bytes;
-        int per_cu = trace_pool_waves_per_cu(lds, 0);
+        const int w8 = c->S.wide == 3;
+        int per_cu = trace_pool_waves_per_cu(lds, 0, w8);
         if (T.hold) { /* pooled kernel: the held deposits' LDS must not cost resident waves */
-            const int per_cu_h = trace_pool_waves_per_cu(lds, 1);
+            const int per_cu_h = trace_pool_waves_per_cu(lds, 1, w8);
             if (per_cu_h < per_cu) T.hold = 0;
             else per_cu = per_cu_h;
         }
         const int64_t waves = (int64_t)cus * (per_cu > 0 ? per_cu : 16);
         /* any pool size works (the wave's cursor hands out paths to dead lanes) */
         const int64_t per = std::max<int64_t>(1, (path_count + waves - 1) / waves);
-        T.pool_paths = c->trace_pool ? per : 0;
+        T.pool_paths = c->trace_pool || c->S.wide == 3 ? per : 0; /* 8-wide: its deeper stacks need the pooled kernel's spill */
         if (lstk < c->S.stack_depth) {
             const int64_t blocks = ((path_count + per - 1) / per + TRACE_BLOCK / 64 - 1) / (TRACE_BLOCK / 64);
             const int64_t threads = blocks * TRACE_BLOCK;
@@ -2613,7 +2632,7 @@ int pm_scene_section(void *ptr, int section, void *out, int64_t max_bytes, int64
     case PM_SCENE_TRI_SHADE: src = S.tri_shade; n = 32 * (int64_t)S.n_tris; break;
     case PM_SCENE_TRI_ID: src = S.tri_id; n = 4 * (int64_t)S.n_tris; break;
     case PM_SCENE_TRI_INFO: src = S.tri_info; n = 16 * (int64_t)S.n_tris; break;
-    case PM_SCENE_BVH4: src = S.wnodes; n = S.wide ? (S.wide == 2 ? 64 : 128) * c->bvh4_nodes : 0; break;
+    case PM_SCENE_BVH4: src = S.wnodes; n = S.wide ? (S.wide == 2 ? 64 : 128) * c->bvh4_nodes : 0; break; /* 3: 8-wide, 128 B */
     case PM_SCENE_INSTANCES: src = S.insts; n = 128 * (int64_t)S.n_inst; break;
     case PM_SCENE_OBJ_TRIS: src = S.obj_v; n = S.n_inst ? 48 * c->obj_tris_stored : 0; break;
     default: FAIL(c, PM_ERR_INVALID, "unknown scene section %d", section);

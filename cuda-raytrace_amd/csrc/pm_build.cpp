@@ -307,15 +307,17 @@ struct Collapse {
         l.code = ~f; l.count = t;
         return l;
     }
-    /* emits the 4-wide node of binary node `node`; returns (its index, stack need) */
+    int width = 4; /* children per node: 4 (collapse_bvh4) or 8 (collapse_bvh8) */
+    /* emits the W-wide node of binary node `node` (8 W floats); returns (its index, stack need) */
     int emit(int node, int level, int &need) {
         depth = std::max(depth, level + 1);
+        const int W = width, NF = 8 * W;
         std::vector<Bin> ch;
         for (int k = 0; k < 2; ++k) {
             Bin c = child_of(node, k);
             if (c.count >= 0) ch.push_back(as_leaf(c));
         }
-        while (ch.size() < 4) { /* open the largest internal child */
+        while ((int)ch.size() < W) { /* open the largest internal child */
             int best = -1;
             for (size_t i = 0; i < ch.size(); ++i)
                 if (ch[i].count == 0 && (best < 0 || ch[i].area() > ch[best].area())) best = (int)i;
@@ -327,12 +329,12 @@ struct Collapse {
                 if (c.count >= 0) ch.push_back(as_leaf(c));
             }
         }
-        const int id = (int)(out.size() / 32);
-        out.resize(out.size() + 32, 0.f);
+        const int id = (int)(out.size() / NF);
+        out.resize(out.size() + NF, 0.f);
         int internal = 0, sub = 0;
-        int codes[4], counts[4];
-        float box[6][4];
-        for (int k = 0; k < 4; ++k) {
+        int codes[8], counts[8];
+        float box[6][8];
+        for (int k = 0; k < W; ++k) {
             if (k < (int)ch.size()) {
                 for (int a = 0; a < 3; ++a) { box[a][k] = ch[k].lo[a]; box[3 + a][k] = ch[k].hi[a]; }
                 codes[k] = ch[k].code; counts[k] = ch[k].count;
@@ -348,11 +350,11 @@ struct Collapse {
                 ++internal;
                 sub = std::max(sub, cn);
             }
-        float *n = &out[(size_t)id * 32];
+        float *n = &out[(size_t)id * NF];
         for (int r = 0; r < 6; ++r)
-            for (int k = 0; k < 4; ++k) n[4 * r + k] = box[r][k];
-        std::memcpy(&n[24], codes, sizeof(codes));
-        std::memcpy(&n[28], counts, sizeof(counts));
+            for (int k = 0; k < W; ++k) n[W * r + k] = box[r][k];
+        std::memcpy(&n[6 * W], codes, W * sizeof(int));
+        std::memcpy(&n[7 * W], counts, W * sizeof(int));
         /* entering this node pushes all hit internal children but one */
         need = (internal > 0 ? internal - 1 : 0) + sub;
         return id;
@@ -360,16 +362,19 @@ struct Collapse {
 };
 } // namespace
 
-void collapse_bvh4(const BvhOut &bin, int leaf_prims, Bvh4Out &out) {
+static void collapse_bvhw(const BvhOut &bin, int leaf_prims, int width, Bvh4Out &out) {
     out.nodes.clear();
     const size_t nn = bin.nodes.size() / 16;
     Collapse C{bin, std::max(1, leaf_prims), out.nodes, std::vector<int>(nn, 0), std::vector<int>(nn, 0)};
+    C.width = width;
     C.ranges(0);
     int need = 0;
     C.emit(0, 0, need);
     out.depth = C.depth;
     out.max_stack = need + 1;
 }
+void collapse_bvh4(const BvhOut &bin, int leaf_prims, Bvh4Out &out) { collapse_bvhw(bin, leaf_prims, 4, out); }
+void collapse_bvh8(const BvhOut &bin, int leaf_prims, Bvh4Out &out) { collapse_bvhw(bin, leaf_prims, 8, out); }
 
 void bvh4_bfs_order(std::vector<float> &nodes) {
     const size_t nn = nodes.size() / 32;
@@ -481,6 +486,84 @@ static bool quantize_nodes(const std::vector<float> &nodes, const std::vector<ui
         std::memcpy(&w[12], codes, sizeof(codes));
     }
     return true;
+}
+
+/* 8-wide nodes (collapse_bvh8, 64 floats) -> 32 u32 (pm_build.h quantize_bvh8) */
+static bool quantize_nodes8(const std::vector<float> &nodes, const std::vector<uint32_t> &refs, std::vector<uint32_t> &q,
+                            int i0, int i1) {
+    for (size_t i = (size_t)i0; i < (size_t)i1; ++i) {
+        const float *n = &nodes[i * 64];
+        int codes[8], counts[8];
+        std::memcpy(codes, &n[48], sizeof(codes));
+        std::memcpy(counts, &n[56], sizeof(counts));
+        uint32_t *w = &q[i * 32];
+        uint32_t ebytes = 0;
+        for (int a = 0; a < 3; ++a) {
+            float lo = INFINITY, hi = -INFINITY;
+            for (int k = 0; k < 8; ++k)
+                if (counts[k] != -1) { lo = std::min(lo, n[8 * a + k]); hi = std::max(hi, n[8 * (3 + a) + k]); }
+            if (!(lo <= hi)) lo = hi = 0.f;
+            const double ext = (double)hi - (double)lo;
+            int e = -126;
+            if (ext > 0.0) {
+                int ex = 0;
+                (void)std::frexp(ext / 255.0, &ex);
+                e = std::max(-126, std::min(127, ex - 1));
+                while (e > -126 && std::ldexp(255.0, e - 1) >= ext) --e;
+            }
+            while (e < 127 && std::ldexp(255.0, e) < ext) ++e;
+            const double s = std::ldexp(1.0, e);
+            const float sf = std::ldexp(1.0f, e);
+            std::memcpy(&w[a], &lo, 4);
+            ebytes |= (uint32_t)(e + 128) << (8 * a);
+            uint32_t ql[2] = {0, 0}, qh[2] = {0, 0};
+            for (int k = 0; k < 8; ++k) {
+                uint32_t bl = 0, bh = 0;
+                if (counts[k] != -1) {
+                    const float clo = n[8 * a + k], chi = n[8 * (3 + a) + k];
+                    bl = (uint32_t)std::min(255.0, std::max(0.0, std::floor(((double)clo - lo) / s)));
+                    bh = (uint32_t)std::min(255.0, std::max(0.0, std::ceil(((double)chi - lo) / s)));
+                    while (bl > 0 && qdecode(lo, bl, sf) > clo) --bl;
+                    while (bh < 255 && qdecode(lo, bh, sf) < chi) ++bh;
+                    if (qdecode(lo, bl, sf) > clo || qdecode(lo, bh, sf) < chi) return false;
+                }
+                ql[k / 4] |= bl << (8 * (k & 3));
+                qh[k / 4] |= bh << (8 * (k & 3));
+            }
+            w[4 + 2 * a] = ql[0]; w[5 + 2 * a] = ql[1];
+            w[10 + 2 * a] = qh[0]; w[11 + 2 * a] = qh[1];
+        }
+        w[3] = ebytes;
+        for (int k = 0; k < 8; ++k) {
+            int32_t word;
+            if (counts[k] == 0) word = codes[k];                   /* internal node */
+            else if (counts[k] < 0) word = (int32_t)0x80000000;    /* empty slot (its box never hits) */
+            else {
+                if (counts[k] >= 16) return false;
+                uint32_t f = (uint32_t)~codes[k], tris = 0;
+                if (!refs.empty()) { /* a triangle run at consecutive storage slots? */
+                    const uint32_t s0 = refs[f] & 0x3fffffffu;
+                    bool t = true;
+                    for (int j = 0; j < counts[k] && t; ++j)
+                        t = (refs[f + j] >> 30) == 0u && (refs[f + j] & 0x3fffffffu) == s0 + (uint32_t)j;
+                    if (t) { f = s0; tris = 1; }
+                }
+                if (f >= (1u << 26)) return false;
+                word = ~(int32_t)((f << 5) | (tris << 4) | (uint32_t)counts[k]);
+            }
+            w[16 + k] = (uint32_t)word;
+        }
+    }
+    return true;
+}
+
+bool quantize_bvh8(const std::vector<float> &nodes, const std::vector<uint32_t> &refs, std::vector<uint32_t> &q) {
+    const size_t nn = nodes.size() / 64;
+    q.assign(nn * 32, 0u);
+    std::atomic<bool> ok{true};
+    const int parts = nn >= 4096 ? build_threads() : 1;
+    parallel_chunks(0, (int)nn, parts, [&](int, int i0, int i1) { if (!quantize_nodes8(nodes, refs, q, i0, i1)) ok = false; });
+    return ok;
 }
 
 int host_threads() { return build_threads(); }

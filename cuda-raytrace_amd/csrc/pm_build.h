@@ -83,6 +83,16 @@ constexpr int LEAF_TRIS = 0x4000;
  * top levels become the first nodes (the LDS nodelets of k_trace_pool) */
 void bvh4_bfs_order(std::vector<float> &nodes);
 bool quantize_bvh4(const std::vector<float> &nodes, const std::vector<uint32_t> &refs, std::vector<uint32_t> &q);
+/* 8-wide (round 6): the same collapse with eight children per node, 64
+ * floats = lox[8] loy[8] loz[8] hix[8] hiy[8] hiz[8] child[8] count[8] */
+void collapse_bvh8(const BvhOut &bin, int leaf_prims, Bvh4Out &out);
+/* 128-B quantized 8-wide nodes (32 u32): [0..2] origin, [3] exponent bytes
+ * (as quantize_bvh4), [4 + 2a, 5 + 2a] lo bytes of axis a (children 0-3,
+ * 4-7), [10 + 2a, 11 + 2a] hi bytes, [16..23] child words: an internal node
+ * index >= 0, INT_MIN for an empty slot, else a leaf ~((s << 5) | (tris << 4)
+ * | n): n < 16 refs from s, or (tris) n triangles at storage slots s ..
+ * (LEAF_TRIS), s < 2^26; [24..31] 0. False if a leaf cannot be coded so. */
+bool quantize_bvh8(const std::vector<float> &nodes, const std::vector<uint32_t> &refs, std::vector<uint32_t> &q);
 
 /* PLOC (parallel locally-ordered clustering, Meister & Bittner 2018), the
  * GPU builder's algorithm (pm_bvh_gpu.hip) restated on the host — the

@@ -588,6 +588,8 @@ PMD bool leaf_isect(const SceneDev &S, uint32_t start, uint32_t count, const Ray
  * child >= 0 internal node, child < 0 leaf with refs start ~child. */
 template <bool ANY, class C, bool INST = false>
 PMD bool traverse4(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int stride, C &cen);
+template <bool ANY, class C>
+PMD bool traverse8(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int stride, C &cen);
 
 template <bool ANY, int MODE, class C>
 PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int stride, C &cen) {
@@ -611,6 +613,7 @@ PMD bool traverse(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int 
     if constexpr (MODE == MODE_INST) {
         return traverse4<ANY, C, true>(S, ray, best, stack, stride, cen);
     } else if constexpr (MODE == MODE_GLOBAL) {
+        if (S.wide == 3) return traverse8<ANY>(S, ray, best, stack, stride, cen);
         if (S.wide) return traverse4<ANY>(S, ray, best, stack, stride, cen);
     }
     uint32_t l0s = 0, l0n = 0, l1s = 0, l1n = 0; /* pending leaves: first ref, count (0 = none) */
@@ -1020,6 +1023,155 @@ PMD bool trav_step(const SceneDev &S, const Ray &ray, TravState &T, const SpillS
     else if (T.sp > 0) { --T.sp; T.cur = stk.get(T.sp); }
     else T.cur = -1;
     return T.l0n != 0 || T.cur >= 0;
+}
+
+/* ------------------------------------------------------- 8-wide trees */
+/* S.wide == 3 (round 6, pm_build.h quantize_bvh8): 128-B quantized nodes of
+ * eight children; the child word is the internal node index (>= 0), INT_MIN
+ * for an empty slot, or a leaf ~((s << 5) | (tris << 4) | n). One visit tests
+ * eight boxes: a third fewer node visits per ray than the 4-wide tree on
+ * C3's soup (tools/bvh_width_sim.cpp: 30.1 -> 20.1), each a dependent fetch. */
+constexpr int BVH8_EMPTY = (int)0x80000000;
+PMD void node8_test(const SceneDev &S, int cur, const v3 &oinv, const v3 &inv, float tmin, float tmax, float t[8],
+                    int c[8]) {
+    const uint4 *nd = reinterpret_cast<const uint4 *>(S.wnodes) + 8 * cur;
+    const uint4 w0 = nd[0], w1 = nd[1], w2 = nd[2], w3 = nd[3], w4 = nd[4], w5 = nd[5];
+    const float ox = __uint_as_float(w0.x), oy = __uint_as_float(w0.y), oz = __uint_as_float(w0.z);
+    const float sx = __uint_as_float(((w0.w & 0xffu) - 1u) << 23);
+    const float sy = __uint_as_float((((w0.w >> 8) & 0xffu) - 1u) << 23);
+    const float sz = __uint_as_float((((w0.w >> 16) & 0xffu) - 1u) << 23);
+    /* node4_decode's folded slab: t = q (2^e / d) + (o - O) / d, one FMA per plane */
+    const float ax = sx * inv.x, ay = sy * inv.y, az = sz * inv.z;
+    const float bx = __builtin_fmaf(ox, inv.x, -oinv.x), by = __builtin_fmaf(oy, inv.y, -oinv.y),
+                bz = __builtin_fmaf(oz, inv.z, -oinv.z);
+    /* byte planes: lo x (w1.x, w1.y), lo y (w1.z, w1.w), lo z (w2.x, w2.y),
+     * hi x (w2.z, w2.w), hi y (w3.x, w3.y), hi z (w3.z, w3.w) */
+    const uint32_t LX[2] = {w1.x, w1.y}, LY[2] = {w1.z, w1.w}, LZ[2] = {w2.x, w2.y};
+    const uint32_t HX[2] = {w2.z, w2.w}, HY[2] = {w3.x, w3.y}, HZ[2] = {w3.z, w3.w};
+    c[0] = (int)w4.x; c[1] = (int)w4.y; c[2] = (int)w4.z; c[3] = (int)w4.w;
+    c[4] = (int)w5.x; c[5] = (int)w5.y; c[6] = (int)w5.z; c[7] = (int)w5.w;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int h = k >> 2;
+        const uint32_t sh = 8u * (uint32_t)(k & 3);
+        const float t0x = __builtin_fmaf((float)((LX[h] >> sh) & 0xffu), ax, bx);
+        const float t0y = __builtin_fmaf((float)((LY[h] >> sh) & 0xffu), ay, by);
+        const float t0z = __builtin_fmaf((float)((LZ[h] >> sh) & 0xffu), az, bz);
+        const float t1x = __builtin_fmaf((float)((HX[h] >> sh) & 0xffu), ax, bx);
+        const float t1y = __builtin_fmaf((float)((HY[h] >> sh) & 0xffu), ay, by);
+        const float t1z = __builtin_fmaf((float)((HZ[h] >> sh) & 0xffu), az, bz);
+        const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), tmin));
+        const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), tmax));
+        t[k] = tn <= tf && c[k] != BVH8_EMPTY ? tn : __int_as_float(0x7f800000);
+    }
+}
+/* a leaf child word's test (its refs, or LEAF_TRIS slots) */
+template <bool ANY, class C>
+PMD bool leaf8_isect(const SceneDev &S, int word, const Ray &ray, Hit &best, C &cen) {
+    const uint32_t w = ~(uint32_t)word;
+    return leaf_isect<ANY, true>(S, w >> 5, (w & 15u) | ((w & 16u) ? 0x4000u : 0u), ray, best, cen);
+}
+/* a node's hit internal children near to far: 32-bit keys (the entry t's
+ * bits — non-negative floats order like their bits — with the low three
+ * replaced by the child's slot; misses and leaves sort last as ~0) through
+ * Batcher's odd-even merge network for 8 (19 min/max pairs). The order only
+ * steers the walk; hits do not depend on it (lowest-id tie-break). */
+PMD void sort8_keys(uint32_t k[8]) {
+    auto cs = [&](int a, int b) { const uint32_t lo = min(k[a], k[b]), hi = max(k[a], k[b]); k[a] = lo; k[b] = hi; };
+    cs(0, 1); cs(2, 3); cs(4, 5); cs(6, 7);
+    cs(0, 2); cs(1, 3); cs(4, 6); cs(5, 7);
+    cs(1, 2); cs(5, 6);
+    cs(0, 4); cs(1, 5); cs(2, 6); cs(3, 7);
+    cs(2, 4); cs(3, 5);
+    cs(1, 2); cs(3, 4); cs(5, 6);
+}
+PMD int child8(const int c[8], uint32_t slot) { /* c[slot & 7] by selects (no dynamic register index) */
+    const int a = (slot & 1u) ? c[1] : c[0], b = (slot & 1u) ? c[3] : c[2];
+    const int d = (slot & 1u) ? c[5] : c[4], e = (slot & 1u) ? c[7] : c[6];
+    const int f = (slot & 2u) ? b : a, g = (slot & 2u) ? e : d;
+    return (slot & 4u) ? g : f;
+}
+/* one node visit of the 8-wide walk: the hit leaves tested at once (every
+ * lane's, in one pass of the wave), the hit internal children sorted, the
+ * nearest returned in `next` (-1: none) and the others pushed far to near */
+template <bool ANY, class C, class Put>
+PMD bool visit8(const SceneDev &S, int node, const Ray &ray, const v3 &oinv, const v3 &inv, Hit &best, C &cen, int &next,
+                Put &&stack_put) {
+    float t[8];
+    int c[8];
+    node8_test(S, node, oinv, inv, ray.tmin, best.t, t, c);
+    const float INF = __int_as_float(0x7f800000);
+    uint32_t key[8], lm = 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if (t[k] != INF && c[k] < 0) lm |= 1u << k;
+        key[k] = t[k] != INF && c[k] >= 0 ? (__float_as_uint(t[k]) & ~7u) | (uint32_t)k : 0xffffffffu;
+    }
+    /* the hit leaves, one per lane per round: as many rounds as the lane with
+     * the most (unrolled per slot, the wave ran the leaf code for every slot
+     * any lane hit) */
+    while (lm != 0u) {
+        const uint32_t k = (uint32_t)__builtin_ctz(lm);
+        lm &= lm - 1u;
+        if (leaf8_isect<ANY>(S, child8(c, k), ray, best, cen) && ANY) return true;
+    }
+    sort8_keys(key);
+#pragma unroll
+    for (int k = 7; k >= 1; --k)
+        if (key[k] != 0xffffffffu) stack_put(child8(c, key[k]));
+    next = key[0] != 0xffffffffu ? child8(c, key[0]) : -1;
+    return false;
+}
+/* one-call closest / any hit on the 8-wide tree (eye pass, shadow rays,
+ * per-lane kernels) */
+template <bool ANY, class C>
+PMD bool traverse8(const SceneDev &S, const Ray &ray, Hit &best, int *stack, int stride, C &cen) {
+    best.t = ray.tmax;
+    best.gid = 0xffffffffu;
+    best.ref = 0xffffffffu;
+    const v3 inv = safe_inv(ray.d);
+    const v3 oinv = mk(ray.o.x * inv.x, ray.o.y * inv.y, ray.o.z * inv.z);
+    int sp = 0, cur = 0, guard = 0;
+    while (cur >= 0 && guard <= S.n_nodes) {
+        ++guard;
+        cen.node();
+        int next = -1;
+        if (visit8<ANY>(S, cur, ray, oinv, inv, best, cen, next, [&](int v) { stack[sp * stride] = v; ++sp; }))
+            return true;
+        if (next >= 0) cur = next;
+        else if (sp > 0) { --sp; cur = stack[sp * stride]; }
+        else cur = -1;
+    }
+    return ANY ? false : best.ref != 0xffffffffu;
+}
+/* resumable 8-wide traversal for k_trace_pool (trav_step's contract): one
+ * node visit per step, its hit leaves tested in the same step (no pending
+ * queue: the registers of eight queued leaves spilled the pooled kernel) */
+struct TravState8 {
+    v3 inv, oinv;
+    Hit best;
+    int cur, sp, guard;
+};
+PMD void trav_begin(const Ray &ray, TravState8 &t) {
+    t.best.t = ray.tmax;
+    t.best.gid = 0xffffffffu;
+    t.best.ref = 0xffffffffu;
+    t.best.beta = t.best.gamma = 0.f;
+    t.inv = safe_inv(ray.d);
+    t.oinv = mk(ray.o.x * t.inv.x, ray.o.y * t.inv.y, ray.o.z * t.inv.z);
+    t.cur = 0; t.sp = 0; t.guard = 0;
+}
+template <class C>
+PMD bool trav_step(const SceneDev &S, const Ray &ray, TravState8 &T, const SpillStack &stk, C &cen) {
+    if (T.cur < 0 || T.guard > S.n_nodes) return false;
+    ++T.guard;
+    cen.node();
+    int next = -1;
+    visit8<false>(S, T.cur, ray, T.oinv, T.inv, T.best, cen, next, [&](int v) { stk.put(T.sp, v); ++T.sp; });
+    if (next >= 0) T.cur = next;
+    else if (T.sp > 0) { --T.sp; T.cur = stk.get(T.sp); }
+    else T.cur = -1;
+    return T.cur >= 0;
 }
 
 template <bool ANY, int MODE>

@@ -34,6 +34,10 @@ inline void pm_launch(F kernel, dim3 grid, dim3 block, uint32_t shmem, hipStream
 constexpr int EYE_BLOCK = 128;     /* traversal kernels: LDS stack column per lane */
 constexpr int TRACE_BLOCK = 256;    /* k_trace: 4 waves compact paths together */
 constexpr int BVH_STACK = BVH_STACK_DEPTH; /* >= max BVH depth (builder enforces it) */
+/* the 8-wide tree's exact stack bound (seven pushes per level) runs deeper:
+ * its stacks hold up to 96 entries (k_trace_pool8 keeps PM_POOL_STACK of them
+ * in LDS and spills the rest; the eye pass's LDS columns take the bound) */
+constexpr int BVH8_STACK = 96;
 constexpr int GATHER_BLOCK = 256;
 /* k_gather_tile: waves per block. Its waves never synchronise with each
  * other, and a block's LDS is held until its last wave ends, so with several
@@ -229,7 +233,7 @@ hipError_t launch_eye(const EyeParams &p, hipStream_t s);
 hipError_t launch_simple(const EyeParams &p, float *out, hipStream_t s);
 /* writes every slot of its paths (deposits, then zeros); count: census */
 /* resident waves of k_trace_pool per CU with `lds` bytes of dynamic LDS per block */
-int trace_pool_waves_per_cu(size_t lds, int hold);
+int trace_pool_waves_per_cu(size_t lds, int hold, int w8 = 0);
 size_t scan_scratch_words(int64_t n);
 int trace_lane_waves_per_cu(const SceneDev &S, size_t lds, int hold);
 /* adaptive-grid histogram: sum the R2_COPIES copies into host-mapped

@@ -544,7 +544,8 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_lane(TraceParams P) {
 constexpr int POOL_STEPS = PM_POOL_STEPS, POOL_SHADE_MIN = PM_POOL_SHADE_MIN;
 enum { PHASE_DEAD = 0, PHASE_TRAV = 1, PHASE_SHADE = 2 };
 
-template <int COUNT, int HOLD>
+/* W8: the 8-wide tree (S.wide == 3, TravState8) */
+template <int COUNT, int HOLD, int W8>
 /* 5 waves/SIMD: 96 VGPRs (102 unconstrained -> 4 waves), no scratch; with
  * the LDS stacks capped at 31 entries (PM_POOL_STACK, the rest spilled) five
  * 256-thread blocks fit a CU. C3 trace (same box): 4.59-4.61 ms at 4 waves,
@@ -557,7 +558,12 @@ template <int COUNT, int HOLD>
 #else
 #define POOL_OCC
 #endif
-__global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams P) { /* ~102 VGPRs without SLP: 4 waves/SIMD */
+/* the 8-wide walk needs 117 VGPRs unconstrained: 4 waves/SIMD (113, no
+ * scratch) by default; 5 spills 88 B */
+#ifndef PM_POOL8_EU
+#define PM_POOL8_EU 4
+#endif
+__device__ __forceinline__ void trace_pool_body(TraceParams P) { /* ~102 VGPRs without SLP: 4 waves/SIMD */
     extern __shared__ __attribute__((aligned(16))) int stk[];
     __shared__ uint32_t perm[28];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -576,7 +582,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
     const int64_t wend = wbegin + P.pool_paths < P.path_count ? wbegin + P.pool_paths : P.path_count;
     int64_t cursor = wbegin; /* wave-uniform: next unassigned path of the pool */
     PathState st;
-    TravState tr;
+    typename std::conditional<W8 != 0, TravState8, TravState>::type tr;
     Held held;
     if (HOLD) held.col = reinterpret_cast<uint32_t *>(stk + lstk * TRACE_BLOCK) + tid; /* after the stacks */
     int phase = PHASE_DEAD;
@@ -627,12 +633,21 @@ __global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams
     }
 }
 
+template <int COUNT, int HOLD>
+__global__ __launch_bounds__(TRACE_BLOCK) POOL_OCC void k_trace_pool(TraceParams P) { trace_pool_body<COUNT, HOLD, 0>(P); }
+template <int COUNT, int HOLD>
+__global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(PM_POOL8_EU, PM_POOL8_EU)))
+void k_trace_pool8(TraceParams P) { trace_pool_body<COUNT, HOLD, 1>(P); }
+
 /* resident waves of the pooled kernel per CU at this LDS size (0 if unknown) */
-int trace_pool_waves_per_cu(size_t lds, int hold) { /* lds: the stacks */
+int trace_pool_waves_per_cu(size_t lds, int hold, int w8) { /* lds: the stacks */
     int blocks = 0;
     if (hold) lds += (size_t)HOLD_WORDS * TRACE_BLOCK * 4;
-    const hipError_t e = hold ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0, 1>, TRACE_BLOCK, lds)
-                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0, 0>, TRACE_BLOCK, lds);
+    const hipError_t e =
+        w8 ? (hold ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool8<0, 1>, TRACE_BLOCK, lds)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool8<0, 0>, TRACE_BLOCK, lds))
+           : (hold ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0, 1>, TRACE_BLOCK, lds)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_trace_pool<0, 0>, TRACE_BLOCK, lds));
     if (e != hipSuccess) return 0;
     return blocks * (TRACE_BLOCK / 64);
 }
@@ -699,7 +714,12 @@ hipError_t launch_trace(const TraceParams &p, int count, hipStream_t s) {
         const unsigned grid = (unsigned)((waves + TRACE_BLOCK / 64 - 1) / (TRACE_BLOCK / 64));
         const bool hold = trace_hold(p);
         const size_t lds_h = lds + (hold ? (size_t)HOLD_WORDS * TRACE_BLOCK * 4 : 0);
-        if (count && hold) pm_launch((k_trace_pool<1, 1>), dim3(grid), dim3(TRACE_BLOCK), lds_h, s, p);
+        if (p.S.wide == 3) {
+            if (count && hold) pm_launch((k_trace_pool8<1, 1>), dim3(grid), dim3(TRACE_BLOCK), lds_h, s, p);
+            else if (count) pm_launch((k_trace_pool8<1, 0>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
+            else if (hold) pm_launch((k_trace_pool8<0, 1>), dim3(grid), dim3(TRACE_BLOCK), lds_h, s, p);
+            else pm_launch((k_trace_pool8<0, 0>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
+        } else if (count && hold) pm_launch((k_trace_pool<1, 1>), dim3(grid), dim3(TRACE_BLOCK), lds_h, s, p);
         else if (count) pm_launch((k_trace_pool<1, 0>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);
         else if (hold) pm_launch((k_trace_pool<0, 1>), dim3(grid), dim3(TRACE_BLOCK), lds_h, s, p);
         else pm_launch((k_trace_pool<0, 0>), dim3(grid), dim3(TRACE_BLOCK), lds, s, p);

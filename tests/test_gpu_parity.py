@@ -981,3 +981,39 @@ def test_kd_gather_reports_stack_overflow(oracle_mod, hip_mod, monkeypatch):
                     ctx.gather(p)
         finally:
             ctx.close()
+
+
+@pytest.mark.parametrize("n_tris", [20_000, 300_000])
+def test_bvh8_equals_bvh4(n_tris, oracle_mod, hip_mod, monkeypatch):
+    """The 8-wide quantized tree (PM_BVH8=1: pm_build.h collapse_bvh8 /
+    quantize_bvh8, pm_device.h traverse8 and the pooled kernel's
+    k_trace_pool8) against the 4-wide one on the same soup: eye records,
+    every photon slot and the grid render bit for bit (closest hits do not
+    depend on the tree; ties resolve to the lowest global id), and the slots
+    equal the oracle's."""
+    sc = scenes.triangle_soup(n_tris, 96, 64)
+    paths = 65_536
+    p = RenderParams.defaults(paths_per_pass=paths)
+    out = {}
+    for w in ("4", "8"):
+        monkeypatch.setenv("PM_BVH8", "1" if w == "8" else "0")
+        ctx = sc.load_into(hip_mod.Context(0))
+        try:
+            info = ctx.scene_info()
+            assert info["mode"] == "bvh-hbm"
+            node_bytes = ctx.scene_section("bvh4").nbytes // max(info["bvh_nodes"], 1)
+            assert node_bytes == (128 if w == "8" else 64), (w, node_bytes)
+            ctx.eye_pass(p)
+            recs = ctx.download_records()
+            ctx.trace_photons(p, 0, 0, paths)
+            slots = ctx.download_slots(paths * 4)
+            img, st = ctx.render(p)
+            out[w] = (recs, slots, img, info["bvh_nodes"])
+        finally:
+            ctx.close()
+    assert out["8"][3] < out["4"][3]
+    assert_bitexact(out["8"][0], out["4"][0], "eye records, 8-wide vs 4-wide")
+    assert_bitexact(out["8"][1], out["4"][1], "photon slots, 8-wide vs 4-wide")
+    assert np.array_equal(out["8"][2].view(np.uint32), out["4"][2].view(np.uint32)), "render, 8-wide vs 4-wide"
+    orc = sc.load_into(oracle_mod.Oracle())
+    assert_bitexact(out["8"][1], orc.trace_photons(p, 0, 0, paths), "photon slots, 8-wide vs oracle")
