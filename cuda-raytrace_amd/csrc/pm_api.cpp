@@ -43,6 +43,12 @@ struct DevBuf {
         if (e == hipSuccess) bytes = n;
         return e;
     }
+    /* ensure() with 50 % headroom: buffers sized by the photon grid or the
+     * valid photons of a pass, which change from pass to pass of a
+     * progressive render (the radius shrinks, the grid gains cells): a
+     * reallocation's hipFree waits for the device and left a ~250 us bubble
+     * in every C5 pass (profiles/r06/c5_realloc) */
+    hipError_t ensure_slack(size_t n) { return n <= bytes && p ? hipSuccess : ensure(n + n / 2); }
     bool external = false; /* caller-owned memory: never freed or grown here */
     void release() { if (p && !external) (void)hipFree(p); p = nullptr; bytes = 0; external = false; }
     template <class T> T *as() const { return (T *)p; }
@@ -1736,8 +1742,8 @@ int pm_trace_photons(void *ptr, const pm_render_params *p, int pass, int64_t pat
     if (fuse) {
         c->fused.r2 = grid_radius2(c, p, true, s);
         const GridDesc g = make_grid(c, p, c->fused.r2);
-        HIPCHK(c, c->d_count.ensure(((size_t)g.ncells + 1) * 4));
-        HIPCHK(c, c->d_scratch.ensure(bucket_scratch_words(end_slot, g.ncells) * 4));
+        HIPCHK(c, c->d_count.ensure_slack(((size_t)g.ncells + 1) * 4));
+        HIPCHK(c, c->d_scratch.ensure_slack(bucket_scratch_words(end_slot, g.ncells) * 4));
         HIPCHK(c, count_zeroed(c, (size_t)g.ncells + 1, s));
         T.bucket = 1;
         T.grid = g;
@@ -1806,13 +1812,13 @@ int pm_build_photon_map(void *ptr, const pm_render_params *p, int64_t n_slots, v
     /* the counting pass below reads every slot's valid bit (and overwrites the keys) */
     if (!counted && (rc = materialize_slots(c, s))) return rc;
     const size_t n = (size_t)n_slots;
-    HIPCHK(c, c->d_count.ensure(((size_t)g.ncells + 1) * 4));
-    HIPCHK(c, c->d_cell_start.ensure(((size_t)g.ncells + 1) * 4));
+    HIPCHK(c, c->d_count.ensure_slack(((size_t)g.ncells + 1) * 4));
+    HIPCHK(c, c->d_cell_start.ensure_slack(((size_t)g.ncells + 1) * 4));
     if (!counted) {
-        HIPCHK(c, c->d_scratch.ensure(bucket_scratch_words(n_slots, g.ncells) * 4));
+        HIPCHK(c, c->d_scratch.ensure_slack(bucket_scratch_words(n_slots, g.ncells) * 4));
         HIPCHK(c, count_zeroed(c, (size_t)g.ncells + 1, s));
     }
-    HIPCHK(c, c->d_pha.ensure(n * 16)); HIPCHK(c, c->d_phb.ensure(n * 32));
+    HIPCHK(c, c->d_pha.ensure_slack(n * 16)); HIPCHK(c, c->d_phb.ensure_slack(n * 32));
     timer_begin(c, "build", s);
     HIPCHK(c, launch_bucket_build(c->d_slots.as<pm_photon>(), n_slots, g, c->d_count.as<uint32_t>(),
                                   c->d_cell_start.as<uint32_t>(), c->d_scratch.as<uint32_t>(), c->d_pha.as<float4>(),
