@@ -84,6 +84,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="oracle threads (default: this process's CPU share: OMP_NUM_THREADS, else its affinity set)")
     ap.add_argument("--no-census", action="store_true")
+    ap.add_argument("--gather-event-every", type=int, default=4,
+                    help="HIP events on the gather of every N-th timed step (the roofline's launch time; 1 = every step)")
     ap.add_argument("--no-alt-exchange", action="store_true",
                     help="N > 1: skip timing the other exchange (reduce <-> allgather) after the headline steps")
     ap.add_argument("--pipeline", type=int, default=int(os.environ.get("PM_BENCH_PIPELINE", "0")),
@@ -319,11 +321,17 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         ctx.timing_reset()
-        # events only on the roofline kernel's stage inside the timed region:
-        # every timed stage boundary costs a few us of idle GPU
-        ctx.set_stage_timing("gather")
+        # events only on the roofline kernel's stage inside the timed region,
+        # and only on every --gather-event-every-th step: a timed dispatch's
+        # events leave ~4.5 us idle before and ~5 us after it (rocprofv3
+        # kernel trace, profiles/r06/event_gaps), 6 % of a C2 step
+        ev_every = max(1, args.gather_event_every)
+        sampled = 0
         t0 = time.perf_counter()
         for i in range(args.steps):
+            timed = i % ev_every == 0
+            sampled += timed
+            ctx.set_stage_timing("gather" if timed else "")
             step(ahead=i < args.steps - 1)
         runner.flush()                 # the last pass's exchange is part of the timed work
         torch.cuda.synchronize()
@@ -458,7 +466,7 @@ def main():
         tiles = np.concatenate([live, np.zeros(pad, bool)]).reshape(-1, 64)
         inactive_read = int((~tiles[tiles.any(axis=1)]).sum()) - pad * int(tiles[-1].any())
     # per-pass gather time of this rank (the all-gather mode launches once per band)
-    gather_pass_ms = gather_ms_total / args.steps if args.steps else 0.0
+    gather_pass_ms = gather_ms_total / sampled if sampled else 0.0     # the event-timed steps
     split = world > 1 and args.exchange == "reduce"
 
     roofline = None
@@ -514,6 +522,8 @@ def main():
             "avg_launch_ms": round(gather_ms, 5),
             "gather_ms_per_pass": round(gather_pass_ms, 5),
             "launches_timed": gather_launches,
+            "launches_timed_note": "HIP events on the gather of every %d-th timed step (%d of %d), on its stream" % (
+                ev_every, sampled, args.steps),
             "achieved_basis": "since round 5 the fresh-pass floor over the per-pass gather time (rounds 2-4 graded "
                               "SURVEY.md §8d's 92-B compulsory bytes, which include PPM-state reads the timed pass "
                               "does not make; round 1 priced the per-lane algorithmic bytes)",
