@@ -523,6 +523,16 @@ constexpr uint32_t SPARSE_CELLS = 20;
 #define PM_TILE_UMAX 512
 #endif
 constexpr int TILE_UMAX = PM_TILE_UMAX; /* C5 (r02 grid): no cap 2.88 ms, 2048 0.44, 1024 0.41, 512 0.43; adaptive grid (r03): 2048 0.268, 1024 0.24, 512 0.205; C2 unchanged */
+/* Dense maps (>= 2 photons per 5 cells: C5's caustic scene, 0.73; C2 0.20)
+ * fall back to the per-lane scans from smaller unions on: C5 tile gather
+ * 0.153-0.159 ms at 512, 0.145-0.148 at 256, 0.150-0.152 at 192, 0.158-0.161
+ * at 128; C2 0.5 % slower at 256, C4 unchanged (round 6, same box,
+ * profiles/r06/tile_umax). The density is read on the device, as for
+ * GROUP_MIN_SPARSE. */
+#ifndef PM_TILE_UMAX_DENSE
+#define PM_TILE_UMAX_DENSE 256
+#endif
+constexpr int TILE_UMAX_DENSE = PM_TILE_UMAX_DENSE;
 static_assert(2 * GROUP_R + 2 <= 8, "group rows exceed the 64-lane row map");
 /* the updated radii of a wave into the adaptive-grid histogram
  * (GatherParams::r2hist): one atomic per distinct bin of the wave (a tile's
@@ -715,8 +725,9 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
      * depth edge two or three, never one huge box. */
     bool pend = small;
     bool direct = R.live && R.r2 > 0.f && !small; /* lanes that scan their own cells from global memory */
-    const int group_min =
-        (uint64_t)P.cell_start[g.ncells] * SPARSE_CELLS < (uint64_t)g.ncells ? GROUP_MIN_SPARSE : GROUP_MIN;
+    const uint64_t n_map = P.cell_start[g.ncells];
+    const int group_min = n_map * SPARSE_CELLS < (uint64_t)g.ncells ? GROUP_MIN_SPARSE : GROUP_MIN;
+    const uint32_t umax = n_map * 5u >= (uint64_t)g.ncells * 2u ? (uint32_t)TILE_UMAX_DENSE : (uint32_t)TILE_UMAX;
     gp.mark(0);
     while (true) {
         const unsigned long long pm = __ballot(pend);
@@ -760,7 +771,7 @@ __global__ __launch_bounds__(TILE_BLOCK) TILE_OCC void k_gather_tile(GatherParam
         /* a dense union (many photons per cell, e.g. C5's caustic scene: 4x
          * C2's density) costs more to stage than its lanes read on their own:
          * above TILE_UMAX photons the group's lanes scan their own cells */
-        if (U > (uint32_t)TILE_UMAX) { direct = direct || mine; continue; }
+        if (U > umax) { direct = direct || mine; continue; }
         const uint32_t gofs = B - pre; /* photon index of concatenated position t in row u: t + gofs_u */
         /* this lane's rows as KR runs of the concatenation: rows (y0 .. y1, z)
          * are neighbours in the union, so each z-layer of the lane's box is
