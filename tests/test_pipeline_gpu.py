@@ -85,3 +85,13 @@ def test_pipelined_mismatched_trace_ahead_is_redone():
     seq = _run(fn, 16384, 4, False, False, 16.0)
     pip = _run(fn, 16384, 4, True, False, 16.0, hint=lambda k: k + 1 if k % 2 else k + 3)
     _same(seq, pip)
+
+
+def test_pipelined_c5_full_size_equals_sequential():
+    """bench.py runs C5 (progressive, 1,048,576 paths per pass at 1080p)
+    pipelined by default: three full-size passes, records bit for bit."""
+    from pmrender import scenes
+    fn = lambda: scenes.caustic_scene(1920, 1080)  # noqa: E731
+    seq = _run(fn, 1_048_576, 3, False, False, 4.0)
+    pip = _run(fn, 1_048_576, 3, True, False, 4.0)
+    _same(seq, pip)
